@@ -1,0 +1,210 @@
+/*
+ * sparsecholesky.h -- C-ABI of the MI355X-native supernodal sparse Cholesky.
+ *
+ * This is the drop-in boundary for the numeric path of evanwporter/SparseCholesky.
+ * The reference has no FFI: its API is header-only C++ templates
+ * (include/chol.hpp).  Each entry point below names the reference interface it
+ * replaces (file:line in the reference).  The C++ drop-in header
+ * include/sparsecholesky/chol.hpp rebuilds the reference's templates
+ * (csc_matrix, SChol, schol, chol, chol_sn, ...) on top of these calls.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  Column pointers are int64 (the reference's
+ *     int overflows past 2^31-1 nonzeros, chol.hpp:52,765); row indices int32.
+ *   - Matrices are CSC.  "A upper" means the reference's csc_matrix<T,sym::upper>
+ *     (chol.hpp:134): entries with row > col are ignored, exactly as the
+ *     reference's etree/ereach/col_count ignore them (chol.hpp:392,696,539).
+ *   - Status: 0 = OK; >0 = 1-based global (natural) column whose pivot was not
+ *     positive ("A is not positive definite.", chol.hpp:849-850; LAPACK info
+ *     style); <0 = an sc_status error code below.
+ *   - The caller owns every host array it passes; the library owns device memory.
+ *     One handle per host thread; all device work runs on the stream given at
+ *     numeric creation (or the library's own stream).
+ */
+#ifndef SPARSECHOLESKY_H
+#define SPARSECHOLESKY_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__)
+#pragma GCC visibility push(default)
+#endif
+
+#define SC_VERSION 100 /* 1.0.0 */
+
+enum sc_status {
+    SC_OK = 0,
+    SC_ERR_ARG = -1,      /* bad argument / malformed CSC */
+    SC_ERR_NOMEM = -2,    /* host allocation failed */
+    SC_ERR_HIP = -3,      /* HIP runtime error (device missing, launch failure) */
+    SC_ERR_DEVMEM = -4,   /* device allocation failed */
+    SC_ERR_STATE = -5,    /* call out of order (e.g. export before factor) */
+    SC_ERR_COMM = -6,     /* RCCL / transport error */
+    SC_ERR_NOTIMPL = -7
+};
+
+typedef struct sc_symbolic sc_symbolic;
+typedef struct sc_numeric sc_numeric;
+
+/* Analysis options.  Defaults: sc_default_options(). */
+typedef struct sc_options {
+    int32_t relax;           /* 1 = relaxed supernode amalgamation (CHOLMOD-style) */
+    int32_t nrelax[3];       /* width thresholds for amalgamation */
+    double zrelax[3];        /* zero-fraction thresholds for amalgamation */
+    int32_t small_front_max; /* fronts with m <= this run in the fused one-workgroup kernel */
+    int32_t panel_nb;        /* inner panel block (potrf/trsm width), 64 */
+    int32_t panel_nb_outer;  /* outer panel block (rank-k panel update width), 256 */
+    int32_t use_graph;       /* capture the level schedule into a hipGraph and replay it */
+    int32_t reserved[8];
+} sc_options;
+
+/* Symbolic statistics (host analysis). */
+typedef struct sc_symbolic_stats {
+    int64_t n;
+    int64_t nnz_A;            /* stored upper entries used */
+    int64_t nnz_L;            /* sum of column counts (reference L pattern) */
+    double flops;             /* F = sum_j colcount[j]^2 */
+    int64_t etree_depth;
+    int64_t n_fundamental;    /* supernodes by the reference rule, in postorder */
+    int64_t n_supernodes;     /* after relaxed amalgamation */
+    int64_t n_levels;         /* assembly-tree height + 1 */
+    int64_t max_front_m;
+    int64_t max_front_w;
+    int64_t panel_entries;    /* sum m*w (L storage incl. relaxed zeros) */
+    int64_t cb_entries;       /* sum (m-w)^2 (contribution-block storage) */
+    double flops_executed;    /* dense flops the fronts actually execute */
+    double flops_syrk_w256;   /* SYRK flops mb*(mb+1)*w of fronts with w >= 256 */
+    int64_t n_small_fronts;
+    int64_t n_large_fronts;
+} sc_symbolic_stats;
+
+/* Version / status text. */
+int32_t sc_version(void);
+const char* sc_status_string(int64_t status);
+void sc_default_options(sc_options* opt);
+
+/* ---------------- host symbolic analysis ----------------
+ * Replaces: schol(A)            chol.hpp:873-946  (pattern of L)
+ *           etree/post_order/col_count inside chol() and schol()
+ *           compute_supernodes / atree / compute_levels  src/chol.cpp:7-136
+ * The supernode partition used numerically is the reference rule
+ * (src/chol.cpp:75-85) applied in etree postorder, plus relaxed amalgamation.
+ */
+int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,
+                   sc_symbolic** out);
+int64_t sc_symbolic_get_stats(const sc_symbolic* sym, sc_symbolic_stats* stats);
+int64_t sc_nnz_L(const sc_symbolic* sym);
+double sc_flops(const sc_symbolic* sym);
+/* Pattern of L in the reference layout (schol(A).p()/i(), chol.hpp:873-946):
+ * Lp[n+1], Li[nnz_L]; lower, diagonal first, rows ascending. */
+int64_t sc_symbolic_pattern(const sc_symbolic* sym, int64_t* Lp, int32_t* Li);
+/* etree parent (chol.hpp:377) and postorder (chol.hpp:466), natural numbering. */
+int64_t sc_symbolic_etree(const sc_symbolic* sym, int32_t* parent, int32_t* post);
+void sc_free_symbolic(sc_symbolic* sym);
+
+/* ---------------- device numeric factorization ----------------
+ * Replaces: chol(A)     chol.hpp:749-863  (simplicial, the parity oracle)
+ *           chol_sn(A)  chol.hpp:1406-1446 (supernodal: dpotrf_ 1263,
+ *                       cblas_dtrsm 1292, cblas_dsyrk 1322, apply_update 1196)
+ * sc_numeric_create allocates the device pools for L panels and contribution
+ * blocks on HIP device `device` (-1 = current) and builds the level schedule.
+ */
+int64_t sc_numeric_create(const sc_symbolic* sym, int32_t device, sc_numeric** out);
+/* Factor with host values Ax[nnz(A)] (same order as Ai).  Includes H2D copy. */
+int64_t sc_factor(sc_numeric* num, const double* Ax);
+/* Factor with device-resident values d_Ax (HBM).  Asynchronous on the library
+ * stream unless sync != 0; sc_numeric_status() syncs and returns the status. */
+int64_t sc_factor_device(sc_numeric* num, const double* d_Ax, int32_t sync);
+int64_t sc_numeric_status(sc_numeric* num);
+/* Export L in the reference CSC layout (chol() output, chol.hpp:749-863):
+ * Lp[n+1], Li[nnz_L], Lx[nnz_L]; any of the three may be NULL. */
+int64_t sc_export_L(sc_numeric* num, int64_t* Lp, int32_t* Li, double* Lx);
+/* Device pointer of the library stream (hipStream_t) for event timing. */
+void* sc_numeric_stream(sc_numeric* num);
+/* Per-phase timing of the last factorization, milliseconds (HIP events):
+ * t[0]=total, t[1]=scatter, t[2]=small fronts, t[3]=assembly, t[4]=potrf,
+ * t[5]=trsm, t[6]=panel update, t[7]=CB syrk.  Enabled by sc_numeric_set_profile. */
+int64_t sc_numeric_set_profile(sc_numeric* num, int32_t on);
+int64_t sc_numeric_timing(sc_numeric* num, double* t, int32_t nt);
+/* SYRK flops and kernel time (ms) of the last factorization restricted to
+ * fronts with w >= wmin (north-star gate: wmin = 256). */
+int64_t sc_numeric_syrk_stats(sc_numeric* num, int32_t wmin, double* flops, double* ms,
+                              int64_t* launches);
+void sc_free_numeric(sc_numeric* num);
+
+/* Solve A x = b with the factor (forward/back substitution on the host,
+ * natural order).  Not in the reference; used for residual checks. */
+int64_t sc_solve_host(sc_numeric* num, const double* b, double* x);
+
+/* ---------------- reference-API helpers (host) ----------------
+ * Each mirrors one reference function, with int64 column pointers. */
+/* etree(A)  chol.hpp:377-410 */
+int64_t sc_etree(int64_t n, const int64_t* Ap, const int32_t* Ai, int32_t* parent);
+/* post_order(parent)  chol.hpp:466-499 */
+int64_t sc_post_order(int64_t n, const int32_t* parent, int32_t* post);
+/* col_count(A, parent, post)  chol.hpp:567-622 */
+int64_t sc_col_count(int64_t n, const int64_t* Ap, const int32_t* Ai, const int32_t* parent,
+                     const int32_t* post, int64_t* colcount);
+/* ereach(A, k, parent, s, w[, x])  chol.hpp:680-739; returns top. Ax/x may be NULL. */
+int64_t sc_ereach(int64_t n, const int64_t* Ap, const int32_t* Ai, const double* Ax, int64_t k,
+                  const int32_t* parent, int32_t* s, int32_t* w, double* x);
+/* compute_levels(parent)  src/chol.cpp:7-40: level_of[n] (0 = deepest level
+ * processed first) ; returns number of levels. */
+int64_t sc_compute_levels(int64_t n, const int32_t* parent, int32_t* level_of);
+/* compute_supernodes(S, supernodes)  src/chol.cpp:42-100 on the reference
+ * pattern (natural order): sn_id[n], supernodes[ns+1]; returns ns. */
+int64_t sc_compute_supernodes(int64_t n, const int32_t* parent, const int64_t* Lp,
+                              int32_t* sn_id, int64_t* supernodes);
+/* atree(S, sn_id, supernodes)  src/chol.cpp:102-136 */
+int64_t sc_atree(int64_t n, const int64_t* Lp, const int32_t* Li, const int32_t* sn_id,
+                 const int64_t* supernodes, int64_t ns, int32_t* super_parent);
+/* triplet_to_csc_matrix(ti, tj, tx, n)  chol.hpp:308-369: swaps to row<=col,
+ * sorts by (col,row), sums duplicates.  Two-phase: call with Ap only to size,
+ * then with Ai/Ax.  Returns nnz. */
+int64_t sc_triplet_to_csc(int64_t n, int64_t nt, const int32_t* ti, const int32_t* tj,
+                          const double* tx, int64_t* Ap, int32_t* Ai, double* Ax);
+/* load_matrix_market_to_csc(filename)  include/mtx_reader.hpp:16-62, with the
+ * banner honoured (symmetric / general / pattern).  Two-phase like above:
+ * first call with Ai==NULL returns n in *n and nnz; second fills. */
+int64_t sc_read_mtx(const char* path, int64_t* n, int64_t* Ap, int32_t* Ai, double* Ax);
+/* Synthetic 3D 7-point Laplacian on a k^3 grid in deterministic geometric
+ * nested-dissection order.  n=k^3, nnz=n+3k^2(k-1).
+ * Ap[n+1], Ai[nnz], Ax[nnz] (upper CSC); perm (new->old) may be NULL. */
+int64_t sc_laplacian3d(int64_t k, int32_t nd_order, int64_t* Ap, int32_t* Ai, double* Ax,
+                       int32_t* perm);
+
+/* ---------------- multi-GPU (subtree partition over RCCL) ----------------
+ * Proportional subtree-to-GPU mapping of the assembly tree; contribution
+ * blocks cross GPUs only at subtree-merge fronts. */
+int64_t sc_dist_unique_id(void* id128);
+int64_t sc_dist_owner_map(const sc_symbolic* sym, int32_t nranks, int32_t* owner_of_supernode,
+                          double* work_per_rank);
+int64_t sc_numeric_create_dist(const sc_symbolic* sym, int32_t device, int32_t rank,
+                               int32_t nranks, const void* id128, sc_numeric** out);
+/* Per-rank message schedule for tests: returns number of messages; if the
+ * arrays are non-NULL fills (level, peer, bytes, is_send) per message. */
+int64_t sc_dist_schedule(const sc_symbolic* sym, int32_t nranks, int32_t rank, int32_t* level,
+                         int32_t* peer, int64_t* bytes, int32_t* is_send, int64_t cap);
+
+/* ---------------- debug / unit-test hooks ---------------- */
+/* C[i,j] -= sum_k A[i,k] A[j,k] for i>=j over an M x N trapezoid (device
+ * pointers, column-major) through the fp64 MFMA SYRK kernel. */
+int64_t sc_debug_syrk(double* dC, int32_t ldc, const double* dA, int32_t lda, int32_t M, int32_t N,
+                      int32_t K);
+int64_t sc_device_count(void);
+/* Message of the last failing call on this thread. */
+const char* sc_last_error(void);
+
+#if defined(__GNUC__)
+#pragma GCC visibility pop
+#endif
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SPARSECHOLESKY_H */

@@ -1,0 +1,336 @@
+// extern "C" boundary (include/sparsecholesky.h).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/sparsecholesky.h"
+#include "numeric.hpp"
+#include "symbolic.hpp"
+
+namespace sc {
+i64 triplet_to_csc(i64 n, i64 nt, const i32* ti, const i32* tj, const double* tx, i64* Ap, i32* Ai,
+                   double* Ax);
+i64 read_mtx(const char* path, i64* n_out, i64* Ap, i32* Ai, double* Ax);
+i64 compute_supernodes_ref(i64 n, const i32* parent, const i64* cp, i32* sn_id, i64* supernodes);
+i64 atree_ref(i64 n, const i64* Lp, const i32* Li, const i32* sn_id, const i64* supernodes, i64 ns,
+              i32* super_parent);
+i64 laplacian3d(i64 k, int nd, i64* Ap, i32* Ai, double* Ax, i32* perm_out);
+i64 dist_owner_map(const Symbolic& S, int nranks, i32* owner, double* work);
+i64 dist_schedule(const Symbolic& S, int nranks, int rank, i32* level, i32* peer, i64* bytes, i32* is_send,
+                  i64 cap);
+i64 numeric_create_dist(const Symbolic& S, int device, int rank, int nranks, const void* id128,
+                        Numeric*& out, std::string& err);
+i64 dist_unique_id(void* id128);
+}  // namespace sc
+
+struct sc_symbolic {
+    sc::Symbolic S;
+};
+struct sc_numeric {
+    sc::Numeric* N = nullptr;
+    const sc_symbolic* sym = nullptr;
+};
+
+static thread_local std::string g_last_error;
+
+extern "C" {
+
+int32_t sc_version(void) { return SC_VERSION; }
+
+const char* sc_status_string(int64_t st) {
+    if (st > 0) return "A is not positive definite.";  // chol.hpp:850
+    switch (st) {
+        case SC_OK: return "ok";
+        case SC_ERR_ARG: return "invalid argument";
+        case SC_ERR_NOMEM: return "host allocation failed";
+        case SC_ERR_HIP: return "HIP runtime error";
+        case SC_ERR_DEVMEM: return "device allocation failed";
+        case SC_ERR_STATE: return "call out of order";
+        case SC_ERR_COMM: return "communication error";
+        case SC_ERR_NOTIMPL: return "not implemented";
+    }
+    return "unknown status";
+}
+
+const char* sc_last_error(void) { return g_last_error.c_str(); }
+
+void sc_default_options(sc_options* opt) {
+    if (!opt) return;
+    std::memset(opt, 0, sizeof(*opt));
+    opt->relax = 1;
+    opt->nrelax[0] = 4;
+    opt->nrelax[1] = 16;
+    opt->nrelax[2] = 48;
+    opt->zrelax[0] = 0.8;
+    opt->zrelax[1] = 0.1;
+    opt->zrelax[2] = 0.05;
+    opt->small_front_max = 128;
+    opt->panel_nb = 64;
+    opt->panel_nb_outer = 256;
+    opt->use_graph = 0;
+}
+
+int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,
+                   sc_symbolic** out) {
+    if (!out) return SC_ERR_ARG;
+    *out = nullptr;
+    sc_options o;
+    if (opt)
+        o = *opt;
+    else
+        sc_default_options(&o);
+    if (o.small_front_max > 128) o.small_front_max = 128;
+    if (o.small_front_max < 0) o.small_front_max = 0;
+    sc_symbolic* h = new (std::nothrow) sc_symbolic();
+    if (!h) return SC_ERR_NOMEM;
+    std::string err;
+    int64_t rc;
+    try {
+        rc = sc::analyze(n, Ap, Ai, o, h->S, err);
+    } catch (const std::bad_alloc&) {
+        rc = SC_ERR_NOMEM;
+        err = "out of host memory";
+    }
+    if (rc != SC_OK) {
+        g_last_error = err;
+        delete h;
+        return rc;
+    }
+    *out = h;
+    return SC_OK;
+}
+
+int64_t sc_symbolic_get_stats(const sc_symbolic* sym, sc_symbolic_stats* st) {
+    if (!sym || !st) return SC_ERR_ARG;
+    *st = sym->S.stats;
+    return SC_OK;
+}
+
+int64_t sc_nnz_L(const sc_symbolic* sym) { return sym ? sym->S.nnzL : SC_ERR_ARG; }
+double sc_flops(const sc_symbolic* sym) { return sym ? sym->S.flops : -1.0; }
+
+int64_t sc_symbolic_pattern(const sc_symbolic* sym, int64_t* Lp, int32_t* Li) {
+    if (!sym || !Lp) return SC_ERR_ARG;
+    sc::pattern_L(sym->S, Lp, Li);
+    return SC_OK;
+}
+
+int64_t sc_symbolic_etree(const sc_symbolic* sym, int32_t* parent, int32_t* post) {
+    if (!sym) return SC_ERR_ARG;
+    const auto& S = sym->S;
+    if (parent) std::memcpy(parent, S.parent.data(), sizeof(int32_t) * (size_t)S.n);
+    if (post) std::memcpy(post, S.post.data(), sizeof(int32_t) * (size_t)S.n);
+    return SC_OK;
+}
+
+void sc_free_symbolic(sc_symbolic* sym) { delete sym; }
+
+int64_t sc_numeric_create(const sc_symbolic* sym, int32_t device, sc_numeric** out) {
+    if (!sym || !out) return SC_ERR_ARG;
+    *out = nullptr;
+    sc_numeric* h = new (std::nothrow) sc_numeric();
+    if (!h) return SC_ERR_NOMEM;
+    std::string err;
+    int64_t rc = sc::numeric_create(sym->S, device, h->N, err);
+    if (rc != SC_OK) {
+        g_last_error = err;
+        delete h;
+        return rc;
+    }
+    h->sym = sym;
+    *out = h;
+    return SC_OK;
+}
+
+int64_t sc_factor_device(sc_numeric* num, const double* d_Ax, int32_t sync) {
+    if (!num || !num->N || (!d_Ax && num->sym->S.nnzA_in > 0)) return SC_ERR_ARG;
+    int64_t rc = sc::numeric_factor(*num->N, d_Ax, sync != 0);
+    if (rc < 0) g_last_error = num->N->err;
+    return rc;
+}
+
+int64_t sc_factor(sc_numeric* num, const double* Ax) {
+    if (!num || !num->N) return SC_ERR_ARG;
+    sc::Numeric& N = *num->N;
+    const int64_t nnz = num->sym->S.nnzA_in;
+    if (nnz > 0 && !Ax) return SC_ERR_ARG;
+    if (hipSetDevice(N.device) != hipSuccess) return SC_ERR_HIP;
+    if (!N.d_Ax_owned) {
+        if (hipMalloc(&N.d_Ax_owned, (size_t)std::max<int64_t>(nnz, 1) * sizeof(double)) != hipSuccess) {
+            N.d_Ax_owned = nullptr;
+            return SC_ERR_DEVMEM;
+        }
+    }
+    if (nnz > 0 && hipMemcpyAsync(N.d_Ax_owned, Ax, (size_t)nnz * sizeof(double), hipMemcpyHostToDevice,
+                                  N.stream) != hipSuccess)
+        return SC_ERR_HIP;
+    return sc_factor_device(num, N.d_Ax_owned, 1);
+}
+
+int64_t sc_numeric_status(sc_numeric* num) {
+    if (!num || !num->N) return SC_ERR_ARG;
+    return sc::numeric_status(*num->N);
+}
+
+int64_t sc_export_L(sc_numeric* num, int64_t* Lp, int32_t* Li, double* Lx) {
+    if (!num || !num->N) return SC_ERR_ARG;
+    try {
+        return sc::numeric_export(*num->N, Lp, Li, Lx);
+    } catch (const std::bad_alloc&) {
+        return SC_ERR_NOMEM;
+    }
+}
+
+void* sc_numeric_stream(sc_numeric* num) { return (num && num->N) ? (void*)num->N->stream : nullptr; }
+
+int64_t sc_numeric_set_profile(sc_numeric* num, int32_t on) {
+    if (!num || !num->N) return SC_ERR_ARG;
+    num->N->profile = on != 0;
+    return SC_OK;
+}
+
+int64_t sc_numeric_timing(sc_numeric* num, double* t, int32_t nt) {
+    if (!num || !num->N || !t) return SC_ERR_ARG;
+    return sc::numeric_timing(*num->N, t, nt);
+}
+
+int64_t sc_numeric_syrk_stats(sc_numeric* num, int32_t wmin, double* flops, double* ms, int64_t* launches) {
+    if (!num || !num->N) return SC_ERR_ARG;
+    return sc::numeric_syrk_stats(*num->N, wmin, flops, ms, launches);
+}
+
+void sc_free_numeric(sc_numeric* num) {
+    if (!num) return;
+    sc::numeric_free(num->N);
+    delete num;
+}
+
+int64_t sc_solve_host(sc_numeric* num, const double* b, double* x) {
+    if (!num || !num->N || !b || !x) return SC_ERR_ARG;
+    const auto& S = num->sym->S;
+    const int64_t n = S.n;
+    std::vector<int64_t> Lp((size_t)n + 1);
+    std::vector<int32_t> Li((size_t)std::max<int64_t>(S.nnzL, 1));
+    std::vector<double> Lx((size_t)std::max<int64_t>(S.nnzL, 1));
+    int64_t st = sc::numeric_export(*num->N, Lp.data(), Li.data(), Lx.data());
+    if (st != SC_OK) return st;
+    std::memmove(x, b, sizeof(double) * (size_t)n);
+    for (int64_t j = 0; j < n; ++j) {  // L y = b
+        x[j] /= Lx[Lp[j]];
+        for (int64_t p = Lp[j] + 1; p < Lp[j + 1]; ++p) x[Li[p]] -= Lx[p] * x[j];
+    }
+    for (int64_t j = n - 1; j >= 0; --j) {  // L^T x = y
+        for (int64_t p = Lp[j] + 1; p < Lp[j + 1]; ++p) x[j] -= Lx[p] * x[Li[p]];
+        x[j] /= Lx[Lp[j]];
+    }
+    return SC_OK;
+}
+
+// ---- reference-API helpers ----
+int64_t sc_etree(int64_t n, const int64_t* Ap, const int32_t* Ai, int32_t* parent) {
+    if (n < 0 || !Ap || !parent) return SC_ERR_ARG;
+    sc::etree(n, Ap, Ai, parent);
+    return SC_OK;
+}
+
+int64_t sc_post_order(int64_t n, const int32_t* parent, int32_t* post) {
+    if (n < 0 || !parent || !post) return SC_ERR_ARG;
+    sc::post_order(n, parent, post);
+    return SC_OK;
+}
+
+int64_t sc_col_count(int64_t n, const int64_t* Ap, const int32_t* Ai, const int32_t* parent,
+                     const int32_t* post, int64_t* colcount) {
+    if (n < 0 || !Ap || !parent || !post || !colcount) return SC_ERR_ARG;
+    sc::col_count(n, Ap, Ai, parent, post, colcount);
+    return SC_OK;
+}
+
+int64_t sc_ereach(int64_t n, const int64_t* Ap, const int32_t* Ai, const double* Ax, int64_t k,
+                  const int32_t* parent, int32_t* s, int32_t* w, double* x) {
+    if (n < 0 || k < 0 || k >= n || !Ap || !parent || !s || !w) return SC_ERR_ARG;
+    std::vector<int32_t> path((size_t)n);
+    return sc::ereach(n, Ap, Ai, Ax, k, parent, s, w, x, path);
+}
+
+int64_t sc_compute_levels(int64_t n, const int32_t* parent, int32_t* level_of) {
+    if (n < 0 || !parent) return SC_ERR_ARG;
+    return sc::compute_levels(n, parent, level_of);
+}
+
+int64_t sc_compute_supernodes(int64_t n, const int32_t* parent, const int64_t* Lp, int32_t* sn_id,
+                              int64_t* supernodes) {
+    if (n < 0 || !parent || !Lp) return SC_ERR_ARG;
+    return sc::compute_supernodes_ref(n, parent, Lp, sn_id, supernodes);
+}
+
+int64_t sc_atree(int64_t n, const int64_t* Lp, const int32_t* Li, const int32_t* sn_id,
+                 const int64_t* supernodes, int64_t ns, int32_t* super_parent) {
+    if (n < 0 || !Lp || !Li || !sn_id || !supernodes || !super_parent) return SC_ERR_ARG;
+    return sc::atree_ref(n, Lp, Li, sn_id, supernodes, ns, super_parent);
+}
+
+int64_t sc_triplet_to_csc(int64_t n, int64_t nt, const int32_t* ti, const int32_t* tj, const double* tx,
+                          int64_t* Ap, int32_t* Ai, double* Ax) {
+    if (n < 0 || nt < 0 || (nt > 0 && (!ti || !tj))) return SC_ERR_ARG;
+    return sc::triplet_to_csc(n, nt, ti, tj, tx, Ap, Ai, Ax);
+}
+
+int64_t sc_read_mtx(const char* path, int64_t* n, int64_t* Ap, int32_t* Ai, double* Ax) {
+    if (!path || !n) return SC_ERR_ARG;
+    return sc::read_mtx(path, n, Ap, Ai, Ax);
+}
+
+int64_t sc_laplacian3d(int64_t k, int32_t nd_order, int64_t* Ap, int32_t* Ai, double* Ax, int32_t* perm) {
+    return sc::laplacian3d(k, nd_order, Ap, Ai, Ax, perm);
+}
+
+// ---- multi-GPU ----
+int64_t sc_dist_unique_id(void* id128) { return sc::dist_unique_id(id128); }
+
+int64_t sc_dist_owner_map(const sc_symbolic* sym, int32_t nranks, int32_t* owner, double* work) {
+    if (!sym || nranks <= 0) return SC_ERR_ARG;
+    return sc::dist_owner_map(sym->S, nranks, owner, work);
+}
+
+int64_t sc_dist_schedule(const sc_symbolic* sym, int32_t nranks, int32_t rank, int32_t* level, int32_t* peer,
+                         int64_t* bytes, int32_t* is_send, int64_t cap) {
+    if (!sym || nranks <= 0 || rank < 0 || rank >= nranks) return SC_ERR_ARG;
+    return sc::dist_schedule(sym->S, nranks, rank, level, peer, bytes, is_send, cap);
+}
+
+int64_t sc_numeric_create_dist(const sc_symbolic* sym, int32_t device, int32_t rank, int32_t nranks,
+                               const void* id128, sc_numeric** out) {
+    if (!sym || !out || nranks <= 0 || rank < 0 || rank >= nranks) return SC_ERR_ARG;
+    *out = nullptr;
+    sc_numeric* h = new (std::nothrow) sc_numeric();
+    if (!h) return SC_ERR_NOMEM;
+    std::string err;
+    int64_t rc = sc::numeric_create_dist(sym->S, device, rank, nranks, id128, h->N, err);
+    if (rc != SC_OK) {
+        g_last_error = err;
+        delete h;
+        return rc;
+    }
+    h->sym = sym;
+    *out = h;
+    return SC_OK;
+}
+
+// ---- debug hooks ----
+int64_t sc_debug_syrk(double* dC, int32_t ldc, const double* dA, int32_t lda, int32_t M, int32_t N,
+                      int32_t K) {
+    if (!dC || !dA || M < 0 || N < 0 || K < 0 || N > M) return SC_ERR_ARG;
+    return sc::debug_syrk(dC, ldc, dA, lda, M, N, K);
+}
+
+int64_t sc_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+}  // extern "C"

@@ -1,0 +1,65 @@
+// Device-side plan layout and kernel launch wrappers (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace sc {
+
+// Inner panel width (POTRF/TRSM block); the diagonal block lives in LDS.
+constexpr int PNB = 64;
+// Rows per TRSM workgroup.
+constexpr int TRSM_ROWS = 64;
+// Columns owned by one assembly workgroup.
+constexpr int ASM_COLS = 64;
+// Output tile edge of the MFMA SYRK kernel.
+constexpr int SYRK_BT = 64;
+
+// C/D register map of v_mfma_f64_16x16x4_f64 on gfx950 (cdna_hip_programming.md
+// section 3): col = lane & 15, row = (lane >> 4) + 4 * reg.
+#define MFMA_F64_ROW(lane, r) (((lane) >> 4) + 4 * (r))
+
+// All device arrays of the numeric plan (internal numbering).
+struct DevPlan {
+    const int32_t* sn_start;    // ns+1
+    const int32_t* sn_m;        // ns
+    const int64_t* panel_off;   // ns+1
+    const int64_t* cb_off;      // ns+1
+    const int32_t* child_ptr;   // ns+1
+    const int32_t* child_list;
+    const int64_t* rel_ptr;     // ns+1
+    const int32_t* relind;
+    const int64_t* a_ptr;       // n+1 (internal columns)
+    const int32_t* a_pos;       // row position in the column's front
+    const int64_t* a_src;       // index into the input value array
+    double* panel_pool;
+    double* cb_pool;
+    int32_t* info;              // min failing internal column + 1
+};
+
+// One lower-trapezoid SYRK update: C[i,j] -= sum_k A[i,k] A[j,k], j < N, j <= i < M.
+struct GemmTask {
+    double* C;
+    const double* A;
+    int64_t ldc;
+    int64_t lda;
+    int32_t M, N, K;
+    int32_t tile_base;  // first tile index of this task within its launch
+};
+
+hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count, int maxm, const double* Ax,
+                              hipStream_t st);
+hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count, const double* Ax,
+                                 hipStream_t st);
+hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hipStream_t st);
+hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st);
+hipError_t launch_syrk(const GemmTask* tasks, int ntasks, int total_tiles, hipStream_t st);
+
+// tiles of an M x N lower trapezoid with square BT tiles
+inline int64_t syrk_tiles(int64_t M, int64_t N, int bt) {
+    const int64_t TM = (M + bt - 1) / bt, TN = (N + bt - 1) / bt;
+    return TN * TM - TN * (TN - 1) / 2;
+}
+
+}  // namespace sc

@@ -1,0 +1,475 @@
+// Device numeric factorization driver.
+//
+// Layout in HBM (one allocation each, doubles):
+//   panel pool  sum_s m_s*w_s      L panels, column-major, ld = m_s (the output)
+//   CB pool     sum_s (m_s-w_s)^2  contribution blocks, column-major, ld = mb_s
+// Schedule: assembly-tree levels, leaves first.  Per level:
+//   small fronts (m <= small_front_max): one fused kernel per LDS size bucket;
+//   large fronts: assemble, then per 64-column step potrf -> trsm -> panel
+//   SYRK update (inner 64-wide within a 256-wide slab, outer at slab ends),
+//   then one CB SYRK with K = w (the north-star MFMA kernel).
+#include "numeric.hpp"
+
+#include <algorithm>
+#include <climits>
+#include <cstring>
+
+namespace sc {
+
+#define HIP_TRY(x)                                                                \
+    do {                                                                          \
+        hipError_t e_ = (x);                                                      \
+        if (e_ != hipSuccess) {                                                   \
+            N.err = std::string(#x) + ": " + hipGetErrorString(e_);               \
+            return SC_ERR_HIP;                                                    \
+        }                                                                         \
+    } while (0)
+
+template <class T>
+static int64_t upload(Numeric& N, const std::vector<T>& v, T*& dptr) {
+    dptr = nullptr;
+    size_t bytes = std::max<size_t>(v.size(), 1) * sizeof(T);
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) {
+        N.err = std::string("hipMalloc(plan): ") + hipGetErrorString(e);
+        return SC_ERR_DEVMEM;
+    }
+    N.allocs.push_back(p);
+    if (!v.empty()) {
+        e = hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            N.err = std::string("hipMemcpy(plan): ") + hipGetErrorString(e);
+            return SC_ERR_HIP;
+        }
+    }
+    dptr = (T*)p;
+    return SC_OK;
+}
+
+static int64_t dalloc(Numeric& N, size_t bytes, void*& p) {
+    p = nullptr;
+    hipError_t e = hipMalloc(&p, std::max<size_t>(bytes, 8));
+    if (e != hipSuccess) {
+        N.err = std::string("hipMalloc(pool ") + std::to_string(bytes) + " B): " + hipGetErrorString(e);
+        return SC_ERR_DEVMEM;
+    }
+    N.allocs.push_back(p);
+    return SC_OK;
+}
+
+#define TRY(x)                        \
+    do {                              \
+        int64_t r_ = (x);             \
+        if (r_ != SC_OK) return r_;   \
+    } while (0)
+
+static int bucket_of(int m) {
+    if (m <= 32) return 32;
+    if (m <= 64) return 64;
+    if (m <= 96) return 96;
+    return 128;
+}
+
+// Build the static launch schedule (host).  Task pointers into the pools are
+// final device addresses, so the schedule can be replayed or graph-captured.
+static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vector<int2>& asmv,
+                              std::vector<int2>& potrf, std::vector<int4>& trsm,
+                              std::vector<GemmTask>& gemm) {
+    const Symbolic& S = *N.S;
+    const int NBO = std::max(PNB, (S.opt.panel_nb_outer / PNB) * PNB);
+    std::vector<std::vector<int32_t>> by_level((size_t)S.nlevels);
+    for (int32_t s = 0; s < S.ns; ++s) by_level[S.level[s]].push_back(s);
+    double* panel_pool = N.P.panel_pool;
+    double* cb_pool = N.P.cb_pool;
+    auto push_gemm_launch = [&](int kind, int level, const std::vector<GemmTask>& tasks, int big,
+                                double flops) {
+        if (tasks.empty()) return;
+        Launch L {};
+        L.kind = kind;
+        L.level = level;
+        L.off = (int64_t)gemm.size();
+        int64_t tiles = 0;
+        for (auto t : tasks) {
+            t.tile_base = (int32_t)tiles;
+            tiles += syrk_tiles(t.M, t.N, SYRK_BT);
+            gemm.push_back(t);
+        }
+        L.count = (int32_t)tiles;
+        L.ntasks = (int32_t)tasks.size();
+        L.big = big;
+        L.flops = flops;
+        N.sched.push_back(L);
+    };
+    for (int32_t lev = 0; lev < S.nlevels; ++lev) {
+        const auto& nodes = by_level[lev];
+        // small fronts by LDS bucket
+        for (int b : {32, 64, 96, 128}) {
+            Launch L {};
+            L.kind = L_SMALL;
+            L.level = lev;
+            L.off = (int64_t)small.size();
+            L.maxm = b;
+            for (int32_t s : nodes)
+                if (S.fclass[s] == FRONT_SMALL && bucket_of(S.sn_m[s]) == b) small.push_back(s);
+            L.count = (int32_t)((int64_t)small.size() - L.off);
+            if (L.count > 0) N.sched.push_back(L);
+        }
+        std::vector<int32_t> large;
+        for (int32_t s : nodes)
+            if (S.fclass[s] == FRONT_LARGE) large.push_back(s);
+        if (large.empty()) continue;
+        {
+            Launch L {};
+            L.kind = L_ASM;
+            L.level = lev;
+            L.off = (int64_t)asmv.size();
+            for (int32_t s : large) {
+                const int m = S.sn_m[s];
+                for (int cb = 0; cb * ASM_COLS < m; ++cb) asmv.push_back(make_int2(s, cb));
+            }
+            L.count = (int32_t)((int64_t)asmv.size() - L.off);
+            N.sched.push_back(L);
+        }
+        int maxw = 0;
+        for (int32_t s : large) maxw = std::max(maxw, S.w(s));
+        for (int k0 = 0; k0 < maxw; k0 += PNB) {
+            Launch Lp {};
+            Lp.kind = L_POTRF;
+            Lp.level = lev;
+            Lp.off = (int64_t)potrf.size();
+            Launch Lt {};
+            Lt.kind = L_TRSM;
+            Lt.level = lev;
+            Lt.off = (int64_t)trsm.size();
+            std::vector<GemmTask> upd;
+            double uflops = 0.0;
+            for (int32_t s : large) {
+                const int w = S.w(s), m = S.sn_m[s];
+                if (w <= k0) continue;
+                const int nb = std::min(PNB, w - k0);
+                const int k1 = k0 + nb;
+                potrf.push_back(make_int2(s, k0));
+                for (int r0 = k1; r0 < m; r0 += TRSM_ROWS) trsm.push_back(make_int4(s, k0, r0, 0));
+                double* pan = panel_pool + S.panel_off[s];
+                const int slab0 = (k0 / NBO) * NBO;
+                const int slab1 = std::min(w, slab0 + NBO);
+                if (k1 < slab1) {
+                    GemmTask t {};
+                    t.C = pan + (int64_t)k1 * m + k1;
+                    t.A = pan + (int64_t)k0 * m + k1;
+                    t.ldc = m;
+                    t.lda = m;
+                    t.M = m - k1;
+                    t.N = slab1 - k1;
+                    t.K = k1 - k0;
+                    upd.push_back(t);
+                    uflops += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
+                } else if (k1 == slab1 && slab1 < w) {
+                    GemmTask t {};
+                    t.C = pan + (int64_t)slab1 * m + slab1;
+                    t.A = pan + (int64_t)slab0 * m + slab1;
+                    t.ldc = m;
+                    t.lda = m;
+                    t.M = m - slab1;
+                    t.N = w - slab1;
+                    t.K = slab1 - slab0;
+                    upd.push_back(t);
+                    uflops += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
+                }
+            }
+            Lp.count = (int32_t)((int64_t)potrf.size() - Lp.off);
+            Lt.count = (int32_t)((int64_t)trsm.size() - Lt.off);
+            if (Lp.count > 0) N.sched.push_back(Lp);
+            if (Lt.count > 0) N.sched.push_back(Lt);
+            push_gemm_launch(L_PANEL, lev, upd, 0, uflops);
+        }
+        // contribution-block SYRK, K = w; fronts with w >= 256 in their own launch
+        for (int big = 1; big >= 0; --big) {
+            std::vector<GemmTask> cbt;
+            double fl = 0.0;
+            for (int32_t s : large) {
+                const int w = S.w(s), m = S.sn_m[s], mb = m - w;
+                if (mb <= 0 || (w >= 256) != (big == 1)) continue;
+                GemmTask t {};
+                t.C = cb_pool + S.cb_off[s];
+                t.A = panel_pool + S.panel_off[s] + w;
+                t.ldc = mb;
+                t.lda = m;
+                t.M = mb;
+                t.N = mb;
+                t.K = w;
+                cbt.push_back(t);
+                fl += (double)mb * (mb + 1.0) * w;
+            }
+            push_gemm_launch(L_CB, lev, cbt, big, fl);
+        }
+    }
+    return SC_OK;
+}
+
+int64_t numeric_create(const Symbolic& S, int device, Numeric*& out, std::string& err) {
+    out = nullptr;
+    Numeric* Np = new (std::nothrow) Numeric();
+    if (!Np) return SC_ERR_NOMEM;
+    Numeric& N = *Np;
+    N.S = &S;
+    auto fail = [&](int64_t rc) {
+        err = N.err;
+        numeric_free(Np);
+        return rc;
+    };
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        N.err = "no HIP device available";
+        return fail(SC_ERR_HIP);
+    }
+    if (device < 0) {
+        if (hipGetDevice(&device) != hipSuccess) device = 0;
+    }
+    if (device >= ndev) {
+        N.err = "device index out of range";
+        return fail(SC_ERR_ARG);
+    }
+    N.device = device;
+    if (hipSetDevice(device) != hipSuccess) {
+        N.err = "hipSetDevice failed";
+        return fail(SC_ERR_HIP);
+    }
+    if (hipStreamCreateWithFlags(&N.stream, hipStreamNonBlocking) != hipSuccess) {
+        N.err = "hipStreamCreate failed";
+        return fail(SC_ERR_HIP);
+    }
+    N.use_graph = S.opt.use_graph != 0;
+    const int32_t ns = S.ns;
+    int64_t rc;
+    DevPlan& P = N.P;
+    int32_t *d_sn_start, *d_sn_m, *d_child_ptr, *d_child_list, *d_relind, *d_apos;
+    int64_t *d_panel_off, *d_cb_off, *d_rel_ptr, *d_aptr, *d_asrc;
+    if ((rc = upload(N, S.sn_start, d_sn_start)) || (rc = upload(N, S.sn_m, d_sn_m)) ||
+        (rc = upload(N, S.panel_off, d_panel_off)) || (rc = upload(N, S.cb_off, d_cb_off)) ||
+        (rc = upload(N, S.child_ptr, d_child_ptr)) || (rc = upload(N, S.child_list, d_child_list)) ||
+        (rc = upload(N, S.rel_ptr, d_rel_ptr)) || (rc = upload(N, S.relind, d_relind)) ||
+        (rc = upload(N, S.a_ptr, d_aptr)) || (rc = upload(N, S.a_pos, d_apos)) ||
+        (rc = upload(N, S.a_src, d_asrc)))
+        return fail(rc);
+    P.sn_start = d_sn_start;
+    P.sn_m = d_sn_m;
+    P.panel_off = d_panel_off;
+    P.cb_off = d_cb_off;
+    P.child_ptr = d_child_ptr;
+    P.child_list = d_child_list;
+    P.rel_ptr = d_rel_ptr;
+    P.relind = d_relind;
+    P.a_ptr = d_aptr;
+    P.a_pos = d_apos;
+    P.a_src = d_asrc;
+    void* p = nullptr;
+    if ((rc = dalloc(N, (size_t)S.panel_off[ns] * sizeof(double), p))) return fail(rc);
+    P.panel_pool = (double*)p;
+    if ((rc = dalloc(N, (size_t)S.cb_off[ns] * sizeof(double), p))) return fail(rc);
+    P.cb_pool = (double*)p;
+    if ((rc = dalloc(N, 64, p))) return fail(rc);
+    P.info = (int32_t*)p;
+
+    std::vector<int32_t> small;
+    std::vector<int2> asmv, potrf;
+    std::vector<int4> trsm;
+    std::vector<GemmTask> gemm;
+    if ((rc = build_schedule(N, small, asmv, potrf, trsm, gemm))) return fail(rc);
+    if ((rc = upload(N, small, N.d_small)) || (rc = upload(N, asmv, N.d_asm)) ||
+        (rc = upload(N, potrf, N.d_potrf)) || (rc = upload(N, trsm, N.d_trsm)) ||
+        (rc = upload(N, gemm, N.d_gemm)))
+        return fail(rc);
+    out = Np;
+    return SC_OK;
+}
+
+static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
+    switch (L.kind) {
+        case L_SMALL:
+            return launch_front_small(N.P, N.d_small + L.off, L.count, L.maxm, d_Ax, N.stream);
+        case L_ASM:
+            return launch_assemble_large(N.P, N.d_asm + L.off, L.count, d_Ax, N.stream);
+        case L_POTRF:
+            return launch_potrf_diag(N.P, N.d_potrf + L.off, L.count, N.stream);
+        case L_TRSM:
+            return launch_trsm_panel(N.P, N.d_trsm + L.off, L.count, N.stream);
+        case L_PANEL:
+        case L_CB:
+            return launch_syrk(N.d_gemm + L.off, L.ntasks, L.count, N.stream);
+    }
+    return hipErrorInvalidValue;
+}
+
+static int64_t enqueue_all(Numeric& N, const double* d_Ax, bool with_events) {
+    HIP_TRY(hipMemsetAsync(N.P.info, 0x7f, sizeof(int32_t), N.stream));
+    for (size_t i = 0; i < N.sched.size(); ++i) {
+        if (with_events) HIP_TRY(hipEventRecord(N.ev[2 * i], N.stream));
+        HIP_TRY(launch_one(N, N.sched[i], d_Ax));
+        if (with_events) HIP_TRY(hipEventRecord(N.ev[2 * i + 1], N.stream));
+    }
+    return SC_OK;
+}
+
+int64_t numeric_factor(Numeric& N, const double* d_Ax, bool sync) {
+    HIP_TRY(hipSetDevice(N.device));
+    N.status_valid = false;
+    N.last_Ax = d_Ax;
+    if (N.profile) {
+        if (N.ev.size() != 2 * N.sched.size()) {
+            for (auto e : N.ev) (void)hipEventDestroy(e);
+            N.ev.assign(2 * N.sched.size(), nullptr);
+            for (auto& e : N.ev) HIP_TRY(hipEventCreate(&e));
+        }
+        TRY(enqueue_all(N, d_Ax, true));
+    } else if (N.use_graph) {
+        if (!N.gexec || N.graph_Ax != d_Ax) {
+            if (N.gexec) {
+                (void)hipGraphExecDestroy(N.gexec);
+                N.gexec = nullptr;
+            }
+            if (N.graph) {
+                (void)hipGraphDestroy(N.graph);
+                N.graph = nullptr;
+            }
+            HIP_TRY(hipStreamBeginCapture(N.stream, hipStreamCaptureModeThreadLocal));
+            int64_t rc = enqueue_all(N, d_Ax, false);
+            hipGraph_t g = nullptr;
+            hipError_t e2 = hipStreamEndCapture(N.stream, &g);
+            if (rc != SC_OK) return rc;
+            HIP_TRY(e2);
+            N.graph = g;
+            HIP_TRY(hipGraphInstantiate(&N.gexec, N.graph, nullptr, nullptr, 0));
+            N.graph_Ax = d_Ax;
+        }
+        HIP_TRY(hipGraphLaunch(N.gexec, N.stream));
+    } else {
+        TRY(enqueue_all(N, d_Ax, false));
+    }
+    N.factored = true;
+    if (sync) return numeric_status(N);
+    return SC_OK;
+}
+
+int64_t numeric_status(Numeric& N) {
+    if (!N.factored) return SC_ERR_STATE;
+    if (N.status_valid) return N.status;
+    HIP_TRY(hipSetDevice(N.device));
+    HIP_TRY(hipStreamSynchronize(N.stream));
+    int32_t info = 0;
+    HIP_TRY(hipMemcpy(&info, N.P.info, sizeof(info), hipMemcpyDeviceToHost));
+    if (info == 0x7f7f7f7f || info <= 0)
+        N.status = 0;
+    else
+        N.status = (int64_t)N.S->post[info - 1] + 1;
+    N.status_valid = true;
+    if (N.profile) {
+        std::memset(N.phase_ms, 0, sizeof(N.phase_ms));
+        hipEvent_t first = nullptr, last = nullptr;
+        for (size_t i = 0; i < N.sched.size(); ++i) {
+            float ms = 0.f;
+            HIP_TRY(hipEventElapsedTime(&ms, N.ev[2 * i], N.ev[2 * i + 1]));
+            int slot = 0;
+            switch (N.sched[i].kind) {
+                case L_SMALL: slot = 2; break;
+                case L_ASM: slot = 3; break;
+                case L_POTRF: slot = 4; break;
+                case L_TRSM: slot = 5; break;
+                case L_PANEL: slot = 6; break;
+                case L_CB: slot = 7; break;
+            }
+            N.phase_ms[slot] += ms;
+            if (!first) first = N.ev[2 * i];
+            last = N.ev[2 * i + 1];
+        }
+        if (first) {
+            float tot = 0.f;
+            HIP_TRY(hipEventElapsedTime(&tot, first, last));
+            N.phase_ms[0] = tot;
+        }
+    }
+    return N.status;
+}
+
+int64_t numeric_timing(Numeric& N, double* t, int nt) {
+    if (!N.profile || !N.status_valid) return SC_ERR_STATE;
+    for (int i = 0; i < nt && i < 8; ++i) t[i] = N.phase_ms[i];
+    return SC_OK;
+}
+
+int64_t numeric_syrk_stats(Numeric& N, int wmin, double* flops, double* ms, int64_t* launches) {
+    // CB SYRK launches are split by w >= 256; wmin selects them (wmin <= 0: all CB launches)
+    double fl = 0.0, t = 0.0;
+    int64_t cnt = 0;
+    const bool have_t = N.profile && N.status_valid && N.ev.size() == 2 * N.sched.size();
+    for (size_t i = 0; i < N.sched.size(); ++i) {
+        const Launch& L = N.sched[i];
+        if (L.kind != L_CB) continue;
+        if (wmin >= 256 && !L.big) continue;
+        fl += L.flops;
+        ++cnt;
+        if (have_t) {
+            float e = 0.f;
+            if (hipEventElapsedTime(&e, N.ev[2 * i], N.ev[2 * i + 1]) == hipSuccess) t += e;
+        }
+    }
+    if (flops) *flops = fl;
+    if (ms) *ms = have_t ? t : -1.0;
+    if (launches) *launches = cnt;
+    return SC_OK;
+}
+
+int64_t numeric_export(Numeric& N, int64_t* Lp, int32_t* Li, double* Lx) {
+    if (!N.factored) return SC_ERR_STATE;
+    int64_t st = numeric_status(N);
+    if (st < 0) return st;
+    const Symbolic& S = *N.S;
+    std::vector<double> host;
+    if (Lx) {
+        host.resize((size_t)std::max<int64_t>(S.panel_off[S.ns], 1));
+        HIP_TRY(hipMemcpy(host.data(), N.P.panel_pool, (size_t)S.panel_off[S.ns] * sizeof(double),
+                          hipMemcpyDeviceToHost));
+    }
+    export_L(S, Lx ? host.data() : nullptr, Lp, Li, Lx);
+    return st;
+}
+
+void numeric_free(Numeric* Np) {
+    if (!Np) return;
+    Numeric& N = *Np;
+    (void)hipSetDevice(N.device);
+    if (N.stream) (void)hipStreamSynchronize(N.stream);
+    if (N.gexec) (void)hipGraphExecDestroy(N.gexec);
+    if (N.graph) (void)hipGraphDestroy(N.graph);
+    for (auto e : N.ev)
+        if (e) (void)hipEventDestroy(e);
+    for (void* p : N.allocs) (void)hipFree(p);
+    if (N.d_Ax_owned) (void)hipFree(N.d_Ax_owned);
+    if (N.stream) (void)hipStreamDestroy(N.stream);
+    delete Np;
+}
+
+int64_t debug_syrk(double* dC, int ldc, const double* dA, int lda, int M, int Nn, int K) {
+    GemmTask t {};
+    t.C = dC;
+    t.A = dA;
+    t.ldc = ldc;
+    t.lda = lda;
+    t.M = M;
+    t.N = Nn;
+    t.K = K;
+    t.tile_base = 0;
+    GemmTask* d = nullptr;
+    if (hipMalloc(&d, sizeof(GemmTask)) != hipSuccess) return SC_ERR_DEVMEM;
+    if (hipMemcpy(d, &t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return SC_ERR_HIP;
+    }
+    hipError_t e = launch_syrk(d, 1, (int)syrk_tiles(M, Nn, SYRK_BT), nullptr);
+    hipError_t e2 = hipDeviceSynchronize();
+    (void)hipFree(d);
+    return (e == hipSuccess && e2 == hipSuccess) ? SC_OK : SC_ERR_HIP;
+}
+
+}  // namespace sc

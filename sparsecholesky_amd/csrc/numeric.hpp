@@ -1,0 +1,79 @@
+// Device numeric factorization driver: pools, level schedule, launches, export.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "kernels.hpp"
+#include "symbolic.hpp"
+
+namespace sc {
+
+enum LaunchKind : int32_t {
+    L_SMALL = 0,
+    L_ASM = 1,
+    L_POTRF = 2,
+    L_TRSM = 3,
+    L_PANEL = 4,
+    L_CB = 5,
+    L_KINDS = 6
+};
+
+struct Launch {
+    int32_t kind;
+    int32_t level;
+    int64_t off;      // first task in the kind's task array
+    int32_t count;    // grid size (tiles for SYRK launches)
+    int32_t ntasks;   // tasks (SYRK launches)
+    int32_t maxm;     // small-front LDS edge
+    int32_t big;      // CB launch covering fronts with w >= 256
+    double flops;     // algorithmic SYRK flops (CB launches: mb*(mb+1)*w)
+};
+
+struct Numeric {
+    const Symbolic* S = nullptr;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevPlan P {};
+    std::vector<void*> allocs;
+    std::vector<Launch> sched;
+    int32_t* d_small = nullptr;
+    int2* d_asm = nullptr;
+    int2* d_potrf = nullptr;
+    int4* d_trsm = nullptr;
+    GemmTask* d_gemm = nullptr;
+    double* d_Ax_owned = nullptr;
+    const double* last_Ax = nullptr;
+    bool factored = false;
+    int64_t status = 0;
+    bool status_valid = false;
+
+    // profiling
+    bool profile = false;
+    std::vector<hipEvent_t> ev;
+    double phase_ms[8] = {0};
+    // hipGraph replay
+    bool use_graph = false;
+    hipGraphExec_t gexec = nullptr;
+    hipGraph_t graph = nullptr;
+    const double* graph_Ax = nullptr;
+
+    // multi-GPU
+    int rank = 0, nranks = 1;
+    void* comm = nullptr;  // ncclComm_t
+
+    std::string err;
+};
+
+int64_t numeric_create(const Symbolic& S, int device, Numeric*& out, std::string& err);
+int64_t numeric_factor(Numeric& N, const double* d_Ax, bool sync);
+int64_t numeric_status(Numeric& N);
+int64_t numeric_export(Numeric& N, int64_t* Lp, int32_t* Li, double* Lx);
+int64_t numeric_timing(Numeric& N, double* t, int nt);
+int64_t numeric_syrk_stats(Numeric& N, int wmin, double* flops, double* ms, int64_t* launches);
+void numeric_free(Numeric* N);
+int64_t debug_syrk(double* dC, int ldc, const double* dA, int lda, int M, int N, int K);
+
+}  // namespace sc

@@ -1,0 +1,192 @@
+"""GPU parity: the HIP numeric path (through the C ABI) vs the CPU oracle.
+
+Bar (BASELINE.json north_star): identical L pattern (p/i) and relative
+Frobenius error < 1e-12 against the reference chol() restatement.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+import sparsecholesky_amd as sc
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-12
+
+
+def rel_fro(a, b):
+    return np.linalg.norm(a - b) / np.linalg.norm(b)
+
+
+def check_parity(A, **kw):
+    st_o, Lp_o, Li_o, Lx_o = oracle.chol(A)
+    assert st_o == 0
+    r = sc.chol(A, **kw)
+    assert r.has_value(), r.error()
+    L = r.value()
+    assert np.array_equal(L.p, Lp_o)
+    assert np.array_equal(L.i, Li_o)
+    err = rel_fro(L.x, Lx_o)
+    assert err < TOL, err
+    return L, err
+
+
+def test_readme_example(gpu, known):
+    g = known["readme5"]
+    A = sc.triplet_to_csc_matrix(g["ti"], g["tj"], g["tx"], 5)
+    L, _ = check_parity(A)
+    assert np.max(np.abs(L.x - np.array(g["Lx_2dec"]))) < g["tol"]
+
+
+def test_gtest_simplicial(gpu, known):  # tests/test_chol.cpp:59-97 against dpotrf_
+    g = known["gtest3"]
+    A = sc.triplet_to_csc_matrix(g["ti"], g["tj"], g["tx"], 3)
+    L = sc.chol(A).value()
+    D = sc.csc_to_dense(L)
+    exp = np.array(g["L_dpotrf_colmajor"]).reshape(3, 3).T
+    assert np.allclose(np.tril(D), np.tril(exp), atol=g["tol"], rtol=0)
+
+
+def test_gtest_supernodal(gpu, known):  # tests/test_chol.cpp:99-136 (fails in the reference)
+    g = known["gtest3"]
+    A = sc.triplet_to_csc_matrix(g["ti"], g["tj"], g["tx"], 3)
+    L = sc.chol_sn(A).value()
+    D = sc.csc_to_dense(L)
+    exp = np.array(g["L_dpotrf_colmajor"]).reshape(3, 3).T
+    assert np.allclose(np.tril(D), np.tril(exp), atol=g["tol"], rtol=0)
+
+
+@pytest.mark.parametrize("name", ["bcsstk01", "1138_bus"])
+def test_reference_matrices(gpu, name, mtx, known):
+    A = mtx(name)
+    L, err = check_parity(A)
+    g = known[name]
+    assert abs(np.linalg.norm(L.x) / g["fro"] - 1) < 1e-12
+    assert abs(L.x[-1] / g["last_diag"] - 1) < 1e-12
+
+
+@pytest.mark.parametrize("name", ["bcsstk01", "1138_bus"])
+def test_reference_matrices_no_relax(gpu, name, mtx):
+    check_parity(mtx(name), relax=0)
+
+
+@pytest.mark.parametrize("k", [8, 16, 24])
+def test_laplacian_nd(gpu, k):
+    check_parity(sc.laplacian3d(k))
+
+
+def test_laplacian_large_fronts_only(gpu):
+    # every front through the blocked large-front path (potrf/trsm/MFMA SYRK)
+    check_parity(sc.laplacian3d(16), small_front_max=0)
+
+
+def test_laplacian_small_nb_outer(gpu):
+    check_parity(sc.laplacian3d(20), panel_nb_outer=64)
+
+
+def test_laplacian_natural_order(gpu):
+    check_parity(sc.laplacian3d(10, nd=False))
+
+
+def test_laplacian_32_residual(gpu):
+    A = sc.laplacian3d(32)
+    L, err = check_parity(A)
+
+
+def test_not_positive_definite(gpu):
+    A = sc.triplet_to_csc_matrix([0, 0, 1], [0, 1, 1], [1.0, 2.0, 1.0], 2)
+    r = sc.chol(A)
+    assert not r.has_value() and r.error() == "A is not positive definite."
+    assert r.status == 2
+
+
+def test_not_positive_definite_large_front(gpu):
+    A = sc.laplacian3d(12)
+    x = A.x.copy()
+    # break one pivot late in the order: make A(k,k) tiny so d <= 0 there
+    k = A.size() - 5
+    diag = A.p[k + 1] - 1
+    assert A.i[diag] == k
+    x[diag] = -1.0
+    B = sc.csc_matrix(A.n_rows, A.n_cols, A.p, A.i, x)
+    r = sc.chol(B, small_front_max=0)
+    assert not r.has_value()
+    assert r.status > 0
+
+
+def test_repeat_factorization_bitwise_deterministic(gpu):
+    A = sc.laplacian3d(16)
+    s = sc.Symbolic(A)
+    num = sc.Numeric(s)
+    assert num.factor(A.x) == 0
+    _, L1 = num.export()
+    assert num.factor(A.x) == 0
+    _, L2 = num.export()
+    assert np.array_equal(L1.x, L2.x)
+
+
+def test_graph_replay_matches_eager(gpu):
+    A = sc.laplacian3d(16)
+    a = sc.chol(A).value()
+    b = sc.chol(A, use_graph=1).value()
+    assert np.array_equal(a.x, b.x)
+
+
+def test_refactor_new_values(gpu):
+    A = sc.laplacian3d(12)
+    s = sc.Symbolic(A)
+    num = sc.Numeric(s)
+    rng = np.random.default_rng(7)
+    for _ in range(2):
+        x = A.x.copy()
+        off = x < 0
+        x[off] = -rng.uniform(0.5, 1.0, off.sum())
+        B = sc.csc_matrix(A.n_rows, A.n_cols, A.p, A.i, x)
+        assert num.factor(x) == 0
+        _, L = num.export()
+        st, Lp, Li, Lx = oracle.chol(B)
+        assert rel_fro(L.x, Lx) < TOL
+
+
+def test_solve_residual(gpu):
+    A = sc.laplacian3d(20)
+    s = sc.Symbolic(A)
+    num = sc.Numeric(s)
+    assert num.factor(A.x) == 0
+    rng = np.random.default_rng(0)
+    xt = rng.standard_normal(A.size())
+    D = sc.csc_to_dense(A)
+    b = D @ xt
+    x = num.solve(b)
+    assert np.linalg.norm(x - xt) / np.linalg.norm(xt) < 1e-10
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 64, 16), (130, 70, 33), (300, 300, 256), (17, 5, 3)])
+def test_syrk_kernel_vs_numpy(gpu, M, N, K):
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(M * 1000 + N + K)
+    A = rng.standard_normal((M, K))
+    C = rng.standard_normal((M, N))
+    dA = torch.tensor(A.T.copy().ravel(), device="cuda", dtype=torch.float64)  # column-major M x K
+    dC = torch.tensor(C.T.copy().ravel(), device="cuda", dtype=torch.float64)
+    rc = sc.lib().sc_debug_syrk(ctypes.c_void_p(dC.data_ptr()), M, ctypes.c_void_p(dA.data_ptr()), M, M, N, K)
+    assert rc == 0
+    got = dC.cpu().numpy().reshape(N, M).T
+    ref = C - A @ A[:N].T
+    mask = np.tril(np.ones((M, N), dtype=bool))
+    assert np.allclose(got[mask], ref[mask], rtol=1e-13, atol=1e-12)
+    assert np.array_equal(got[~mask], C[~mask])  # strictly-upper part untouched
+
+
+def test_device_resident_factor(gpu):
+    torch = pytest.importorskip("torch")
+    A = sc.laplacian3d(16)
+    s = sc.Symbolic(A)
+    num = sc.Numeric(s, device=0)
+    dx = torch.tensor(A.x, device="cuda", dtype=torch.float64)
+    torch.cuda.synchronize()
+    assert num.factor_device(dx.data_ptr()) == 0
+    _, L = num.export()
+    st, Lp, Li, Lx = oracle.chol(A)
+    assert rel_fro(L.x, Lx) < TOL

@@ -1,0 +1,147 @@
+"""Product host symbolic analysis (C++) vs the oracle and the reference's known answers."""
+import numpy as np
+import pytest
+
+import oracle
+import sparsecholesky_amd as sc
+
+
+def inputs(mtx):
+    yield "readme5", sc.triplet_to_csc_matrix([0, 1, 2, 1, 3, 2, 3, 3, 4, 4], [0, 0, 0, 1, 1, 2, 2, 3, 3, 4],
+                                              [5, 1, 1, 4, 1, 4, 1, 5, 1, 3], 5)
+    yield "bcsstk01", mtx("bcsstk01")
+    yield "1138_bus", mtx("1138_bus")
+    yield "lap8", sc.laplacian3d(8)
+    yield "lap16", sc.laplacian3d(16)
+    yield "lap12nat", sc.laplacian3d(12, nd=False)
+
+
+def test_reference_helpers_match_oracle(mtx):
+    for name, A in inputs(mtx):
+        sy = oracle.symbolic(A)
+        parent = sc.etree(A)
+        assert np.array_equal(parent, sy["parent"]), name
+        post = sc.post_order(parent)
+        assert np.array_equal(post, sy["post"]), name
+        cc = sc.col_count(A, parent, post)
+        assert np.array_equal(cc, sy["colcount"]), name
+
+
+def test_schol_pattern_matches_oracle(mtx):
+    for name, A in inputs(mtx):
+        S = sc.schol(A)
+        Lp, Li, parent = oracle.schol(A)
+        assert np.array_equal(S.p, Lp) and np.array_equal(S.i, Li), name
+        assert np.array_equal(S.parent, parent), name
+
+
+def test_symbolic_stats(mtx, known):
+    for name in ("bcsstk01", "1138_bus"):
+        s = sc.Symbolic(mtx(name)).stats()
+        g = known[name]
+        assert s["nnz_L"] == g["nnz_L"] and s["flops"] == g["flops"] and s["etree_depth"] == g["etree_depth"]
+        assert s["flops_executed"] >= s["flops"]
+
+
+def test_reference_supernodes_and_atree(mtx, known):  # src/chol.cpp:42-136, SURVEY App. C
+    for name in ("bcsstk01", "1138_bus"):
+        S = sc.schol(mtx(name))
+        sn_id, sup = sc.compute_supernodes(S)
+        g = known[name]
+        assert len(sup) - 1 == g["ref_supernodes"]
+        at = sc.atree(S, sn_id, sup)
+        assert len(sc.compute_levels(at)) == g["ref_atree_levels"]
+    S = sc.schol(mtx("bcsstk01"))
+    _, sup = sc.compute_supernodes(S)
+    w, c = np.unique(np.diff(sup), return_counts=True)
+    assert {str(a): int(b) for a, b in zip(w, c)} == known["bcsstk01"]["ref_sn_widths"]
+    S = sc.schol(mtx("1138_bus"))
+    _, sup = sc.compute_supernodes(S)
+    assert np.diff(sup).max() == known["1138_bus"]["ref_max_width"]
+
+
+def test_gtest_etree_and_reach(known):  # tests/test_chol.cpp:6-57 through the product library
+    A = sc.build_csc_matrix_from_pattern(known["etree_pattern"])
+    parent = sc.etree(A)
+    assert parent.tolist() == known["etree_expected"]
+    n = A.size()
+    for use_x in (True, False):
+        s = np.zeros(n, dtype=np.int32)
+        w = np.full(n, -1, dtype=np.int32)
+        x = np.zeros(n) if use_x else None
+        top = sc.ereach(A, known["reach_k"], parent, s, w, x)
+        assert top == 0 and s.tolist() == known["reach_expected"]
+
+
+def test_compute_levels_deepest_first():
+    parent = np.array([2, 5, 4, 5, 5, 6, -1], dtype=np.int32)
+    lv = sc.compute_levels(parent)
+    assert lv[-1] == [6] and sorted(sum(lv, [])) == list(range(7))
+    assert lv[0] == [0]  # 0 -> 2 -> 4 -> 5 -> 6 is the deepest chain
+
+
+@pytest.mark.parametrize("k", [48, 64])
+def test_laplacian_table_large(k, known):  # product symbolic on the bigger Appendix B rows
+    row = [r for r in known["laplacian_nd"] if r[0] == k][0]
+    A = sc.laplacian3d(k)
+    s = sc.Symbolic(A).stats()
+    assert (s["n"], s["nnz_A"], s["nnz_L"], s["flops"], s["etree_depth"]) == tuple(row[1:])
+
+
+def test_options_relaxation_changes_partition():
+    A = sc.laplacian3d(16)
+    a = sc.Symbolic(A, relax=0).stats()
+    b = sc.Symbolic(A).stats()
+    assert a["n_supernodes"] == a["n_fundamental"]
+    assert b["n_supernodes"] < a["n_supernodes"]
+    assert a["flops_executed"] == pytest.approx(a["flops"], rel=1e-12)  # no padding without relaxation
+
+
+def test_triplet_to_csc_contract():  # chol.hpp:308-369: swap to upper, sort, sum duplicates
+    A = sc.triplet_to_csc_matrix([1, 0, 0, 2, 2], [0, 1, 0, 2, 0], [1.0, 2.0, 4.0, 5.0, 7.0], 3)
+    assert A.p.tolist() == [0, 1, 2, 4]
+    assert A.i.tolist() == [0, 0, 0, 2]
+    assert A.x.tolist() == [4.0, 3.0, 7.0, 5.0]
+
+
+def test_lower_entries_ignored():
+    # entries with row > col are ignored (chol.hpp:392,696)
+    A = sc.triplet_to_csc_matrix([0, 0, 1], [0, 1, 1], [4.0, 1.0, 3.0], 2)
+    B = sc.csc_matrix(2, 2, np.array([0, 2, 4], dtype=np.int64), np.array([0, 1, 0, 1], dtype=np.int32),
+                      np.array([4.0, 99.0, 1.0, 3.0]))
+    assert np.array_equal(sc.etree(A), sc.etree(B))
+    assert sc.Symbolic(B).nnz_L == sc.Symbolic(A).nnz_L == 3
+
+
+def test_mtx_loader(mtx, known):
+    A = mtx("bcsstk01")
+    assert A.size() == 48 and A.capacity() == known["bcsstk01"]["nnz_A_upper"]
+    assert np.all(A.i <= np.repeat(np.arange(48), np.diff(A.p)))
+
+
+def test_laplacian_generator_is_permuted_stencil():
+    k = 6
+    A, perm = sc.laplacian3d(k, with_perm=True)
+    n = k ** 3
+    assert sorted(perm.tolist()) == list(range(n))
+    D = sc.csc_to_dense(A)
+    # undo the permutation and compare with the natural-order stencil
+    N = sc.csc_to_dense(sc.laplacian3d(k, nd=False))
+    assert np.array_equal(D, N[np.ix_(perm, perm)])
+    assert np.allclose(np.diag(D), 6.0)
+
+
+def test_invalid_input_rejected():
+    A = sc.csc_matrix(2, 2, np.array([0, 1, 3], dtype=np.int64), np.array([0, 5, 1], dtype=np.int32),
+                      np.array([1.0, 1.0, 1.0]))
+    with pytest.raises(sc.LibraryError):
+        sc.Symbolic(A)
+
+
+def test_empty_and_single():
+    A0 = sc.csc_matrix(0, 0, np.zeros(1, dtype=np.int64), np.zeros(0, dtype=np.int32), np.zeros(0))
+    s = sc.Symbolic(A0).stats()
+    assert s["n"] == 0 and s["nnz_L"] == 0 and s["n_supernodes"] == 0
+    A1 = sc.triplet_to_csc_matrix([0], [0], [9.0], 1)
+    s = sc.Symbolic(A1).stats()
+    assert s["nnz_L"] == 1 and s["n_supernodes"] == 1
