@@ -141,6 +141,14 @@ def lib() -> C.CDLL:
             raise LibraryError(
                 f"{LIB_PATH} missing: build it with `make -C sparsecholesky_amd/csrc` "
                 "(or __graft_entry__.build())")
+        # torch (when present) bundles its own libamdhip64.so.7; loading it first
+        # lets this library bind to the same HIP runtime (same soname) so device
+        # pointers and streams are shared instead of two runtimes fighting over
+        # the device.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, res, args in _SIGS:
             f = getattr(L, name)
