@@ -76,6 +76,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-k", type=int, default=32)
     ap.add_argument("--graph", type=int, default=0)
+    ap.add_argument("--relax-wmax", type=int, default=None)
+    ap.add_argument("--nbo", type=int, default=None, help="panel outer block (rank-k update width)")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
@@ -85,21 +87,48 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus > 1 or world > 1:
-        raise SystemExit("multi-GPU bench not available in this build")
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.gpus > 1 and world == 1:
+        raise SystemExit("multi-GPU runs are launched with torch.distributed.run (one rank per GPU)")
     torch.cuda.set_device(local_rank)
     dev = local_rank
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        # CPU group: carries only the RCCL unique id, barriers and the max-time
+        # reduction; the data path (contribution blocks) is RCCL inside the library.
+        dist.init_process_group("gloo")
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
 
     t0 = time.perf_counter()
     A = sc.laplacian3d(args.k)
     t_gen = time.perf_counter() - t0
     t0 = time.perf_counter()
-    symb = sc.Symbolic(A, use_graph=args.graph)
+    kw = {"use_graph": args.graph if world == 1 else 0}
+    if args.relax_wmax is not None:
+        kw["relax_wmax"] = args.relax_wmax
+    if args.nbo is not None:
+        kw["panel_nb_outer"] = args.nbo
+    symb = sc.Symbolic(A, **kw)
     t_an = time.perf_counter() - t0
     st = symb.stats()
     F = st["flops"]
     t0 = time.perf_counter()
-    num = sc.Numeric(symb, device=dev)
+    work_share = None
+    if world > 1:
+        uid = [sc.dist_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        num = sc.Numeric(symb, device=dev, rank=rank, nranks=world, uid=uid[0])
+        _, wr = symb.owner_map(world)
+        work_share = [round(float(x) / float(wr.sum()), 4) for x in wr]
+    else:
+        num = sc.Numeric(symb, device=dev)
     t_alloc = time.perf_counter() - t0
     d_Ax = torch.from_numpy(A.x).to(f"cuda:{dev}")
     torch.cuda.synchronize()
@@ -109,28 +138,33 @@ def main():
         assert rc == 0, f"factorization failed: {rc}"
 
     num.set_profile(not args.graph)
-    torch.cuda.synchronize()
+    barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         num.factor_device(d_Ax.data_ptr(), sync=False)
     rc = num.status()  # synchronizes the library stream
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    assert rc == 0
+    barrier()
+    assert rc == 0, f"factorization failed: {rc}"
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
     ms_step = dt * 1e3 / args.steps
     gflops = F / (ms_step * 1e-3) / 1e9
 
     roof = None
     phases = None
     if not args.graph:
-        phases = num.timing().tolist()
+        phases = [round(x, 3) for x in num.timing().tolist()]
         fl, ms, nl = num.syrk_stats(256)
         if ms > 0 and nl > 0:
             ach = fl / (ms * 1e-3) / 1e12
             roof = {
                 "bound": "mfma", "achieved": round(ach, 3), "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(ach / FP64_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                "kernel": "syrk_mfma_kernel (CB update, fronts w>=256)",
+                "kernel": "syrk_mfma_kernel<*,1> (CB update, fronts w>=256)" + (" on rank 0" if world > 1 else ""),
                 "flops_per_step": fl, "kernel_ms_per_step": round(ms, 3), "launches_per_step": nl,
             }
 
@@ -138,7 +172,7 @@ def main():
         "metric": "numeric-factorization fp64 GFLOP/s (F=sum colcount^2)",
         "value": round(gflops, 2),
         "unit": "GFLOP/s",
-        "n_gpus": 1,
+        "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3),
@@ -151,15 +185,24 @@ def main():
             "workload": f"lap3d_{args.k}_nd",
             "n": st["n"], "nnz_A_upper": st["nnz_A"], "nnz_L": st["nnz_L"], "flops": F,
             "supernodes": st["n_supernodes"], "levels": st["n_levels"], "max_front": st["max_front_m"],
-            "flops_executed": st["flops_executed"], "parallelism": "single GPU",
+            "flops_executed": st["flops_executed"],
+            "parallelism": "single GPU" if world == 1 else
+            f"subtree partition over {world} GPUs, RCCL p2p of contribution blocks at merge fronts",
+            "work_share_per_rank": work_share,
+            "options": {"relax_wmax": symb.opt.relax_wmax, "panel_nb_outer": symb.opt.panel_nb_outer,
+                        "small_front_max": symb.opt.small_front_max, "use_graph": symb.opt.use_graph},
         },
         "roofline": roof,
         "timing_s": {"generate": round(t_gen, 3), "analyze": round(t_an, 3), "numeric_create": round(t_alloc, 3)},
         "phase_ms": phases,
     }
-    if not args.no_cpu_baseline and rank == 0:
+    if not args.no_cpu_baseline and rank == 0 and world == 1:
         out["cpu_baseline"] = cpu_baseline(args.cpu_k)
-    print(json.dumps(out), flush=True)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -59,7 +59,9 @@ typedef struct sc_options {
     int32_t panel_nb;        /* inner panel block (potrf/trsm width), 64 */
     int32_t panel_nb_outer;  /* outer panel block (rank-k panel update width), 256 */
     int32_t use_graph;       /* capture the level schedule into a hipGraph and replay it */
-    int32_t reserved[8];
+    int32_t relax_wmax;      /* never amalgamate two supernodes that are both wider than this */
+    int32_t syrk_tile;       /* 64 (default) or 128: output tile edge of the MFMA SYRK kernel */
+    int32_t reserved[6];
 } sc_options;
 
 /* Symbolic statistics (host analysis). */
@@ -126,7 +128,7 @@ int64_t sc_export_L(sc_numeric* num, int64_t* Lp, int32_t* Li, double* Lx);
 /* Device pointer of the library stream (hipStream_t) for event timing. */
 void* sc_numeric_stream(sc_numeric* num);
 /* Per-phase timing of the last factorization, milliseconds (HIP events):
- * t[0]=total, t[1]=scatter, t[2]=small fronts, t[3]=assembly, t[4]=potrf,
+ * t[0]=total, t[1]=CB transfers (multi-GPU), t[2]=small fronts, t[3]=assembly, t[4]=potrf,
  * t[5]=trsm, t[6]=panel update, t[7]=CB syrk.  Enabled by sc_numeric_set_profile. */
 int64_t sc_numeric_set_profile(sc_numeric* num, int32_t on);
 int64_t sc_numeric_timing(sc_numeric* num, double* t, int32_t nt);
@@ -180,9 +182,14 @@ int64_t sc_laplacian3d(int64_t k, int32_t nd_order, int64_t* Ap, int32_t* Ai, do
 /* ---------------- multi-GPU (subtree partition over RCCL) ----------------
  * Proportional subtree-to-GPU mapping of the assembly tree; contribution
  * blocks cross GPUs only at subtree-merge fronts. */
+/* RCCL unique id (128 bytes), created on rank 0 and broadcast by the caller. */
 int64_t sc_dist_unique_id(void* id128);
 int64_t sc_dist_owner_map(const sc_symbolic* sym, int32_t nranks, int32_t* owner_of_supernode,
                           double* work_per_rank);
+/* This process is `rank` of `nranks` (one GPU each); it factors only the
+ * supernodes it owns and exchanges contribution blocks with ncclSend/ncclRecv
+ * after each assembly-tree level.  id128 == NULL: emulate all nranks ranks'
+ * partitioned schedule inside this process on one device (validation mode). */
 int64_t sc_numeric_create_dist(const sc_symbolic* sym, int32_t device, int32_t rank,
                                int32_t nranks, const void* id128, sc_numeric** out);
 /* Per-rank message schedule for tests: returns number of messages; if the

@@ -66,7 +66,8 @@ class Options(C.Structure):
     _fields_ = [
         ("relax", C.c_int32), ("nrelax", C.c_int32 * 3), ("zrelax", C.c_double * 3),
         ("small_front_max", C.c_int32), ("panel_nb", C.c_int32), ("panel_nb_outer", C.c_int32),
-        ("use_graph", C.c_int32), ("reserved", C.c_int32 * 8),
+        ("use_graph", C.c_int32), ("relax_wmax", C.c_int32), ("syrk_tile", C.c_int32),
+        ("reserved", C.c_int32 * 6),
     ]
 
 
@@ -471,10 +472,23 @@ class Symbolic:
 class Numeric:
     """Device factorization handle (pools + level schedule on one HIP device)."""
 
-    def __init__(self, symb: Symbolic, device: int = -1):
+    def __init__(self, symb: Symbolic, device: int = -1, rank: int = 0, nranks: int = 1,
+                 uid: Optional[bytes] = None, virtual: bool = False):
+        """nranks > 1 with ``uid`` (from :func:`dist_unique_id` on rank 0): this process is
+        ``rank`` of a subtree-partitioned multi-GPU factorization over RCCL.  ``virtual=True``
+        emulates all ``nranks`` ranks' partitioned schedule in this one process."""
         self.symb = symb
+        self.rank, self.nranks = rank, nranks
         h = C.c_void_p()
-        _check(lib().sc_numeric_create(symb.h, device, C.byref(h)), "numeric_create")
+        if nranks > 1 or virtual:
+            idbuf = None
+            if not virtual:
+                assert uid is not None and len(uid) == 128
+                idbuf = C.create_string_buffer(uid, 128)
+            _check(lib().sc_numeric_create_dist(symb.h, device, rank, nranks, idbuf, C.byref(h)),
+                   "numeric_create_dist")
+        else:
+            _check(lib().sc_numeric_create(symb.h, device, C.byref(h)), "numeric_create")
         self.h = h
 
     def factor(self, Ax: np.ndarray) -> int:
@@ -524,6 +538,13 @@ class Numeric:
         if h and _lib is not None:
             _lib.sc_free_numeric(h)
             self.h = None
+
+
+def dist_unique_id() -> bytes:
+    """RCCL unique id (128 bytes) for sc_numeric_create_dist; create on rank 0, broadcast."""
+    buf = C.create_string_buffer(128)
+    _check(lib().sc_dist_unique_id(buf), "dist_unique_id")
+    return buf.raw
 
 
 # --------------------------------------------------------------------------

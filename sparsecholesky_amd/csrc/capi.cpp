@@ -71,6 +71,8 @@ void sc_default_options(sc_options* opt) {
     opt->panel_nb = 64;
     opt->panel_nb_outer = 256;
     opt->use_graph = 0;
+    opt->relax_wmax = 1024;
+    opt->syrk_tile = 64;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,

@@ -8,6 +8,8 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "numeric.hpp"
 #include "symbolic.hpp"
 
@@ -65,6 +67,9 @@ i64 dist_owner_map(const Symbolic& S, int nranks, i32* owner, double* work_per_r
         }
     };
     const double eps = 1e-9;
+    // multi-rank (merge) fronts, placed after the subtrees: least-loaded rank of
+    // their interval, children before parents
+    std::vector<std::pair<i32, std::pair<i32, i32>>> shared;
     while (!stack.empty()) {
         Item it = stack.back();
         stack.pop_back();
@@ -77,6 +82,7 @@ i64 dist_owner_map(const Symbolic& S, int nranks, i32* owner, double* work_per_r
             continue;
         }
         own[it.s] = lo;
+        shared.push_back({it.s, {lo, hi}});
         double Wc = 0.0;
         for (i32 q = S.child_ptr[it.s]; q < S.child_ptr[it.s + 1]; ++q) Wc += work[S.child_list[q]];
         double cum = 0.0;
@@ -86,6 +92,26 @@ i64 dist_owner_map(const Symbolic& S, int nranks, i32* owner, double* work_per_r
             cum += work[c];
             const double b = it.a + (it.b - it.a) * (Wc > 0 ? cum / Wc : 1.0);
             stack.push_back({c, a, b});
+        }
+    }
+    {
+        std::vector<double> load((size_t)nranks, 0.0);
+        std::vector<char> is_shared((size_t)S.ns, 0);
+        for (auto& sh : shared) is_shared[sh.first] = 1;
+        for (i32 s = 0; s < S.ns; ++s) {
+            if (is_shared[s]) continue;
+            const double m = S.sn_m[s], w = S.w(s);
+            load[own[s]] += w * m * m - m * w * (w - 1) + (w - 1) * w * (2 * w - 1) / 6.0;
+        }
+        std::sort(shared.begin(), shared.end());  // postorder: children first
+        for (auto& sh : shared) {
+            const i32 s = sh.first, lo = sh.second.first, hi = sh.second.second;
+            i32 best = lo;
+            for (i32 r = lo + 1; r < hi; ++r)
+                if (load[r] < load[best]) best = r;
+            own[s] = best;
+            const double m = S.sn_m[s], w = S.w(s);
+            load[best] += w * m * m - m * w * (w - 1) + (w - 1) * w * (2 * w - 1) / 6.0;
         }
     }
     if (owner) std::memcpy(owner, own.data(), sizeof(i32) * (size_t)S.ns);
@@ -126,21 +152,92 @@ i64 dist_schedule(const Symbolic& S, int nranks, int rank, i32* level, i32* peer
     return cnt;
 }
 
+// ---------------- RCCL transport ----------------
+static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+
 i64 dist_unique_id(void* id128) {
-    (void)id128;
-    return SC_ERR_NOTIMPL;
+    if (!id128) return SC_ERR_ARG;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return SC_ERR_COMM;
+    std::memcpy(id128, &id, sizeof(id));
+    return SC_OK;
 }
 
+// All CB transfers of one level as one RCCL group on the library stream: both
+// sides post them in the same global order (level, then child id), so the
+// point-to-point matching per peer pair is consistent.
+hipError_t comm_launch(Numeric& N, const Launch& L) {
+    if (!N.comm) return hipErrorInvalidValue;
+    ncclComm_t comm = (ncclComm_t)N.comm;
+    if (ncclGroupStart() != ncclSuccess) return hipErrorUnknown;
+    for (int64_t q = L.off; q < L.off + L.count; ++q) {
+        const Msg& g = N.msgs[q];
+        ncclResult_t r = g.is_send ? ncclSend(g.buf, (size_t)g.count, ncclDouble, g.peer, comm, N.stream)
+                                   : ncclRecv(g.buf, (size_t)g.count, ncclDouble, g.peer, comm, N.stream);
+        if (r != ncclSuccess) {
+            N.err = std::string("rccl p2p: ") + ncclGetErrorString(r);
+            (void)ncclGroupEnd();
+            return hipErrorUnknown;
+        }
+    }
+    ncclResult_t r = ncclGroupEnd();
+    if (r != ncclSuccess) {
+        N.err = std::string("rccl group: ") + ncclGetErrorString(r);
+        return hipErrorUnknown;
+    }
+    return hipSuccess;
+}
+
+void comm_destroy(Numeric& N) {
+    if (N.comm) {
+        (void)ncclCommDestroy((ncclComm_t)N.comm);
+        N.comm = nullptr;
+    }
+}
+
+// Real multi-GPU handle: this process is `rank` of `nranks` (one GPU each).
+// Every rank allocates the full pools (288 GB HBM per GPU holds them) but only
+// computes the supernodes the proportional mapping gives it.
 i64 numeric_create_dist(const Symbolic& S, int device, int rank, int nranks, const void* id128, Numeric*& out,
                         std::string& err) {
-    (void)S;
-    (void)device;
-    (void)rank;
-    (void)nranks;
-    (void)id128;
     out = nullptr;
-    err = "distributed numeric factorization not built yet";
-    return SC_ERR_NOTIMPL;
+    Numeric* Np = new (std::nothrow) Numeric();
+    if (!Np) return SC_ERR_NOMEM;
+    Numeric& N = *Np;
+    N.rank = rank;
+    N.nranks = nranks;
+    N.owner.resize((size_t)S.ns);
+    dist_owner_map(S, nranks, N.owner.data(), nullptr);
+    if (!id128) {
+        // in-process emulation of all ranks (shared pools, no transfers)
+        N.virt_ranks = nranks;
+    } else if (nranks > 1) {
+        int dev = device;
+        if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
+        if (hipSetDevice(dev) != hipSuccess) {
+            err = "hipSetDevice failed";
+            delete Np;
+            return SC_ERR_HIP;
+        }
+        ncclUniqueId id;
+        std::memcpy(&id, id128, sizeof(id));
+        ncclComm_t comm = nullptr;
+        ncclResult_t r = ncclCommInitRank(&comm, nranks, id, rank);
+        if (r != ncclSuccess) {
+            err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+            delete Np;
+            return SC_ERR_COMM;
+        }
+        N.comm = comm;
+    }
+    i64 rc = numeric_init(N, S, device);
+    if (rc != SC_OK) {
+        err = N.err;
+        numeric_free(Np);
+        return rc;
+    }
+    out = Np;
+    return SC_OK;
 }
 
 }  // namespace sc

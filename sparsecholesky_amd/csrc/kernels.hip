@@ -256,7 +256,7 @@ __global__ __launch_bounds__(256) void trsm_panel_kernel(DevPlan P, const int4* 
 // (2 x 2), each wave (BT/2) x (BT/2) = RT x RT tiles of v_mfma_f64_16x16x4_f64.
 // A (M x K) and the B operand (its first N rows) share one column-major array.
 // ---------------------------------------------------------------------------
-template <int BT>
+template <int BT, int TAG>
 __global__ __launch_bounds__(256) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks, int ntasks) {
     constexpr int BK = 16;
     constexpr int LDT = BT + 16;  // +128 B row pad: the two k-rows read by a half-wave hit disjoint banks
@@ -401,9 +401,20 @@ hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hip
     return hipGetLastError();
 }
 
-hipError_t launch_syrk(const GemmTask* tasks, int ntasks, int total_tiles, hipStream_t st) {
+// TAG only separates the launches in profiles: 0 = panel update, 1 = CB update.
+hipError_t launch_syrk(const GemmTask* tasks, int ntasks, int total_tiles, int bt, int tag, hipStream_t st) {
     if (total_tiles <= 0) return hipSuccess;
-    hipLaunchKernelGGL(syrk_mfma_kernel<SYRK_BT>, dim3(total_tiles), dim3(256), 0, st, tasks, ntasks);
+    if (bt == 128) {
+        if (tag)
+            hipLaunchKernelGGL((syrk_mfma_kernel<128, 1>), dim3(total_tiles), dim3(256), 0, st, tasks, ntasks);
+        else
+            hipLaunchKernelGGL((syrk_mfma_kernel<128, 0>), dim3(total_tiles), dim3(256), 0, st, tasks, ntasks);
+    } else {
+        if (tag)
+            hipLaunchKernelGGL((syrk_mfma_kernel<64, 1>), dim3(total_tiles), dim3(256), 0, st, tasks, ntasks);
+        else
+            hipLaunchKernelGGL((syrk_mfma_kernel<64, 0>), dim3(total_tiles), dim3(256), 0, st, tasks, ntasks);
+    }
     return hipGetLastError();
 }
 

@@ -13,8 +13,9 @@ constexpr int PNB = 64;
 constexpr int TRSM_ROWS = 64;
 // Columns owned by one assembly workgroup.
 constexpr int ASM_COLS = 64;
-// Output tile edge of the MFMA SYRK kernel.
-constexpr int SYRK_BT = 64;
+// Output tile edges of the MFMA SYRK kernel (per launch).
+constexpr int SYRK_BT_SMALL = 64;
+constexpr int SYRK_BT_LARGE = 128;
 
 // C/D register map of v_mfma_f64_16x16x4_f64 on gfx950 (cdna_hip_programming.md
 // section 3): col = lane & 15, row = (lane >> 4) + 4 * reg.
@@ -54,7 +55,7 @@ hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count,
                                  hipStream_t st);
 hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hipStream_t st);
 hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st);
-hipError_t launch_syrk(const GemmTask* tasks, int ntasks, int total_tiles, hipStream_t st);
+hipError_t launch_syrk(const GemmTask* tasks, int ntasks, int total_tiles, int bt, int tag, hipStream_t st);
 
 // tiles of an M x N lower trapezoid with square BT tiles
 inline int64_t syrk_tiles(int64_t M, int64_t N, int bt) {

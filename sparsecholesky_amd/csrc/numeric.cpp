@@ -89,10 +89,14 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         L.kind = kind;
         L.level = level;
         L.off = (int64_t)gemm.size();
+        // 128x128 tiles when every task is at least 256 wide (little edge waste)
+        int minN = INT32_MAX;
+        for (auto& t : tasks) minN = std::min(minN, (int)t.N);
+        L.bt = (S.opt.syrk_tile == 128 && minN >= 256) ? SYRK_BT_LARGE : SYRK_BT_SMALL;
         int64_t tiles = 0;
         for (auto t : tasks) {
             t.tile_base = (int32_t)tiles;
-            tiles += syrk_tiles(t.M, t.N, SYRK_BT);
+            tiles += syrk_tiles(t.M, t.N, L.bt);
             gemm.push_back(t);
         }
         L.count = (int32_t)tiles;
@@ -101,8 +105,8 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         L.flops = flops;
         N.sched.push_back(L);
     };
-    for (int32_t lev = 0; lev < S.nlevels; ++lev) {
-        const auto& nodes = by_level[lev];
+    // one level's fronts (already filtered to the ranks this process runs)
+    auto emit_level = [&](int32_t lev, const std::vector<int32_t>& nodes) {
         // small fronts by LDS bucket
         for (int b : {32, 64, 96, 128}) {
             Launch L {};
@@ -118,7 +122,7 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         std::vector<int32_t> large;
         for (int32_t s : nodes)
             if (S.fclass[s] == FRONT_LARGE) large.push_back(s);
-        if (large.empty()) continue;
+        if (large.empty()) return;
         {
             Launch L {};
             L.kind = L_ASM;
@@ -204,6 +208,46 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             }
             push_gemm_launch(L_CB, lev, cbt, big, fl);
         }
+        };
+    for (int32_t lev = 0; lev < S.nlevels; ++lev) {
+        if (N.owner.empty()) {
+            emit_level(lev, by_level[lev]);
+            continue;
+        }
+        const int nr = N.virt_ranks > 1 ? N.virt_ranks : 1;
+        for (int r = 0; r < nr; ++r) {
+            const int who = N.virt_ranks > 1 ? r : N.rank;
+            std::vector<int32_t> mine;
+            for (int32_t s : by_level[lev])
+                if (N.owner[s] == who) mine.push_back(s);
+            if (!mine.empty()) emit_level(lev, mine);
+        }
+        if (N.virt_ranks > 1) continue;  // shared pools: nothing moves
+        // contribution blocks that leave / enter this rank after this level
+        Launch L {};
+        L.kind = L_COMM;
+        L.level = lev;
+        L.off = (int64_t)N.msgs.size();
+        for (int32_t c : by_level[lev]) {
+            const int32_t p = S.sn_parent[c];
+            if (p < 0 || N.owner[c] == N.owner[p]) continue;
+            const int64_t mb = S.mb(c);
+            Msg g {};
+            g.buf = cb_pool + S.cb_off[c];
+            g.count = mb * mb;
+            g.child = c;
+            if (N.owner[c] == N.rank) {
+                g.peer = N.owner[p];
+                g.is_send = 1;
+                N.msgs.push_back(g);
+            } else if (N.owner[p] == N.rank) {
+                g.peer = N.owner[c];
+                g.is_send = 0;
+                N.msgs.push_back(g);
+            }
+        }
+        L.count = (int32_t)((int64_t)N.msgs.size() - L.off);
+        if (L.count > 0) N.sched.push_back(L);
     }
     return SC_OK;
 }
@@ -212,13 +256,19 @@ int64_t numeric_create(const Symbolic& S, int device, Numeric*& out, std::string
     out = nullptr;
     Numeric* Np = new (std::nothrow) Numeric();
     if (!Np) return SC_ERR_NOMEM;
-    Numeric& N = *Np;
-    N.S = &S;
-    auto fail = [&](int64_t rc) {
-        err = N.err;
+    int64_t rc = numeric_init(*Np, S, device);
+    if (rc != SC_OK) {
+        err = Np->err;
         numeric_free(Np);
         return rc;
-    };
+    }
+    out = Np;
+    return SC_OK;
+}
+
+int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
+    N.S = &S;
+    auto fail = [&](int64_t rc) { return rc; };
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         N.err = "no HIP device available";
@@ -281,9 +331,10 @@ int64_t numeric_create(const Symbolic& S, int device, Numeric*& out, std::string
         (rc = upload(N, potrf, N.d_potrf)) || (rc = upload(N, trsm, N.d_trsm)) ||
         (rc = upload(N, gemm, N.d_gemm)))
         return fail(rc);
-    out = Np;
     return SC_OK;
 }
+
+hipError_t comm_launch(Numeric& N, const Launch& L);  // dist.cpp
 
 static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
     switch (L.kind) {
@@ -297,7 +348,9 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
             return launch_trsm_panel(N.P, N.d_trsm + L.off, L.count, N.stream);
         case L_PANEL:
         case L_CB:
-            return launch_syrk(N.d_gemm + L.off, L.ntasks, L.count, N.stream);
+            return launch_syrk(N.d_gemm + L.off, L.ntasks, L.count, L.bt, L.kind == L_CB ? 1 : 0, N.stream);
+        case L_COMM:
+            return comm_launch(N, L);
     }
     return hipErrorInvalidValue;
 }
@@ -378,6 +431,7 @@ int64_t numeric_status(Numeric& N) {
                 case L_TRSM: slot = 5; break;
                 case L_PANEL: slot = 6; break;
                 case L_CB: slot = 7; break;
+                case L_COMM: slot = 1; break;
             }
             N.phase_ms[slot] += ms;
             if (!first) first = N.ev[2 * i];
@@ -435,11 +489,14 @@ int64_t numeric_export(Numeric& N, int64_t* Lp, int32_t* Li, double* Lx) {
     return st;
 }
 
+void comm_destroy(Numeric& N);  // dist.cpp
+
 void numeric_free(Numeric* Np) {
     if (!Np) return;
     Numeric& N = *Np;
     (void)hipSetDevice(N.device);
     if (N.stream) (void)hipStreamSynchronize(N.stream);
+    comm_destroy(N);
     if (N.gexec) (void)hipGraphExecDestroy(N.gexec);
     if (N.graph) (void)hipGraphDestroy(N.graph);
     for (auto e : N.ev)
@@ -466,7 +523,8 @@ int64_t debug_syrk(double* dC, int ldc, const double* dA, int lda, int M, int Nn
         (void)hipFree(d);
         return SC_ERR_HIP;
     }
-    hipError_t e = launch_syrk(d, 1, (int)syrk_tiles(M, Nn, SYRK_BT), nullptr);
+    const int bt = (Nn >= 256) ? SYRK_BT_LARGE : SYRK_BT_SMALL;
+    hipError_t e = launch_syrk(d, 1, (int)syrk_tiles(M, Nn, bt), bt, 0, nullptr);
     hipError_t e2 = hipDeviceSynchronize();
     (void)hipFree(d);
     return (e == hipSuccess && e2 == hipSuccess) ? SC_OK : SC_ERR_HIP;

@@ -18,7 +18,17 @@ enum LaunchKind : int32_t {
     L_TRSM = 3,
     L_PANEL = 4,
     L_CB = 5,
-    L_KINDS = 6
+    L_COMM = 6,  // CB send/recv group after a level (multi-GPU)
+    L_KINDS = 7
+};
+
+// One point-to-point contribution-block transfer (multi-GPU).
+struct Msg {
+    double* buf;
+    int64_t count;  // doubles
+    int32_t peer;
+    int32_t is_send;
+    int32_t child;  // supernode whose CB moves
 };
 
 struct Launch {
@@ -29,6 +39,7 @@ struct Launch {
     int32_t ntasks;   // tasks (SYRK launches)
     int32_t maxm;     // small-front LDS edge
     int32_t big;      // CB launch covering fronts with w >= 256
+    int32_t bt;       // SYRK tile edge (64 or 128)
     double flops;     // algorithmic SYRK flops (CB launches: mb*(mb+1)*w)
 };
 
@@ -60,12 +71,20 @@ struct Numeric {
     hipGraph_t graph = nullptr;
     const double* graph_Ax = nullptr;
 
-    // multi-GPU
-    int rank = 0, nranks = 1;
+    // multi-GPU: owner rank per supernode (empty = single GPU).  virt_ranks > 1
+    // runs the partitioned schedule of all ranks in this one process (shared
+    // pools, no transfers) to validate the partition on one device.
+    int rank = 0, nranks = 1, virt_ranks = 0;
+    std::vector<int32_t> owner;
+    std::vector<Msg> msgs;
     void* comm = nullptr;  // ncclComm_t
+    double comm_ms = 0.0;
 
     std::string err;
 };
+
+// Builds pools + schedule; owner/rank restrict the schedule to one rank's fronts.
+int64_t numeric_init(Numeric& N, const Symbolic& S, int device);
 
 int64_t numeric_create(const Symbolic& S, int device, Numeric*& out, std::string& err);
 int64_t numeric_factor(Numeric& N, const double* d_Ax, bool sync);

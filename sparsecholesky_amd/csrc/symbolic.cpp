@@ -252,7 +252,9 @@ i64 analyze(i64 n, const i64* Ap, const i32* Ai, const sc_options& opt, Symbolic
             const double newzeros = (double)nscol0 * (double)(nscol0 + lnz1 - lnz0);
             const double totz = newzeros + zeros[j] + zeros[j + 1];
             bool merge = false;
-            if (ns <= opt.nrelax[0] || newzeros == 0.0) {
+            if (opt.relax_wmax > 0 && nscol0 > opt.relax_wmax && nscol1 > opt.relax_wmax) {
+                merge = false;  // keep wide fronts apart: their coupling goes through the CB SYRK
+            } else if (ns <= opt.nrelax[0] || newzeros == 0.0) {
                 merge = true;
             } else {
                 const double denom =

@@ -191,3 +191,20 @@ def test_device_resident_factor(gpu):
     _, L = num.export()
     st, Lp, Li, Lx = oracle.chol(A)
     assert rel_fro(L.x, Lx) < TOL
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 8])
+def test_partitioned_schedule_bitwise_equal(gpu, nranks):
+    # the multi-GPU partition (every front computed once by its owner, per-level
+    # ordering) emulated in one process must reproduce the single-GPU factor
+    A = sc.laplacian3d(20)
+    s = sc.Symbolic(A)
+    ref = sc.Numeric(s)
+    assert ref.factor(A.x) == 0
+    _, L0 = ref.export()
+    v = sc.Numeric(s, nranks=nranks, virtual=True)
+    assert v.factor(A.x) == 0
+    _, L1 = v.export()
+    assert np.array_equal(L0.x, L1.x)
+    st, Lp, Li, Lx = oracle.chol(A)
+    assert rel_fro(L1.x, Lx) < TOL
