@@ -78,6 +78,7 @@ def main():
     ap.add_argument("--graph", type=int, default=0)
     ap.add_argument("--relax-wmax", type=int, default=None)
     ap.add_argument("--nbo", type=int, default=None, help="panel outer block (rank-k update width)")
+    ap.add_argument("--lookahead", type=int, default=None)
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
@@ -115,6 +116,8 @@ def main():
         kw["relax_wmax"] = args.relax_wmax
     if args.nbo is not None:
         kw["panel_nb_outer"] = args.nbo
+    if args.lookahead is not None:
+        kw["lookahead"] = args.lookahead
     symb = sc.Symbolic(A, **kw)
     t_an = time.perf_counter() - t0
     st = symb.stats()
@@ -167,6 +170,12 @@ def main():
                 "kernel": "syrk_mfma_kernel<*,1> (CB update, fronts w>=256)" + (" on rank 0" if world > 1 else ""),
                 "flops_per_step": fl, "kernel_ms_per_step": round(ms, 3), "launches_per_step": nl,
             }
+        pfl, pms, pnl = num.syrk_stats(-1)
+        cfl, cms, cnl = num.syrk_stats(0)
+        if pms > 0 and cms > 0:
+            roof["other_syrk"] = {"panel_update_tflops": round(pfl / (pms * 1e-3) / 1e12, 2),
+                                  "panel_update_ms": round(pms, 2), "panel_update_flops": pfl,
+                                  "cb_all_tflops": round(cfl / (cms * 1e-3) / 1e12, 2)}
 
     out = {
         "metric": "numeric-factorization fp64 GFLOP/s (F=sum colcount^2)",
@@ -190,7 +199,8 @@ def main():
             f"subtree partition over {world} GPUs, RCCL p2p of contribution blocks at merge fronts",
             "work_share_per_rank": work_share,
             "options": {"relax_wmax": symb.opt.relax_wmax, "panel_nb_outer": symb.opt.panel_nb_outer,
-                        "small_front_max": symb.opt.small_front_max, "use_graph": symb.opt.use_graph},
+                        "small_front_max": symb.opt.small_front_max, "use_graph": symb.opt.use_graph,
+                        "lookahead": symb.opt.lookahead},
         },
         "roofline": roof,
         "timing_s": {"generate": round(t_gen, 3), "analyze": round(t_an, 3), "numeric_create": round(t_alloc, 3)},

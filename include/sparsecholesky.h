@@ -61,7 +61,8 @@ typedef struct sc_options {
     int32_t use_graph;       /* capture the level schedule into a hipGraph and replay it */
     int32_t relax_wmax;      /* never amalgamate two supernodes that are both wider than this */
     int32_t syrk_tile;       /* 64 (default) or 128: output tile edge of the MFMA SYRK kernel */
-    int32_t reserved[6];
+    int32_t lookahead;       /* 0: none; 1: trailing panel updates on a 2nd stream; 2: same, 2nd stream CU-masked to 7/8 */
+    int32_t reserved[5];
 } sc_options;
 
 /* Symbolic statistics (host analysis). */
@@ -106,6 +107,11 @@ double sc_flops(const sc_symbolic* sym);
 int64_t sc_symbolic_pattern(const sc_symbolic* sym, int64_t* Lp, int32_t* Li);
 /* etree parent (chol.hpp:377) and postorder (chol.hpp:466), natural numbering. */
 int64_t sc_symbolic_etree(const sc_symbolic* sym, int32_t* parent, int32_t* post);
+/* The relaxed supernode partition used on the device (internal = postorder
+ * numbering): sn_start[ns+1] first internal column, sn_m[ns] front rows,
+ * sn_parent[ns] assembly-tree parent (-1 = root), level[ns] height.  Any may be NULL. */
+int64_t sc_symbolic_supernodes(const sc_symbolic* sym, int32_t* sn_start, int32_t* sn_m, int32_t* sn_parent,
+                               int32_t* level);
 void sc_free_symbolic(sc_symbolic* sym);
 
 /* ---------------- device numeric factorization ----------------
@@ -132,8 +138,17 @@ void* sc_numeric_stream(sc_numeric* num);
  * t[5]=trsm, t[6]=panel update, t[7]=CB syrk.  Enabled by sc_numeric_set_profile. */
 int64_t sc_numeric_set_profile(sc_numeric* num, int32_t on);
 int64_t sc_numeric_timing(sc_numeric* num, double* t, int32_t nt);
+/* Wall time (ms) of each assembly-tree level of the last profiled factorization;
+ * returns the number of levels. */
+int64_t sc_numeric_level_times(sc_numeric* num, double* ms, int32_t nl);
+/* Per-launch trace of the last profiled factorization (kind: 0 small fronts,
+ * 1 assembly, 2 potrf, 3 trsm, 4 panel SYRK, 5 CB SYRK, 6 CB transfer); returns
+ * the launch count; arrays may be NULL to query it. */
+int64_t sc_numeric_launch_trace(sc_numeric* num, int32_t* kind, int32_t* level, int32_t* stream, double* ms,
+                                double* flops, int64_t cap);
 /* SYRK flops and kernel time (ms) of the last factorization restricted to
- * fronts with w >= wmin (north-star gate: wmin = 256). */
+ * fronts with w >= wmin (north-star gate: wmin = 256); wmin = 0: every CB launch;
+ * wmin = -1: the panel-update launches. */
 int64_t sc_numeric_syrk_stats(sc_numeric* num, int32_t wmin, double* flops, double* ms,
                               int64_t* launches);
 void sc_free_numeric(sc_numeric* num);
@@ -202,6 +217,10 @@ int64_t sc_dist_schedule(const sc_symbolic* sym, int32_t nranks, int32_t rank, i
  * pointers, column-major) through the fp64 MFMA SYRK kernel. */
 int64_t sc_debug_syrk(double* dC, int32_t ldc, const double* dA, int32_t lda, int32_t M, int32_t N,
                       int32_t K);
+/* Microbenchmarks (TFLOP/s): which=0 register-only fp64 MFMA probe (M blocks of
+ * 4 waves, K iterations, arg accumulators); which=1/2 the SYRK kernel on an M x M
+ * triangle with depth K, tile arg (64/128), with / without the XCD tile order. */
+int64_t sc_debug_bench(int32_t which, int32_t M, int32_t K, int32_t reps, int32_t arg, double* tflops);
 int64_t sc_device_count(void);
 /* Message of the last failing call on this thread. */
 const char* sc_last_error(void);

@@ -1,0 +1,32 @@
+"""Kernel microbenchmarks on the GPU box: fp64 MFMA ceiling and the SYRK kernel."""
+import ctypes as C
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import sparsecholesky_amd as sc  # noqa: E402
+
+
+def run(which, M, K, reps, arg):
+    t = C.c_double()
+    rc = sc.lib().sc_debug_bench(which, M, K, reps, arg, C.byref(t))
+    return round(t.value, 2) if rc == 0 else f"rc={rc}"
+
+
+def main():
+    out = {}
+    for blocks in (256, 512, 1024, 2048):
+        for nacc in (2, 4, 8):
+            out[f"peak blocks={blocks} nacc={nacc}"] = run(0, blocks, 20000, 3, nacc)
+    for M, K in ((4096, 1024), (8192, 2048), (16384, 4096), (16384, 8192)):
+        for which in (1, 2):
+            for tile in (64, 128):
+                out[f"syrk M={M} K={K} tile={tile} {'xcd' if which == 1 else 'plain'}"] = run(which, M, K, 3, tile)
+    for k, v in out.items():
+        print(f"{k:45s} {v}")
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

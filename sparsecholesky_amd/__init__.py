@@ -67,7 +67,7 @@ class Options(C.Structure):
         ("relax", C.c_int32), ("nrelax", C.c_int32 * 3), ("zrelax", C.c_double * 3),
         ("small_front_max", C.c_int32), ("panel_nb", C.c_int32), ("panel_nb_outer", C.c_int32),
         ("use_graph", C.c_int32), ("relax_wmax", C.c_int32), ("syrk_tile", C.c_int32),
-        ("reserved", C.c_int32 * 6),
+        ("lookahead", C.c_int32), ("reserved", C.c_int32 * 5),
     ]
 
 
@@ -101,6 +101,7 @@ _SIGS = [
     ("sc_flops", _D, [_P]),
     ("sc_symbolic_pattern", _I64, [_P, _P, _P]),
     ("sc_symbolic_etree", _I64, [_P, _P, _P]),
+    ("sc_symbolic_supernodes", _I64, [_P, _P, _P, _P, _P]),
     ("sc_free_symbolic", None, [_P]),
     ("sc_numeric_create", _I64, [_P, _I32, C.POINTER(_P)]),
     ("sc_factor", _I64, [_P, _P]),
@@ -110,6 +111,8 @@ _SIGS = [
     ("sc_numeric_stream", _P, [_P]),
     ("sc_numeric_set_profile", _I64, [_P, _I32]),
     ("sc_numeric_timing", _I64, [_P, _P, _I32]),
+    ("sc_numeric_level_times", _I64, [_P, _P, _I32]),
+    ("sc_numeric_launch_trace", _I64, [_P, _P, _P, _P, _P, _P, _I64]),
     ("sc_numeric_syrk_stats", _I64, [_P, _I32, C.POINTER(_D), C.POINTER(_D), C.POINTER(_I64)]),
     ("sc_free_numeric", None, [_P]),
     ("sc_solve_host", _I64, [_P, _P, _P]),
@@ -128,6 +131,7 @@ _SIGS = [
     ("sc_numeric_create_dist", _I64, [_P, _I32, _I32, _I32, _P, C.POINTER(_P)]),
     ("sc_dist_schedule", _I64, [_P, _I32, _I32, _P, _P, _P, _P, _I64]),
     ("sc_debug_syrk", _I64, [_P, _I32, _P, _I32, _I32, _I32, _I32]),
+    ("sc_debug_bench", _I64, [_I32, _I32, _I32, _I32, _I32, C.POINTER(_D)]),
     ("sc_device_count", _I64, []),
 ]
 
@@ -445,6 +449,16 @@ class Symbolic:
         _check(lib().sc_symbolic_etree(self.h, _ptr(parent), _ptr(post)), "etree")
         return parent, post
 
+    def supernodes(self):
+        """dict(start, m, w, parent, level) of the device supernode partition (postorder numbering)."""
+        ns = self.stats()["n_supernodes"]
+        st = np.zeros(ns + 1, dtype=np.int32)
+        m = np.zeros(max(ns, 1), dtype=np.int32)
+        par = np.zeros(max(ns, 1), dtype=np.int32)
+        lev = np.zeros(max(ns, 1), dtype=np.int32)
+        _check(lib().sc_symbolic_supernodes(self.h, _ptr(st), _ptr(m), _ptr(par), _ptr(lev)), "supernodes")
+        return dict(start=st, m=m[:ns], w=np.diff(st), parent=par[:ns], level=lev[:ns])
+
     def owner_map(self, nranks: int):
         ns = self.stats()["n_supernodes"]
         own = np.zeros(max(ns, 1), dtype=np.int32)
@@ -508,6 +522,19 @@ class Numeric:
         t = np.zeros(8)
         _check(lib().sc_numeric_timing(self.h, _ptr(t), 8), "timing")
         return t
+
+    def level_times(self) -> np.ndarray:
+        nl = self.symb.stats()["n_levels"]
+        t = np.zeros(max(nl, 1))
+        _check(lib().sc_numeric_level_times(self.h, _ptr(t), nl), "level_times")
+        return t[:nl]
+
+    def launch_trace(self) -> dict:
+        n = _check(lib().sc_numeric_launch_trace(self.h, None, None, None, None, None, 0), "launch_trace")
+        k, l, st = (np.zeros(max(n, 1), dtype=np.int32) for _ in range(3))
+        ms, fl = np.zeros(max(n, 1)), np.zeros(max(n, 1))
+        _check(lib().sc_numeric_launch_trace(self.h, _ptr(k), _ptr(l), _ptr(st), _ptr(ms), _ptr(fl), n), "trace")
+        return dict(kind=k[:n], level=l[:n], stream=st[:n], ms=ms[:n], flops=fl[:n])
 
     def syrk_stats(self, wmin: int = 256):
         fl, ms, nl = C.c_double(), C.c_double(), C.c_int64()

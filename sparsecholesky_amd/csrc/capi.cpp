@@ -71,8 +71,9 @@ void sc_default_options(sc_options* opt) {
     opt->panel_nb = 64;
     opt->panel_nb_outer = 256;
     opt->use_graph = 0;
-    opt->relax_wmax = 1024;
+    opt->relax_wmax = 128;
     opt->syrk_tile = 64;
+    opt->lookahead = 1;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,
@@ -126,6 +127,18 @@ int64_t sc_symbolic_etree(const sc_symbolic* sym, int32_t* parent, int32_t* post
     if (parent) std::memcpy(parent, S.parent.data(), sizeof(int32_t) * (size_t)S.n);
     if (post) std::memcpy(post, S.post.data(), sizeof(int32_t) * (size_t)S.n);
     return SC_OK;
+}
+
+int64_t sc_symbolic_supernodes(const sc_symbolic* sym, int32_t* sn_start, int32_t* sn_m, int32_t* sn_parent,
+                               int32_t* level) {
+    if (!sym) return SC_ERR_ARG;
+    const auto& S = sym->S;
+    const size_t ns = (size_t)S.ns;
+    if (sn_start) std::memcpy(sn_start, S.sn_start.data(), sizeof(int32_t) * (ns + 1));
+    if (sn_m && ns) std::memcpy(sn_m, S.sn_m.data(), sizeof(int32_t) * ns);
+    if (sn_parent && ns) std::memcpy(sn_parent, S.sn_parent.data(), sizeof(int32_t) * ns);
+    if (level && ns) std::memcpy(level, S.level.data(), sizeof(int32_t) * ns);
+    return S.ns;
 }
 
 void sc_free_symbolic(sc_symbolic* sym) { delete sym; }
@@ -197,6 +210,17 @@ int64_t sc_numeric_set_profile(sc_numeric* num, int32_t on) {
 int64_t sc_numeric_timing(sc_numeric* num, double* t, int32_t nt) {
     if (!num || !num->N || !t) return SC_ERR_ARG;
     return sc::numeric_timing(*num->N, t, nt);
+}
+
+int64_t sc_numeric_level_times(sc_numeric* num, double* ms, int32_t nl) {
+    if (!num || !num->N || !ms) return SC_ERR_ARG;
+    return sc::numeric_level_times(*num->N, ms, nl);
+}
+
+int64_t sc_numeric_launch_trace(sc_numeric* num, int32_t* kind, int32_t* level, int32_t* strm, double* ms,
+                                double* flops, int64_t cap) {
+    if (!num || !num->N) return SC_ERR_ARG;
+    return sc::numeric_launch_trace(*num->N, kind, level, strm, ms, flops, cap);
 }
 
 int64_t sc_numeric_syrk_stats(sc_numeric* num, int32_t wmin, double* flops, double* ms, int64_t* launches) {
@@ -327,6 +351,11 @@ int64_t sc_debug_syrk(double* dC, int32_t ldc, const double* dA, int32_t lda, in
                       int32_t K) {
     if (!dC || !dA || M < 0 || N < 0 || K < 0 || N > M) return SC_ERR_ARG;
     return sc::debug_syrk(dC, ldc, dA, lda, M, N, K);
+}
+
+int64_t sc_debug_bench(int32_t which, int32_t M, int32_t K, int32_t reps, int32_t arg, double* tflops) {
+    if (!tflops || M <= 0 || K <= 0 || reps <= 0) return SC_ERR_ARG;
+    return sc::debug_bench(which, M, K, reps, arg, tflops);
 }
 
 int64_t sc_device_count(void) {

@@ -118,6 +118,7 @@ __global__ __launch_bounds__(256) void assemble_large_kernel(DevPlan P, const in
     const int2 t = tasks[blockIdx.x];
     const int s = t.x;
     const int tid = threadIdx.x;
+    const int lane = tid & 63, wid = tid >> 6;
     const int c0 = P.sn_start[s];
     const int w = P.sn_start[s + 1] - c0;
     const int m = P.sn_m[s];
@@ -126,95 +127,132 @@ __global__ __launch_bounds__(256) void assemble_large_kernel(DevPlan P, const in
     const int j1 = min(m, j0 + ASM_COLS);
     double* panel = P.panel_pool + P.panel_off[s];
     double* cbs = P.cb_pool + P.cb_off[s];
-    // zero the lower part of the owned columns
-    for (int j = j0; j < j1; ++j) {
-        if (j < w) {
-            for (int r = j + tid; r < m; r += 256) panel[(int64_t)j * m + r] = 0.0;
-        } else {
-            const int jj = j - w;
-            for (int r = jj + tid; r < mb; r += 256) cbs[(int64_t)jj * mb + r] = 0.0;
-        }
+    // zero the lower part of the owned columns: one wave per column
+    for (int j = j0 + wid; j < j1; j += 4) {
+        double* col = (j < w) ? panel + (int64_t)j * m : cbs + (int64_t)(j - w) * mb - w;
+#pragma unroll 4
+        for (int r = j + lane; r < m; r += 64) col[r] = 0.0;
     }
     __syncthreads();
-    for (int j = j0; j < min(j1, w); ++j) {
+    for (int j = j0 + wid; j < min(j1, w); j += 4) {
         const int64_t a0 = P.a_ptr[c0 + j], a1 = P.a_ptr[c0 + j + 1];
-        for (int64_t q = a0 + tid; q < a1; q += 256) panel[(int64_t)j * m + P.a_pos[q]] = Ax[P.a_src[q]];
+        for (int64_t q = a0 + lane; q < a1; q += 64) panel[(int64_t)j * m + P.a_pos[q]] = Ax[P.a_src[q]];
     }
     __syncthreads();
+    // extend-add: children in fixed order; within a child, one wave per child
+    // column (relative indices are injective, so columns never collide)
     for (int ci = P.child_ptr[s]; ci < P.child_ptr[s + 1]; ++ci) {
         const int c = P.child_list[ci];
         const int mbc = P.sn_m[c] - (P.sn_start[c + 1] - P.sn_start[c]);
-        const int32_t* rel = P.relind + P.rel_ptr[c];
-        const double* cb = P.cb_pool + P.cb_off[c];
+        const int32_t* __restrict__ rel = P.relind + P.rel_ptr[c];
+        const double* __restrict__ cb = P.cb_pool + P.cb_off[c];
         const int jlo = lower_bound_i32(rel, mbc, j0);
         const int jhi = lower_bound_i32(rel, mbc, j1);
-        for (int jc = jlo; jc < jhi; ++jc) {
+        for (int jc = jlo + wid; jc < jhi; jc += 4) {
             const int pj = rel[jc];
-            const double* src = cb + (int64_t)jc * mbc;
-            if (pj < w) {
-                double* dst = panel + (int64_t)pj * m;
-                for (int ic = jc + tid; ic < mbc; ic += 256) dst[rel[ic]] += src[ic];
-            } else {
-                double* dst = cbs + (int64_t)(pj - w) * mb - w;
-                for (int ic = jc + tid; ic < mbc; ic += 256) dst[rel[ic]] += src[ic];
-            }
+            const double* __restrict__ src = cb + (int64_t)jc * mbc;
+            double* dst = (pj < w) ? panel + (int64_t)pj * m : cbs + (int64_t)(pj - w) * mb - w;
+#pragma unroll 4
+            for (int ic = jc + lane; ic < mbc; ic += 64) dst[rel[ic]] += src[ic];
         }
         __syncthreads();
     }
 }
 
+// Wave-uniform broadcast of lane `src`'s double (two v_readlane_b32).
+__device__ __forceinline__ double readlane_f64(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), src);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Step J of the register-resident right-looking Cholesky of a <= 64 x 64 block
+// (lane = row).  Template recursion forces full unrolling so r[] keeps static
+// register indices (a rolled loop turns them into select chains).
+template <int J>
+__device__ __forceinline__ void potrf_steps(double (&r)[PNB], double* colj, int lane, int nb, int32_t* info,
+                                            int col0) {
+    if constexpr (J < PNB) {
+        if (J < nb) {
+            const double d = readlane_f64(r[J], J);
+            if (lane == 0 && !(d > 0.0)) report_fail(info, col0 + J);
+            const double piv = sqrt(d);
+            const double inv = 1.0 / piv;
+            const double rj = (lane == J) ? piv : r[J] * inv;
+            r[J] = rj;
+            colj[lane] = rj;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int q = J + 1; q < PNB; ++q) r[q] = fma(-rj, colj[q], r[q]);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            potrf_steps<J + 1>(r, colj, lane, nb, info, col0);
+        }
+    }
+}
+
+// One wave factors the nb x nb (nb <= 64) lower block at `blk` (ld) in place.
+__device__ __forceinline__ void potrf_block_wave(double* blk, int64_t ld, int nb, int lane, double* colj,
+                                                 int32_t* info, int col0) {
+    const bool live = lane < nb;
+    double r[PNB];
+#pragma unroll
+    for (int c = 0; c < PNB; ++c) r[c] = (live && c <= lane) ? blk[(int64_t)c * ld + lane] : 0.0;
+    potrf_steps<0>(r, colj, lane, nb, info, col0);
+    if (live) {
+#pragma unroll
+        for (int c = 0; c < PNB; ++c)
+            if (c < nb && c <= lane) blk[(int64_t)c * ld + lane] = r[c];
+    }
+}
+
 // ---------------------------------------------------------------------------
-// Large fronts, diagonal block POTRF (nb <= 64): one workgroup per front.
+// Large fronts, diagonal block POTRF (nb <= 64), one wave per front: lane i keeps
+// row i in registers; the pivot is broadcast with v_readlane, column j through
+// LDS; entries above the diagonal carry harmless garbage and are never stored.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void potrf_diag_kernel(DevPlan P, const int2* __restrict__ tasks) {
-    __shared__ double D[PNB * (PNB + 1)];
-    __shared__ double s_piv;
+__global__ __launch_bounds__(64) void potrf_diag_kernel(DevPlan P, const int2* __restrict__ tasks) {
+    __shared__ double colj[PNB];
     const int2 t = tasks[blockIdx.x];
     const int s = t.x, k0 = t.y;
-    const int tid = threadIdx.x;
     const int c0 = P.sn_start[s];
     const int w = P.sn_start[s + 1] - c0;
     const int m = P.sn_m[s];
     const int nb = min(PNB, w - k0);
-    constexpr int LD = PNB + 1;
     double* blk = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m + k0;
-    for (int idx = tid; idx < nb * nb; idx += 256) {
-        const int r = idx % nb, c = idx / nb;
-        D[c * LD + r] = (r >= c) ? blk[(int64_t)c * m + r] : 0.0;
-    }
-    __syncthreads();
-    const int i = tid % PNB, g = tid / PNB;  // 4 column groups
-    for (int k = 0; k < nb; ++k) {
-        if (tid == 0) {
-            double d = D[k * LD + k];
-            if (!(d > 0.0)) report_fail(P.info, c0 + k0 + k);
-            s_piv = sqrt(d);
-            D[k * LD + k] = s_piv;
+    potrf_block_wave(blk, m, nb, threadIdx.x, colj, P.info, c0 + k0);
+}
+
+// Forward substitution steps of one row against L11 (column-major in LDS).
+template <int J>
+__device__ __forceinline__ void trsm_steps(double (&r)[PNB], const double* Lc, const double* invd, int nb) {
+    constexpr int LD = PNB + 2;
+    if constexpr (J < PNB) {
+        if (J < nb) {
+            const double rj = r[J] * invd[J];
+            r[J] = rj;
+#pragma unroll
+            for (int q = J + 1; q < PNB; ++q) r[q] = fma(-rj, Lc[J * LD + q], r[q]);
+            trsm_steps<J + 1>(r, Lc, invd, nb);
         }
-        __syncthreads();
-        const double dk = s_piv;
-        if (tid > k && tid < nb) D[k * LD + tid] = D[k * LD + tid] / dk;
-        __syncthreads();
-        if (i > k && i < nb) {
-            const double lik = D[k * LD + i];
-            for (int j = k + 1 + g; j <= i; j += 4) D[j * LD + i] -= lik * D[k * LD + j];
-        }
-        __syncthreads();
-    }
-    for (int idx = tid; idx < nb * nb; idx += 256) {
-        const int r = idx % nb, c = idx / nb;
-        if (r >= c) blk[(int64_t)c * m + r] = D[c * LD + r];
     }
 }
 
 // ---------------------------------------------------------------------------
-// Large fronts, panel TRSM: X := X * L11^{-T} for a 64-row block below the
-// diagonal block.  tasks = (s, k0, r0): rows [r0, min(m, r0+64)).
+// Large fronts, panel TRSM: X := X * L11^{-T} for rows below the diagonal block.
+// One lane per row (256 rows per workgroup), the row in registers; right-looking
+// substitution x_j *= 1/L(j,j), x_q -= x_j L(q,j) for q > j (independent FMAs).
+// L11 columns and the reciprocal diagonal are broadcast from LDS; no barriers
+// inside the solve.  tasks = (s, k0, r0): rows [r0, min(m, r0 + TRSM_ROWS)).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void trsm_panel_kernel(DevPlan P, const int4* __restrict__ tasks) {
-    constexpr int LD = PNB + 1;
-    __shared__ double L[PNB * LD];
-    __shared__ double X[PNB * LD];  // X[col * LD + row]
+    constexpr int LD = PNB + 2;
+    __shared__ double Lc[PNB * LD];  // Lc[j * LD + q] = L11(q, j), column-major
+    __shared__ double invd[PNB];
     const int4 t = tasks[blockIdx.x];
     const int s = t.x, k0 = t.y, r0 = t.z;
     const int tid = threadIdx.x;
@@ -222,31 +260,26 @@ __global__ __launch_bounds__(256) void trsm_panel_kernel(DevPlan P, const int4* 
     const int w = P.sn_start[s + 1] - c0;
     const int m = P.sn_m[s];
     const int nb = min(PNB, w - k0);
-    const int nr = min(TRSM_ROWS, m - r0);
-    const double* pan = P.panel_pool + P.panel_off[s];
+    double* pan = P.panel_pool + P.panel_off[s];
     const double* blk = pan + (int64_t)k0 * m + k0;
-    for (int idx = tid; idx < nb * nb; idx += 256) {
-        const int r = idx % nb, c = idx / nb;
-        L[c * LD + r] = (r >= c) ? blk[(int64_t)c * m + r] : 0.0;
-    }
-    const double* xs = pan + (int64_t)k0 * m + r0;
-    for (int idx = tid; idx < nb * TRSM_ROWS; idx += 256) {
-        const int r = idx % TRSM_ROWS, c = idx / TRSM_ROWS;
-        X[c * LD + r] = (r < nr) ? xs[(int64_t)c * m + r] : 0.0;
+    for (int idx = tid; idx < PNB * PNB; idx += 256) {
+        const int q = idx % PNB, j = idx / PNB;
+        const double v = (q < nb && j < nb && j <= q) ? blk[(int64_t)j * m + q] : 0.0;
+        Lc[j * LD + q] = v;
+        if (q == j) invd[j] = (j < nb) ? 1.0 / v : 0.0;
     }
     __syncthreads();
-    const int r = tid % TRSM_ROWS, g = tid / TRSM_ROWS;
-    for (int j = 0; j < nb; ++j) {
-        if (g == 0) X[j * LD + r] = X[j * LD + r] / L[j * LD + j];
-        __syncthreads();
-        const double xj = X[j * LD + r];
-        for (int jj = j + 1 + g; jj < nb; jj += 4) X[jj * LD + r] -= xj * L[j * LD + jj];
-        __syncthreads();
-    }
-    double* xd = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m + r0;
-    for (int idx = tid; idx < nb * TRSM_ROWS; idx += 256) {
-        const int rr = idx % TRSM_ROWS, c = idx / TRSM_ROWS;
-        if (rr < nr) xd[(int64_t)c * m + rr] = X[c * LD + rr];
+    const int row = r0 + tid;
+    const bool live = row < m;
+    double* xs = pan + (int64_t)k0 * m + (live ? row : r0);
+    double r[PNB];
+#pragma unroll
+    for (int c = 0; c < PNB; ++c) r[c] = (live && c < nb) ? xs[(int64_t)c * m] : 0.0;
+    trsm_steps<0>(r, Lc, invd, nb);
+    if (live) {
+#pragma unroll
+        for (int c = 0; c < PNB; ++c)
+            if (c < nb) xs[(int64_t)c * m] = r[c];
     }
 }
 
@@ -257,41 +290,18 @@ __global__ __launch_bounds__(256) void trsm_panel_kernel(DevPlan P, const int4* 
 // A (M x K) and the B operand (its first N rows) share one column-major array.
 // ---------------------------------------------------------------------------
 template <int BT, int TAG>
-__global__ __launch_bounds__(256) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks, int ntasks) {
+__global__ __launch_bounds__(256) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
+                                                         const int2* __restrict__ tiles) {
     constexpr int BK = 16;
     constexpr int LDT = BT + 16;  // +128 B row pad: the two k-rows read by a half-wave hit disjoint banks
     constexpr int RT = BT / 32;   // 16x16 MFMA tiles per wave per dimension
     __shared__ double As[2][BK * LDT];
     __shared__ double Bs[2][BK * LDT];
 
-    // locate the task (tasks sorted by tile_base)
-    const int bid = blockIdx.x;
-    int lo = 0, hi = ntasks - 1;
-    while (lo < hi) {
-        int mid = (lo + hi + 1) >> 1;
-        if (tasks[mid].tile_base <= bid)
-            lo = mid;
-        else
-            hi = mid - 1;
-    }
-    const GemmTask T = tasks[lo];
-    int idx = bid - T.tile_base;
-    // lower-trapezoid enumeration, column-major over tile columns: column tj has (TM - tj) tiles
-    const int TM = (T.M + BT - 1) / BT;
-    int tj = 0;
-    {
-        // closed form then fix-up: S(tj) = tj*TM - tj*(tj-1)/2
-        const double a = 2.0 * TM + 1.0;
-        double disc = a * a - 8.0 * (double)idx;
-        int guess = (int)floor((a - sqrt(disc > 0 ? disc : 0.0)) * 0.5);
-        if (guess < 0) guess = 0;
-        auto S = [&](int c) { return (int64_t)c * TM - (int64_t)c * (c - 1) / 2; };
-        while (guess > 0 && S(guess) > idx) --guess;
-        while (S(guess + 1) <= idx) ++guess;
-        tj = guess;
-        idx -= (int)S(tj);
-    }
-    const int ti = tj + idx;
+    // host-ordered tile list: blocks sharing an XCD walk a contiguous, L2-blocked run of tiles
+    const int2 tl = tiles[blockIdx.x];
+    const GemmTask T = tasks[tl.x];
+    const int ti = tl.y >> 16, tj = tl.y & 0xffff;
     const int row0 = ti * BT, col0 = tj * BT;
 
     const int tid = threadIdx.x;
@@ -391,7 +401,7 @@ hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count,
 
 hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hipStream_t st) {
     if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(potrf_diag_kernel, dim3(count), dim3(256), 0, st, P, tasks);
+    hipLaunchKernelGGL(potrf_diag_kernel, dim3(count), dim3(64), 0, st, P, tasks);
     return hipGetLastError();
 }
 
@@ -402,19 +412,46 @@ hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hip
 }
 
 // TAG only separates the launches in profiles: 0 = panel update, 1 = CB update.
-hipError_t launch_syrk(const GemmTask* tasks, int ntasks, int total_tiles, int bt, int tag, hipStream_t st) {
+hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st) {
     if (total_tiles <= 0) return hipSuccess;
     if (bt == 128) {
         if (tag)
-            hipLaunchKernelGGL((syrk_mfma_kernel<128, 1>), dim3(total_tiles), dim3(256), 0, st, tasks, ntasks);
+            hipLaunchKernelGGL((syrk_mfma_kernel<128, 1>), dim3(total_tiles), dim3(256), 0, st, tasks, tiles);
         else
-            hipLaunchKernelGGL((syrk_mfma_kernel<128, 0>), dim3(total_tiles), dim3(256), 0, st, tasks, ntasks);
+            hipLaunchKernelGGL((syrk_mfma_kernel<128, 0>), dim3(total_tiles), dim3(256), 0, st, tasks, tiles);
     } else {
         if (tag)
-            hipLaunchKernelGGL((syrk_mfma_kernel<64, 1>), dim3(total_tiles), dim3(256), 0, st, tasks, ntasks);
+            hipLaunchKernelGGL((syrk_mfma_kernel<64, 1>), dim3(total_tiles), dim3(256), 0, st, tasks, tiles);
         else
-            hipLaunchKernelGGL((syrk_mfma_kernel<64, 0>), dim3(total_tiles), dim3(256), 0, st, tasks, ntasks);
+            hipLaunchKernelGGL((syrk_mfma_kernel<64, 0>), dim3(total_tiles), dim3(256), 0, st, tasks, tiles);
     }
+    return hipGetLastError();
+}
+
+// Peak probe: independent fp64 MFMA chains, operands in registers.
+template <int NACC>
+__global__ __launch_bounds__(256) void mfma_peak_kernel(double* out, int iters) {
+    double4_t acc[NACC];
+#pragma unroll
+    for (int j = 0; j < NACC; ++j) acc[j] = (double4_t){0.0, 0.0, 0.0, 0.0};
+    const double a = 1.0 + threadIdx.x * 1e-9, b = 1.0 - blockIdx.x * 1e-9;
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int j = 0; j < NACC; ++j) acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[j], 0, 0, 0);
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < NACC; ++j) s += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];
+    if (s == 1234.5) out[blockIdx.x] = s;  // keep the chain live
+}
+
+hipError_t launch_mfma_peak(double* out, int blocks, int iters, int nacc, hipStream_t st) {
+    if (nacc == 8)
+        hipLaunchKernelGGL((mfma_peak_kernel<8>), dim3(blocks), dim3(256), 0, st, out, iters);
+    else if (nacc == 2)
+        hipLaunchKernelGGL((mfma_peak_kernel<2>), dim3(blocks), dim3(256), 0, st, out, iters);
+    else
+        hipLaunchKernelGGL((mfma_peak_kernel<4>), dim3(blocks), dim3(256), 0, st, out, iters);
     return hipGetLastError();
 }
 

@@ -4,15 +4,16 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 namespace sc {
 
 // Inner panel width (POTRF/TRSM block); the diagonal block lives in LDS.
 constexpr int PNB = 64;
-// Rows per TRSM workgroup.
-constexpr int TRSM_ROWS = 64;
-// Columns owned by one assembly workgroup.
-constexpr int ASM_COLS = 64;
+// Rows per TRSM workgroup (one lane per row).
+constexpr int TRSM_ROWS = 256;
+// Columns owned by one assembly workgroup (one wave per column at a time).
+constexpr int ASM_COLS = 16;
 // Output tile edges of the MFMA SYRK kernel (per launch).
 constexpr int SYRK_BT_SMALL = 64;
 constexpr int SYRK_BT_LARGE = 128;
@@ -46,7 +47,7 @@ struct GemmTask {
     int64_t ldc;
     int64_t lda;
     int32_t M, N, K;
-    int32_t tile_base;  // first tile index of this task within its launch
+    int32_t pad;
 };
 
 hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count, int maxm, const double* Ax,
@@ -55,12 +56,20 @@ hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count,
                                  hipStream_t st);
 hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hipStream_t st);
 hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st);
-hipError_t launch_syrk(const GemmTask* tasks, int ntasks, int total_tiles, int bt, int tag, hipStream_t st);
+hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st);
+hipError_t launch_mfma_peak(double* out, int blocks, int iters, int nacc, hipStream_t st);
 
 // tiles of an M x N lower trapezoid with square BT tiles
 inline int64_t syrk_tiles(int64_t M, int64_t N, int bt) {
     const int64_t TM = (M + bt - 1) / bt, TN = (N + bt - 1) / bt;
     return TN * TM - TN * (TN - 1) / 2;
 }
+
+// Append the lower-trapezoid tiles of `task` as {task, ti<<16 | tj}, walking
+// G x G super-tiles so that consecutive tiles share row and column panels.
+void append_tiles(std::vector<int2>& out, int task, int M, int N, int bt, int G = 8);
+// Permute a launch's tile run so block b (XCD b % 8 under round-robin dispatch)
+// takes a contiguous chunk: neighbouring tiles share one XCD's L2.
+void xcd_order(int2* tiles, int64_t n);
 
 }  // namespace sc

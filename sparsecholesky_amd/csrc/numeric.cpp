@@ -73,9 +73,28 @@ static int bucket_of(int m) {
 
 // Build the static launch schedule (host).  Task pointers into the pools are
 // final device addresses, so the schedule can be replayed or graph-captured.
+void append_tiles(std::vector<int2>& out, int task, int M, int N, int bt, int G) {
+    const int TM = (M + bt - 1) / bt, TN = (N + bt - 1) / bt;
+    for (int sj = 0; sj < TN; sj += G)
+        for (int si = sj; si < TM; si += G)
+            for (int tj = sj; tj < std::min(TN, sj + G); ++tj)
+                for (int ti = std::max(si, tj); ti < std::min(TM, si + G); ++ti)
+                    out.push_back(make_int2(task, (ti << 16) | tj));
+}
+
+void xcd_order(int2* tiles, int64_t n) {
+    if (n <= 8) return;
+    std::vector<int2> src(tiles, tiles + n);
+    const int64_t q = n / 8, r = n % 8;
+    for (int64_t b = 0; b < n; ++b) {
+        const int64_t x = b % 8, j = b / 8;
+        tiles[b] = src[x * q + std::min(x, r) + j];
+    }
+}
+
 static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vector<int2>& asmv,
                               std::vector<int2>& potrf, std::vector<int4>& trsm,
-                              std::vector<GemmTask>& gemm) {
+                              std::vector<GemmTask>& gemm, std::vector<int2>& tiles) {
     const Symbolic& S = *N.S;
     const int NBO = std::max(PNB, (S.opt.panel_nb_outer / PNB) * PNB);
     std::vector<std::vector<int32_t>> by_level((size_t)S.nlevels);
@@ -83,26 +102,43 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
     double* panel_pool = N.P.panel_pool;
     double* cb_pool = N.P.cb_pool;
     auto push_gemm_launch = [&](int kind, int level, const std::vector<GemmTask>& tasks, int big,
-                                double flops) {
+                                double flops, int strm = 0) {
         if (tasks.empty()) return;
         Launch L {};
         L.kind = kind;
         L.level = level;
+        L.strm = strm;
         L.off = (int64_t)gemm.size();
         // 128x128 tiles when every task is at least 256 wide (little edge waste)
         int minN = INT32_MAX;
         for (auto& t : tasks) minN = std::min(minN, (int)t.N);
         L.bt = (S.opt.syrk_tile == 128 && minN >= 256) ? SYRK_BT_LARGE : SYRK_BT_SMALL;
-        int64_t tiles = 0;
-        for (auto t : tasks) {
-            t.tile_base = (int32_t)tiles;
-            tiles += syrk_tiles(t.M, t.N, L.bt);
-            gemm.push_back(t);
+        L.toff = (int64_t)tiles.size();
+        for (size_t q = 0; q < tasks.size(); ++q) {
+            append_tiles(tiles, (int)q, tasks[q].M, tasks[q].N, L.bt);
+            gemm.push_back(tasks[q]);
         }
-        L.count = (int32_t)tiles;
+        L.count = (int32_t)((int64_t)tiles.size() - L.toff);
+        xcd_order(tiles.data() + L.toff, L.count);
         L.ntasks = (int32_t)tasks.size();
         L.big = big;
         L.flops = flops;
+        N.sched.push_back(L);
+    };
+    // cross-stream dependencies: record an event on a stream / make a stream wait on it
+    auto push_record = [&](int strm) -> int {
+        Launch L {};
+        L.kind = L_RECORD;
+        L.strm = strm;
+        L.count = N.n_sync_events++;
+        N.sched.push_back(L);
+        return L.count;
+    };
+    auto push_wait = [&](int strm, int ev) {
+        Launch L {};
+        L.kind = L_WAIT;
+        L.strm = strm;
+        L.count = ev;
         N.sched.push_back(L);
     };
     // one level's fronts (already filtered to the ranks this process runs)
@@ -137,6 +173,25 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         }
         int maxw = 0;
         for (int32_t s : large) maxw = std::max(maxw, S.w(s));
+        // Lookahead: at a slab end the outer rank-NBO update is split into the next
+        // slab's columns (stream 0, needed by the next POTRF/TRSM) and the rest
+        // (stream 1), which overlaps the next slab's factorization.  A later outer
+        // update of overlapping columns waits for the stream-1 work first.
+        int b_pending = -1;
+        auto add_update = [&](std::vector<GemmTask>& v, double& fl, double* pan, int m, int c_lo, int c_hi, int ka,
+                              int kb) {
+            if (c_hi <= c_lo || kb <= ka) return;
+            GemmTask t {};
+            t.C = pan + (int64_t)c_lo * m + c_lo;
+            t.A = pan + (int64_t)ka * m + c_lo;
+            t.ldc = m;
+            t.lda = m;
+            t.M = m - c_lo;
+            t.N = c_hi - c_lo;
+            t.K = kb - ka;
+            v.push_back(t);
+            fl += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
+        };
         for (int k0 = 0; k0 < maxw; k0 += PNB) {
             Launch Lp {};
             Lp.kind = L_POTRF;
@@ -146,8 +201,8 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             Lt.kind = L_TRSM;
             Lt.level = lev;
             Lt.off = (int64_t)trsm.size();
-            std::vector<GemmTask> upd;
-            double uflops = 0.0;
+            std::vector<GemmTask> upd, outer_a, outer_b;
+            double uflops = 0.0, afl = 0.0, bfl = 0.0;
             for (int32_t s : large) {
                 const int w = S.w(s), m = S.sn_m[s];
                 if (w <= k0) continue;
@@ -159,27 +214,11 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
                 const int slab0 = (k0 / NBO) * NBO;
                 const int slab1 = std::min(w, slab0 + NBO);
                 if (k1 < slab1) {
-                    GemmTask t {};
-                    t.C = pan + (int64_t)k1 * m + k1;
-                    t.A = pan + (int64_t)k0 * m + k1;
-                    t.ldc = m;
-                    t.lda = m;
-                    t.M = m - k1;
-                    t.N = slab1 - k1;
-                    t.K = k1 - k0;
-                    upd.push_back(t);
-                    uflops += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
+                    add_update(upd, uflops, pan, m, k1, slab1, k0, k1);
                 } else if (k1 == slab1 && slab1 < w) {
-                    GemmTask t {};
-                    t.C = pan + (int64_t)slab1 * m + slab1;
-                    t.A = pan + (int64_t)slab0 * m + slab1;
-                    t.ldc = m;
-                    t.lda = m;
-                    t.M = m - slab1;
-                    t.N = w - slab1;
-                    t.K = slab1 - slab0;
-                    upd.push_back(t);
-                    uflops += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
+                    const int nxt = S.opt.lookahead ? std::min(w, slab1 + NBO) : w;
+                    add_update(outer_a, afl, pan, m, slab1, nxt, slab0, slab1);
+                    add_update(outer_b, bfl, pan, m, nxt, w, slab0, slab1);
                 }
             }
             Lp.count = (int32_t)((int64_t)potrf.size() - Lp.off);
@@ -187,7 +226,22 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             if (Lp.count > 0) N.sched.push_back(Lp);
             if (Lt.count > 0) N.sched.push_back(Lt);
             push_gemm_launch(L_PANEL, lev, upd, 0, uflops);
+            int e_trsm = -1;
+            if (!outer_b.empty()) e_trsm = push_record(0);
+            if (!outer_a.empty()) {
+                if (b_pending >= 0) {
+                    push_wait(0, b_pending);
+                    b_pending = -1;
+                }
+                push_gemm_launch(L_PANEL, lev, outer_a, 0, afl);
+            }
+            if (!outer_b.empty()) {
+                push_wait(1, e_trsm);
+                push_gemm_launch(L_PANEL, lev, outer_b, 0, bfl, 1);
+                b_pending = push_record(1);
+            }
         }
+        if (b_pending >= 0) push_wait(0, b_pending);
         // contribution-block SYRK, K = w; fronts with w >= 256 in their own launch
         for (int big = 1; big >= 0; --big) {
             std::vector<GemmTask> cbt;
@@ -286,7 +340,24 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
         N.err = "hipSetDevice failed";
         return fail(SC_ERR_HIP);
     }
-    if (hipStreamCreateWithFlags(&N.stream, hipStreamNonBlocking) != hipSuccess) {
+    // critical path (assembly, POTRF/TRSM chain, next-slab updates) on the high
+    // priority stream; the overlapped trailing updates on the low priority one
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    bool ok = hipStreamCreateWithPriority(&N.stream, hipStreamNonBlocking, prio_hi) == hipSuccess;
+    if (ok && S.opt.lookahead == 2) {
+        // trailing updates may not use every 8th CU: the critical path always finds room
+        hipDeviceProp_t prop;
+        (void)hipGetDeviceProperties(&prop, device);
+        const int ncu = prop.multiProcessorCount;
+        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+        for (int c = 0; c < ncu; ++c)
+            if (c % 8 != 7) mask[c / 32] |= 1u << (c % 32);
+        ok = hipExtStreamCreateWithCUMask(&N.stream2, (uint32_t)mask.size(), mask.data()) == hipSuccess;
+    } else if (ok) {
+        ok = hipStreamCreateWithPriority(&N.stream2, hipStreamNonBlocking, prio_lo) == hipSuccess;
+    }
+    if (!ok) {
         N.err = "hipStreamCreate failed";
         return fail(SC_ERR_HIP);
     }
@@ -326,10 +397,17 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     std::vector<int2> asmv, potrf;
     std::vector<int4> trsm;
     std::vector<GemmTask> gemm;
-    if ((rc = build_schedule(N, small, asmv, potrf, trsm, gemm))) return fail(rc);
+    std::vector<int2> tiles;
+    if ((rc = build_schedule(N, small, asmv, potrf, trsm, gemm, tiles))) return fail(rc);
+    N.sync_ev.assign((size_t)N.n_sync_events, nullptr);
+    for (auto& e : N.sync_ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            N.err = "hipEventCreate failed";
+            return fail(SC_ERR_HIP);
+        }
     if ((rc = upload(N, small, N.d_small)) || (rc = upload(N, asmv, N.d_asm)) ||
         (rc = upload(N, potrf, N.d_potrf)) || (rc = upload(N, trsm, N.d_trsm)) ||
-        (rc = upload(N, gemm, N.d_gemm)))
+        (rc = upload(N, gemm, N.d_gemm)) || (rc = upload(N, tiles, N.d_tiles)))
         return fail(rc);
     return SC_OK;
 }
@@ -337,7 +415,12 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
 hipError_t comm_launch(Numeric& N, const Launch& L);  // dist.cpp
 
 static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
+    hipStream_t st = L.strm ? N.stream2 : N.stream;
     switch (L.kind) {
+        case L_RECORD:
+            return hipEventRecord(N.sync_ev[L.count], st);
+        case L_WAIT:
+            return hipStreamWaitEvent(st, N.sync_ev[L.count], 0);
         case L_SMALL:
             return launch_front_small(N.P, N.d_small + L.off, L.count, L.maxm, d_Ax, N.stream);
         case L_ASM:
@@ -348,7 +431,7 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
             return launch_trsm_panel(N.P, N.d_trsm + L.off, L.count, N.stream);
         case L_PANEL:
         case L_CB:
-            return launch_syrk(N.d_gemm + L.off, L.ntasks, L.count, L.bt, L.kind == L_CB ? 1 : 0, N.stream);
+            return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st);
         case L_COMM:
             return comm_launch(N, L);
     }
@@ -358,9 +441,12 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
 static int64_t enqueue_all(Numeric& N, const double* d_Ax, bool with_events) {
     HIP_TRY(hipMemsetAsync(N.P.info, 0x7f, sizeof(int32_t), N.stream));
     for (size_t i = 0; i < N.sched.size(); ++i) {
-        if (with_events) HIP_TRY(hipEventRecord(N.ev[2 * i], N.stream));
-        HIP_TRY(launch_one(N, N.sched[i], d_Ax));
-        if (with_events) HIP_TRY(hipEventRecord(N.ev[2 * i + 1], N.stream));
+        const Launch& L = N.sched[i];
+        const bool timed = with_events && L.kind < L_RECORD;
+        hipStream_t st = L.strm ? N.stream2 : N.stream;
+        if (timed) HIP_TRY(hipEventRecord(N.ev[2 * i], st));
+        HIP_TRY(launch_one(N, L, d_Ax));
+        if (timed) HIP_TRY(hipEventRecord(N.ev[2 * i + 1], st));
     }
     return SC_OK;
 }
@@ -421,6 +507,7 @@ int64_t numeric_status(Numeric& N) {
         std::memset(N.phase_ms, 0, sizeof(N.phase_ms));
         hipEvent_t first = nullptr, last = nullptr;
         for (size_t i = 0; i < N.sched.size(); ++i) {
+            if (N.sched[i].kind >= L_RECORD) continue;
             float ms = 0.f;
             HIP_TRY(hipEventElapsedTime(&ms, N.ev[2 * i], N.ev[2 * i + 1]));
             int slot = 0;
@@ -434,8 +521,10 @@ int64_t numeric_status(Numeric& N) {
                 case L_COMM: slot = 1; break;
             }
             N.phase_ms[slot] += ms;
-            if (!first) first = N.ev[2 * i];
-            last = N.ev[2 * i + 1];
+            if (N.sched[i].strm == 0) {
+                if (!first) first = N.ev[2 * i];
+                last = N.ev[2 * i + 1];
+            }
         }
         if (first) {
             float tot = 0.f;
@@ -446,6 +535,47 @@ int64_t numeric_status(Numeric& N) {
     return N.status;
 }
 
+// Wall time per assembly-tree level (first main-stream launch start to last end).
+int64_t numeric_level_times(Numeric& N, double* ms, int nl) {
+    if (!N.profile || !N.status_valid) return SC_ERR_STATE;
+    const int L = N.S->nlevels;
+    std::vector<int> first(L, -1), last(L, -1);
+    for (size_t i = 0; i < N.sched.size(); ++i) {
+        const Launch& l = N.sched[i];
+        if (l.kind >= L_RECORD || l.strm != 0) continue;
+        if (first[l.level] < 0) first[l.level] = (int)i;
+        last[l.level] = (int)i;
+    }
+    for (int v = 0; v < L && v < nl; ++v) {
+        float t = 0.f;
+        if (first[v] >= 0) HIP_TRY(hipEventElapsedTime(&t, N.ev[2 * first[v]], N.ev[2 * last[v] + 1]));
+        ms[v] = t;
+    }
+    return L;
+}
+
+// Per-launch trace of the last profiled factorization: kind, level, stream, ms, flops.
+int64_t numeric_launch_trace(Numeric& N, int32_t* kind, int32_t* level, int32_t* strm, double* ms, double* flops,
+                             int64_t cap) {
+    if (!N.profile || !N.status_valid) return SC_ERR_STATE;
+    int64_t n = 0;
+    for (size_t i = 0; i < N.sched.size(); ++i) {
+        const Launch& l = N.sched[i];
+        if (l.kind >= L_RECORD) continue;
+        if (n < cap && kind) {
+            float t = 0.f;
+            HIP_TRY(hipEventElapsedTime(&t, N.ev[2 * i], N.ev[2 * i + 1]));
+            kind[n] = l.kind;
+            level[n] = l.level;
+            strm[n] = l.strm;
+            ms[n] = t;
+            flops[n] = l.flops;
+        }
+        ++n;
+    }
+    return n;
+}
+
 int64_t numeric_timing(Numeric& N, double* t, int nt) {
     if (!N.profile || !N.status_valid) return SC_ERR_STATE;
     for (int i = 0; i < nt && i < 8; ++i) t[i] = N.phase_ms[i];
@@ -453,13 +583,14 @@ int64_t numeric_timing(Numeric& N, double* t, int nt) {
 }
 
 int64_t numeric_syrk_stats(Numeric& N, int wmin, double* flops, double* ms, int64_t* launches) {
-    // CB SYRK launches are split by w >= 256; wmin selects them (wmin <= 0: all CB launches)
+    // CB SYRK launches are split by w >= 256; wmin selects them (0: all CB launches,
+    // -1: the panel-update launches instead)
     double fl = 0.0, t = 0.0;
     int64_t cnt = 0;
     const bool have_t = N.profile && N.status_valid && N.ev.size() == 2 * N.sched.size();
     for (size_t i = 0; i < N.sched.size(); ++i) {
         const Launch& L = N.sched[i];
-        if (L.kind != L_CB) continue;
+        if (L.kind != (wmin < 0 ? L_PANEL : L_CB)) continue;
         if (wmin >= 256 && !L.big) continue;
         fl += L.flops;
         ++cnt;
@@ -501,9 +632,12 @@ void numeric_free(Numeric* Np) {
     if (N.graph) (void)hipGraphDestroy(N.graph);
     for (auto e : N.ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto e : N.sync_ev)
+        if (e) (void)hipEventDestroy(e);
     for (void* p : N.allocs) (void)hipFree(p);
     if (N.d_Ax_owned) (void)hipFree(N.d_Ax_owned);
     if (N.stream) (void)hipStreamDestroy(N.stream);
+    if (N.stream2) (void)hipStreamDestroy(N.stream2);
     delete Np;
 }
 
@@ -516,18 +650,92 @@ int64_t debug_syrk(double* dC, int ldc, const double* dA, int lda, int M, int Nn
     t.M = M;
     t.N = Nn;
     t.K = K;
-    t.tile_base = 0;
+    const int bt = SYRK_BT_SMALL;
+    std::vector<int2> tiles;
+    append_tiles(tiles, 0, M, Nn, bt);
+    xcd_order(tiles.data(), (int64_t)tiles.size());
     GemmTask* d = nullptr;
+    int2* dt = nullptr;
     if (hipMalloc(&d, sizeof(GemmTask)) != hipSuccess) return SC_ERR_DEVMEM;
-    if (hipMemcpy(d, &t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMalloc(&dt, std::max<size_t>(tiles.size(), 1) * sizeof(int2)) != hipSuccess) {
         (void)hipFree(d);
-        return SC_ERR_HIP;
+        return SC_ERR_DEVMEM;
     }
-    const int bt = (Nn >= 256) ? SYRK_BT_LARGE : SYRK_BT_SMALL;
-    hipError_t e = launch_syrk(d, 1, (int)syrk_tiles(M, Nn, bt), bt, 0, nullptr);
+    hipError_t e = hipMemcpy(d, &t, sizeof(t), hipMemcpyHostToDevice);
+    if (e == hipSuccess && !tiles.empty())
+        e = hipMemcpy(dt, tiles.data(), tiles.size() * sizeof(int2), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_syrk(d, dt, (int)tiles.size(), bt, 0, nullptr);
     hipError_t e2 = hipDeviceSynchronize();
     (void)hipFree(d);
+    (void)hipFree(dt);
     return (e == hipSuccess && e2 == hipSuccess) ? SC_OK : SC_ERR_HIP;
+}
+
+// Times `reps` launches of a grid of syrk tiles (M=N, K) on device buffers and of
+// the register-only MFMA peak probe; returns TFLOP/s for each.
+int64_t debug_bench(int which, int M, int K, int reps, int arg, double* tflops) {
+    *tflops = 0.0;
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return SC_ERR_HIP;
+    double flops = 0.0;
+    void *bufA = nullptr, *bufC = nullptr, *bt = nullptr, *bl = nullptr;
+    int64_t rc = SC_OK;
+    if (which == 0) {  // MFMA peak probe: arg = accumulators per wave, M = blocks
+        if (hipMalloc(&bufC, 8 * (size_t)std::max(M, 1)) != hipSuccess) return SC_ERR_DEVMEM;
+        (void)launch_mfma_peak((double*)bufC, M, K, arg, nullptr);
+        (void)hipDeviceSynchronize();
+        (void)hipEventRecord(e0, nullptr);
+        for (int r = 0; r < reps; ++r) (void)launch_mfma_peak((double*)bufC, M, K, arg, nullptr);
+        (void)hipEventRecord(e1, nullptr);
+        flops = 2.0 * 16 * 16 * 4 * (double)arg * K * M * 4.0 * reps;  // 4 waves per block
+    } else {  // SYRK kernel on an M x M lower triangle, K deep (arg = tile 64/128)
+        const size_t na = (size_t)M * K, nc = (size_t)M * M;
+        if (hipMalloc(&bufA, na * 8) != hipSuccess || hipMalloc(&bufC, nc * 8) != hipSuccess) {
+            rc = SC_ERR_DEVMEM;
+            goto done;
+        }
+        (void)hipMemset(bufA, 0, na * 8);
+        (void)hipMemset(bufC, 0, nc * 8);
+        {
+            GemmTask t {};
+            t.C = (double*)bufC;
+            t.A = (const double*)bufA;
+            t.ldc = M;
+            t.lda = M;
+            t.M = M;
+            t.N = M;
+            t.K = K;
+            const int tb = arg == 128 ? 128 : 64;
+            std::vector<int2> tiles;
+            append_tiles(tiles, 0, M, M, tb);
+            if (which == 1) xcd_order(tiles.data(), (int64_t)tiles.size());
+            (void)hipMalloc(&bt, sizeof(GemmTask));
+            (void)hipMalloc(&bl, tiles.size() * sizeof(int2));
+            (void)hipMemcpy(bt, &t, sizeof(t), hipMemcpyHostToDevice);
+            (void)hipMemcpy(bl, tiles.data(), tiles.size() * sizeof(int2), hipMemcpyHostToDevice);
+            (void)launch_syrk((GemmTask*)bt, (int2*)bl, (int)tiles.size(), tb, 1, nullptr);
+            (void)hipDeviceSynchronize();
+            (void)hipEventRecord(e0, nullptr);
+            for (int r = 0; r < reps; ++r) (void)launch_syrk((GemmTask*)bt, (int2*)bl, (int)tiles.size(), tb, 1, nullptr);
+            (void)hipEventRecord(e1, nullptr);
+            flops = (double)M * (M + 1.0) * K * reps;
+        }
+    }
+    {
+        (void)hipEventSynchronize(e1);
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        *tflops = flops / (ms * 1e-3) / 1e12;
+        if (hipGetLastError() != hipSuccess) rc = SC_ERR_HIP;
+    }
+done:
+    if (bufA) (void)hipFree(bufA);
+    if (bufC) (void)hipFree(bufC);
+    if (bt) (void)hipFree(bt);
+    if (bl) (void)hipFree(bl);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return rc;
 }
 
 }  // namespace sc

@@ -18,8 +18,10 @@ enum LaunchKind : int32_t {
     L_TRSM = 3,
     L_PANEL = 4,
     L_CB = 5,
-    L_COMM = 6,  // CB send/recv group after a level (multi-GPU)
-    L_KINDS = 7
+    L_COMM = 6,    // CB send/recv group after a level (multi-GPU)
+    L_RECORD = 7,  // record sync event `count` on stream `strm`
+    L_WAIT = 8,    // stream `strm` waits for sync event `count`
+    L_KINDS = 9
 };
 
 // One point-to-point contribution-block transfer (multi-GPU).
@@ -35,11 +37,13 @@ struct Launch {
     int32_t kind;
     int32_t level;
     int64_t off;      // first task in the kind's task array
+    int64_t toff;     // first tile in the SYRK tile list
     int32_t count;    // grid size (tiles for SYRK launches)
     int32_t ntasks;   // tasks (SYRK launches)
     int32_t maxm;     // small-front LDS edge
     int32_t big;      // CB launch covering fronts with w >= 256
     int32_t bt;       // SYRK tile edge (64 or 128)
+    int32_t strm;     // 0 = main stream, 1 = lookahead stream
     double flops;     // algorithmic SYRK flops (CB launches: mb*(mb+1)*w)
 };
 
@@ -47,6 +51,9 @@ struct Numeric {
     const Symbolic* S = nullptr;
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;  // trailing panel updates overlapped with the next slab
+    std::vector<hipEvent_t> sync_ev;
+    int32_t n_sync_events = 0;
     DevPlan P {};
     std::vector<void*> allocs;
     std::vector<Launch> sched;
@@ -55,6 +62,7 @@ struct Numeric {
     int2* d_potrf = nullptr;
     int4* d_trsm = nullptr;
     GemmTask* d_gemm = nullptr;
+    int2* d_tiles = nullptr;
     double* d_Ax_owned = nullptr;
     const double* last_Ax = nullptr;
     bool factored = false;
@@ -91,8 +99,12 @@ int64_t numeric_factor(Numeric& N, const double* d_Ax, bool sync);
 int64_t numeric_status(Numeric& N);
 int64_t numeric_export(Numeric& N, int64_t* Lp, int32_t* Li, double* Lx);
 int64_t numeric_timing(Numeric& N, double* t, int nt);
+int64_t numeric_level_times(Numeric& N, double* ms, int nl);
+int64_t numeric_launch_trace(Numeric& N, int32_t* kind, int32_t* level, int32_t* strm, double* ms, double* flops,
+                             int64_t cap);
 int64_t numeric_syrk_stats(Numeric& N, int wmin, double* flops, double* ms, int64_t* launches);
 void numeric_free(Numeric* N);
 int64_t debug_syrk(double* dC, int ldc, const double* dA, int lda, int M, int N, int K);
+int64_t debug_bench(int which, int M, int K, int reps, int arg, double* tflops);
 
 }  // namespace sc

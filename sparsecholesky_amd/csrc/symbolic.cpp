@@ -245,6 +245,9 @@ i64 analyze(i64 n, const i64* Ap, const i32* Ai, const sc_options& opt, Symbolic
         snz[f] = icc[fstart[f]];
     }
     if (opt.relax) {
+        std::vector<i32> gkids((size_t)nf, 0);  // children of each (merged) group
+        for (i32 f = 0; f < nf; ++f)
+            if (fparent[f] >= 0) gkids[fparent[f]]++;
         for (i32 j = nf - 2; j >= 0; --j) {
             if (fparent[j] != j + 1) continue;
             const i64 nscol0 = nscol[j], nscol1 = nscol[j + 1], ns = nscol0 + nscol1;
@@ -252,8 +255,10 @@ i64 analyze(i64 n, const i64* Ap, const i32* Ai, const sc_options& opt, Symbolic
             const double newzeros = (double)nscol0 * (double)(nscol0 + lnz1 - lnz0);
             const double totz = newzeros + zeros[j] + zeros[j + 1];
             bool merge = false;
-            if (opt.relax_wmax > 0 && nscol0 > opt.relax_wmax && nscol1 > opt.relax_wmax) {
-                merge = false;  // keep wide fronts apart: their coupling goes through the CB SYRK
+            if (opt.relax_wmax > 0 && nscol0 > opt.relax_wmax && nscol1 > opt.relax_wmax && gkids[j + 1] > 1) {
+                // a wide child of a wide parent with siblings stays apart: its coupling goes
+                // through the CB SYRK and the siblings stay parallel.  Chains still merge.
+                merge = false;
             } else if (ns <= opt.nrelax[0] || newzeros == 0.0) {
                 merge = true;
             } else {
@@ -268,6 +273,7 @@ i64 analyze(i64 n, const i64* Ap, const i32* Ai, const sc_options& opt, Symbolic
                 nscol[j] = ns;
                 snz[j] = nscol0 + lnz1;
                 absorbed[j + 1] = 1;
+                gkids[j] += gkids[j + 1] - 1;
             }
         }
     }
