@@ -135,7 +135,10 @@ int64_t sc_export_L(sc_numeric* num, int64_t* Lp, int32_t* Li, double* Lx);
 void* sc_numeric_stream(sc_numeric* num);
 /* Per-phase timing of the last factorization, milliseconds (HIP events):
  * t[0]=total, t[1]=CB transfers (multi-GPU), t[2]=small fronts, t[3]=assembly, t[4]=potrf,
- * t[5]=trsm, t[6]=panel update, t[7]=CB syrk.  Enabled by sc_numeric_set_profile. */
+ * t[5]=trsm, t[6]=panel update, t[7]=CB syrk.  sc_numeric_set_profile(num, 1): HIP
+ * events around every launch (eager runs; sets use_graph aside); 2: timestamp
+ * kernels around the CB SYRK launches only, which also works under hipGraph
+ * replay (feeds sc_numeric_syrk_stats). */
 int64_t sc_numeric_set_profile(sc_numeric* num, int32_t on);
 int64_t sc_numeric_timing(sc_numeric* num, double* t, int32_t nt);
 /* Wall time (ms) of each assembly-tree level of the last profiled factorization;

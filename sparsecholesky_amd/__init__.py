@@ -515,8 +515,10 @@ class Numeric:
     def status(self) -> int:
         return _check(lib().sc_numeric_status(self.h), "status")
 
-    def set_profile(self, on: bool = True):
-        _check(lib().sc_numeric_set_profile(self.h, 1 if on else 0), "set_profile")
+    def set_profile(self, on=True):
+        """True/1: HIP events around every launch (eager); 2: timestamp kernels around the
+        CB SYRK launches only (compatible with hipGraph replay); False/0: off."""
+        _check(lib().sc_numeric_set_profile(self.h, int(on)), "set_profile")
 
     def timing(self) -> np.ndarray:
         t = np.zeros(8)

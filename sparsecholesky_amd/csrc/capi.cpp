@@ -203,7 +203,7 @@ void* sc_numeric_stream(sc_numeric* num) { return (num && num->N) ? (void*)num->
 
 int64_t sc_numeric_set_profile(sc_numeric* num, int32_t on) {
     if (!num || !num->N) return SC_ERR_ARG;
-    num->N->profile = on != 0;
+    num->N->profile = (on == 1 || on == 2) ? on : 0;
     return SC_OK;
 }
 

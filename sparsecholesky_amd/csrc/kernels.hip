@@ -428,6 +428,14 @@ hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles
     return hipGetLastError();
 }
 
+// Timestamp probe for graph-captured timing (s_memrealtime: constant 100 MHz).
+__global__ void stamp_kernel(uint64_t* slot) { *slot = __builtin_amdgcn_s_memrealtime(); }
+
+hipError_t launch_stamp(uint64_t* slot, hipStream_t st) {
+    hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(1), 0, st, slot);
+    return hipGetLastError();
+}
+
 // Peak probe: independent fp64 MFMA chains, operands in registers.
 template <int NACC>
 __global__ __launch_bounds__(256) void mfma_peak_kernel(double* out, int iters) {

@@ -399,6 +399,12 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     std::vector<GemmTask> gemm;
     std::vector<int2> tiles;
     if ((rc = build_schedule(N, small, asmv, potrf, trsm, gemm, tiles))) return fail(rc);
+    N.stamp_of.assign(N.sched.size(), -1);
+    int nstamp = 0;
+    for (size_t i = 0; i < N.sched.size(); ++i)
+        if (N.sched[i].kind == L_CB) N.stamp_of[i] = nstamp++;
+    if ((rc = dalloc(N, (size_t)std::max(1, 2 * nstamp) * sizeof(uint64_t), p))) return fail(rc);
+    N.d_stamps = (uint64_t*)p;
     N.sync_ev.assign((size_t)N.n_sync_events, nullptr);
     for (auto& e : N.sync_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
@@ -438,32 +444,61 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
     return hipErrorInvalidValue;
 }
 
-static int64_t enqueue_all(Numeric& N, const double* d_Ax, bool with_events) {
+static int64_t enqueue_all(Numeric& N, const double* d_Ax, int prof) {
     HIP_TRY(hipMemsetAsync(N.P.info, 0x7f, sizeof(int32_t), N.stream));
     for (size_t i = 0; i < N.sched.size(); ++i) {
         const Launch& L = N.sched[i];
-        const bool timed = with_events && L.kind < L_RECORD;
+        const bool timed = prof == 1 && L.kind < L_RECORD;
+        const bool stamped = prof == 2 && N.stamp_of[i] >= 0;
         hipStream_t st = L.strm ? N.stream2 : N.stream;
         if (timed) HIP_TRY(hipEventRecord(N.ev[2 * i], st));
+        if (stamped) HIP_TRY(launch_stamp(N.d_stamps + 2 * N.stamp_of[i], st));
         HIP_TRY(launch_one(N, L, d_Ax));
+        if (stamped) HIP_TRY(launch_stamp(N.d_stamps + 2 * N.stamp_of[i] + 1, st));
         if (timed) HIP_TRY(hipEventRecord(N.ev[2 * i + 1], st));
     }
     return SC_OK;
+}
+
+// Duration (ms) of launch i in the last profiled factorization, or -1.
+static double launch_ms(Numeric& N, size_t i, const std::vector<uint64_t>& stamps) {
+    if (N.profile == 1) {
+        if (N.ev.size() != 2 * N.sched.size() || N.sched[i].kind >= L_RECORD) return -1.0;
+        float t = 0.f;
+        if (hipEventElapsedTime(&t, N.ev[2 * i], N.ev[2 * i + 1]) != hipSuccess) return -1.0;
+        return t;
+    }
+    if (N.profile == 2 && N.stamp_of[i] >= 0 && !stamps.empty()) {
+        const int q = N.stamp_of[i];
+        return (double)(stamps[2 * q + 1] - stamps[2 * q]) * 1e-5;  // 100 MHz ticks -> ms
+    }
+    return -1.0;
+}
+
+static std::vector<uint64_t> read_stamps(Numeric& N) {
+    std::vector<uint64_t> h;
+    if (N.profile != 2 || !N.d_stamps) return h;
+    int n = 0;
+    for (int32_t v : N.stamp_of) n = std::max(n, v + 1);
+    h.resize((size_t)2 * n);
+    if (n && hipMemcpy(h.data(), N.d_stamps, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+        h.clear();
+    return h;
 }
 
 int64_t numeric_factor(Numeric& N, const double* d_Ax, bool sync) {
     HIP_TRY(hipSetDevice(N.device));
     N.status_valid = false;
     N.last_Ax = d_Ax;
-    if (N.profile) {
-        if (N.ev.size() != 2 * N.sched.size()) {
-            for (auto e : N.ev) (void)hipEventDestroy(e);
-            N.ev.assign(2 * N.sched.size(), nullptr);
-            for (auto& e : N.ev) HIP_TRY(hipEventCreate(&e));
-        }
-        TRY(enqueue_all(N, d_Ax, true));
-    } else if (N.use_graph) {
-        if (!N.gexec || N.graph_Ax != d_Ax) {
+    if (N.profile == 1 && N.ev.size() != 2 * N.sched.size()) {
+        for (auto e : N.ev) (void)hipEventDestroy(e);
+        N.ev.assign(2 * N.sched.size(), nullptr);
+        for (auto& e : N.ev) HIP_TRY(hipEventCreate(&e));
+    }
+    if (N.use_graph && N.profile != 1) {
+        // the whole level schedule (both streams, and the timing events when
+        // profiling) as one hipGraph, re-captured only when its inputs change
+        if (!N.gexec || N.graph_Ax != d_Ax || N.graph_profiled != N.profile) {
             if (N.gexec) {
                 (void)hipGraphExecDestroy(N.gexec);
                 N.gexec = nullptr;
@@ -473,7 +508,7 @@ int64_t numeric_factor(Numeric& N, const double* d_Ax, bool sync) {
                 N.graph = nullptr;
             }
             HIP_TRY(hipStreamBeginCapture(N.stream, hipStreamCaptureModeThreadLocal));
-            int64_t rc = enqueue_all(N, d_Ax, false);
+            int64_t rc = enqueue_all(N, d_Ax, N.profile);
             hipGraph_t g = nullptr;
             hipError_t e2 = hipStreamEndCapture(N.stream, &g);
             if (rc != SC_OK) return rc;
@@ -481,10 +516,11 @@ int64_t numeric_factor(Numeric& N, const double* d_Ax, bool sync) {
             N.graph = g;
             HIP_TRY(hipGraphInstantiate(&N.gexec, N.graph, nullptr, nullptr, 0));
             N.graph_Ax = d_Ax;
+            N.graph_profiled = N.profile;
         }
         HIP_TRY(hipGraphLaunch(N.gexec, N.stream));
     } else {
-        TRY(enqueue_all(N, d_Ax, false));
+        TRY(enqueue_all(N, d_Ax, N.profile));
     }
     N.factored = true;
     if (sync) return numeric_status(N);
@@ -503,7 +539,7 @@ int64_t numeric_status(Numeric& N) {
     else
         N.status = (int64_t)N.S->post[info - 1] + 1;
     N.status_valid = true;
-    if (N.profile) {
+    if (N.profile == 1) {
         std::memset(N.phase_ms, 0, sizeof(N.phase_ms));
         hipEvent_t first = nullptr, last = nullptr;
         for (size_t i = 0; i < N.sched.size(); ++i) {
@@ -537,7 +573,7 @@ int64_t numeric_status(Numeric& N) {
 
 // Wall time per assembly-tree level (first main-stream launch start to last end).
 int64_t numeric_level_times(Numeric& N, double* ms, int nl) {
-    if (!N.profile || !N.status_valid) return SC_ERR_STATE;
+    if (N.profile != 1 || !N.status_valid) return SC_ERR_STATE;
     const int L = N.S->nlevels;
     std::vector<int> first(L, -1), last(L, -1);
     for (size_t i = 0; i < N.sched.size(); ++i) {
@@ -557,7 +593,7 @@ int64_t numeric_level_times(Numeric& N, double* ms, int nl) {
 // Per-launch trace of the last profiled factorization: kind, level, stream, ms, flops.
 int64_t numeric_launch_trace(Numeric& N, int32_t* kind, int32_t* level, int32_t* strm, double* ms, double* flops,
                              int64_t cap) {
-    if (!N.profile || !N.status_valid) return SC_ERR_STATE;
+    if (N.profile != 1 || !N.status_valid) return SC_ERR_STATE;
     int64_t n = 0;
     for (size_t i = 0; i < N.sched.size(); ++i) {
         const Launch& l = N.sched[i];
@@ -577,7 +613,7 @@ int64_t numeric_launch_trace(Numeric& N, int32_t* kind, int32_t* level, int32_t*
 }
 
 int64_t numeric_timing(Numeric& N, double* t, int nt) {
-    if (!N.profile || !N.status_valid) return SC_ERR_STATE;
+    if (N.profile != 1 || !N.status_valid) return SC_ERR_STATE;
     for (int i = 0; i < nt && i < 8; ++i) t[i] = N.phase_ms[i];
     return SC_OK;
 }
@@ -587,7 +623,8 @@ int64_t numeric_syrk_stats(Numeric& N, int wmin, double* flops, double* ms, int6
     // -1: the panel-update launches instead)
     double fl = 0.0, t = 0.0;
     int64_t cnt = 0;
-    const bool have_t = N.profile && N.status_valid && N.ev.size() == 2 * N.sched.size();
+    bool have_t = N.status_valid && N.profile != 0;
+    const std::vector<uint64_t> stamps = read_stamps(N);
     for (size_t i = 0; i < N.sched.size(); ++i) {
         const Launch& L = N.sched[i];
         if (L.kind != (wmin < 0 ? L_PANEL : L_CB)) continue;
@@ -595,8 +632,11 @@ int64_t numeric_syrk_stats(Numeric& N, int wmin, double* flops, double* ms, int6
         fl += L.flops;
         ++cnt;
         if (have_t) {
-            float e = 0.f;
-            if (hipEventElapsedTime(&e, N.ev[2 * i], N.ev[2 * i + 1]) == hipSuccess) t += e;
+            const double e = launch_ms(N, i, stamps);
+            if (e < 0)
+                have_t = false;
+            else
+                t += e;
         }
     }
     if (flops) *flops = fl;

@@ -69,8 +69,11 @@ struct Numeric {
     int64_t status = 0;
     bool status_valid = false;
 
-    // profiling
-    bool profile = false;
+    // profiling: 1 = HIP events around every launch (eager runs); 2 = timestamp
+    // kernels around the CB SYRK launches only (works inside hipGraph replay)
+    int profile = 0;
+    uint64_t* d_stamps = nullptr;
+    std::vector<int32_t> stamp_of;  // launch -> stamp pair index, -1 = none
     std::vector<hipEvent_t> ev;
     double phase_ms[8] = {0};
     // hipGraph replay
@@ -78,6 +81,7 @@ struct Numeric {
     hipGraphExec_t gexec = nullptr;
     hipGraph_t graph = nullptr;
     const double* graph_Ax = nullptr;
+    int graph_profiled = 0;
 
     // multi-GPU: owner rank per supernode (empty = single GPU).  virt_ranks > 1
     // runs the partitioned schedule of all ranks in this one process (shared
