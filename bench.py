@@ -79,6 +79,7 @@ def main():
     ap.add_argument("--relax-wmax", type=int, default=None)
     ap.add_argument("--nbo", type=int, default=None, help="panel outer block (rank-k update width)")
     ap.add_argument("--lookahead", type=int, default=None)
+    ap.add_argument("--tile", type=int, default=None, help="SYRK tile: 0 auto, 64, 128")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
@@ -118,6 +119,8 @@ def main():
         kw["panel_nb_outer"] = args.nbo
     if args.lookahead is not None:
         kw["lookahead"] = args.lookahead
+    if args.tile is not None:
+        kw["syrk_tile"] = args.tile
     symb = sc.Symbolic(A, **kw)
     t_an = time.perf_counter() - t0
     st = symb.stats()
@@ -204,7 +207,7 @@ def main():
             "work_share_per_rank": work_share,
             "options": {"relax_wmax": symb.opt.relax_wmax, "panel_nb_outer": symb.opt.panel_nb_outer,
                         "small_front_max": symb.opt.small_front_max, "use_graph": symb.opt.use_graph,
-                        "lookahead": symb.opt.lookahead},
+                        "lookahead": symb.opt.lookahead, "syrk_tile": symb.opt.syrk_tile},
         },
         "roofline": roof,
         "timing_s": {"generate": round(t_gen, 3), "analyze": round(t_an, 3), "numeric_create": round(t_alloc, 3)},

@@ -285,16 +285,18 @@ __global__ __launch_bounds__(256) void trsm_panel_kernel(DevPlan P, const int4* 
 
 // ---------------------------------------------------------------------------
 // fp64 MFMA SYRK on a lower trapezoid: C[i,j] -= sum_k A[i,k] * A[j,k] for
-// 0 <= j < N, j <= i < M.  Tiles BT x BT with ti >= tj; 256 threads = 4 waves
-// (2 x 2), each wave (BT/2) x (BT/2) = RT x RT tiles of v_mfma_f64_16x16x4_f64.
-// A (M x K) and the B operand (its first N rows) share one column-major array.
+// 0 <= j < N, j <= i < M.  BT x BT output tiles (ti >= tj) on WM x WN waves, each
+// wave (BT/WM) x (BT/WN) = RTM x RTN tiles of v_mfma_f64_16x16x4_f64.  A (M x K)
+// and the B operand (its first N rows) share one column-major array.  K is
+// staged through double-buffered LDS (register staging, BK = 16).
 // ---------------------------------------------------------------------------
-template <int BT, int TAG>
-__global__ __launch_bounds__(256) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
-                                                         const int2* __restrict__ tiles) {
+template <int BT, int WM, int WN, int TAG>
+__global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
+                                                                  const int2* __restrict__ tiles) {
+    constexpr int NT = 64 * WM * WN;
     constexpr int BK = 16;
     constexpr int LDT = BT + 16;  // +128 B row pad: the two k-rows read by a half-wave hit disjoint banks
-    constexpr int RT = BT / 32;   // 16x16 MFMA tiles per wave per dimension
+    constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
     __shared__ double As[2][BK * LDT];
     __shared__ double Bs[2][BK * LDT];
 
@@ -307,23 +309,23 @@ __global__ __launch_bounds__(256) void syrk_mfma_kernel(const GemmTask* __restri
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = tid >> 6;
-    const int wr = wid >> 1, wc = wid & 1;
+    const int wr = wid / WN, wc = wid % WN;
     const double* __restrict__ A = T.A;
     const int64_t lda = T.lda;
 
-    double4_t acc[RT][RT];
+    double4_t acc[RTM][RTN];
 #pragma unroll
-    for (int a = 0; a < RT; ++a)
+    for (int a = 0; a < RTM; ++a)
 #pragma unroll
-        for (int b = 0; b < RT; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
+        for (int b = 0; b < RTN; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
 
-    // staging: BK x BT doubles per operand; 256 threads -> (BT*BK/256) each
-    constexpr int PER = BT * BK / 256;
+    // staging: BK x BT doubles per operand over NT threads
+    constexpr int PER = BT * BK / NT;
     double ra[PER], rb[PER];
     auto gload = [&](int k0) {
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
-            const int e = tid + q * 256;
+            const int e = tid + q * NT;
             const int r = e % BT, kk = e / BT;
             const int gk = k0 + kk;
             const int gr = row0 + r, gc = col0 + r;
@@ -334,7 +336,7 @@ __global__ __launch_bounds__(256) void syrk_mfma_kernel(const GemmTask* __restri
     auto sstore = [&](int buf) {
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
-            const int e = tid + q * 256;
+            const int e = tid + q * NT;
             const int r = e % BT, kk = e / BT;
             As[buf][kk * LDT + r] = ra[q];
             Bs[buf][kk * LDT + r] = rb[q];
@@ -350,16 +352,16 @@ __global__ __launch_bounds__(256) void syrk_mfma_kernel(const GemmTask* __restri
         if (kt + 1 < nk) gload((kt + 1) * BK);
 #pragma unroll
         for (int kk = 0; kk < BK; kk += 4) {
-            double av[RT], bv[RT];
+            double av[RTM], bv[RTN];
             const int krow = kk + (lane >> 4);
 #pragma unroll
-            for (int a = 0; a < RT; ++a) av[a] = As[cur][krow * LDT + wr * (BT / 2) + a * 16 + (lane & 15)];
+            for (int a = 0; a < RTM; ++a) av[a] = As[cur][krow * LDT + wr * (BT / WM) + a * 16 + (lane & 15)];
 #pragma unroll
-            for (int b = 0; b < RT; ++b) bv[b] = Bs[cur][krow * LDT + wc * (BT / 2) + b * 16 + (lane & 15)];
+            for (int b = 0; b < RTN; ++b) bv[b] = Bs[cur][krow * LDT + wc * (BT / WN) + b * 16 + (lane & 15)];
 #pragma unroll
-            for (int a = 0; a < RT; ++a)
+            for (int a = 0; a < RTM; ++a)
 #pragma unroll
-                for (int b = 0; b < RT; ++b)
+                for (int b = 0; b < RTN; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
         }
         if (kt + 1 < nk) sstore(cur ^ 1);
@@ -370,13 +372,13 @@ __global__ __launch_bounds__(256) void syrk_mfma_kernel(const GemmTask* __restri
     double* __restrict__ C = T.C;
     const int64_t ldc = T.ldc;
 #pragma unroll
-    for (int a = 0; a < RT; ++a)
+    for (int a = 0; a < RTM; ++a)
 #pragma unroll
-        for (int b = 0; b < RT; ++b)
+        for (int b = 0; b < RTN; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int gi = row0 + wr * (BT / 2) + a * 16 + MFMA_F64_ROW(lane, r);
-                const int gj = col0 + wc * (BT / 2) + b * 16 + (lane & 15);
+                const int gi = row0 + wr * (BT / WM) + a * 16 + MFMA_F64_ROW(lane, r);
+                const int gj = col0 + wc * (BT / WN) + b * 16 + (lane & 15);
                 if (gi < T.M && gj < T.N && gi >= gj) C[gi + gj * ldc] -= acc[a][b][r];
             }
 }
@@ -412,19 +414,38 @@ hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hip
 }
 
 // TAG only separates the launches in profiles: 0 = panel update, 1 = CB update.
+// bt = 64: 64x64 tiles on 4 waves (2x2); bt = 128: 128x128 tiles on 8 waves (2x4).
+template <int TAG>
+static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int bt, hipStream_t st) {
+    if (bt == 128)
+        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG>), dim3(n), dim3(512), 0, st, tasks, tiles);
+    else
+        hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG>), dim3(n), dim3(256), 0, st, tasks, tiles);
+}
+
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st) {
     if (total_tiles <= 0) return hipSuccess;
-    if (bt == 128) {
-        if (tag)
-            hipLaunchKernelGGL((syrk_mfma_kernel<128, 1>), dim3(total_tiles), dim3(256), 0, st, tasks, tiles);
-        else
-            hipLaunchKernelGGL((syrk_mfma_kernel<128, 0>), dim3(total_tiles), dim3(256), 0, st, tasks, tiles);
-    } else {
-        if (tag)
-            hipLaunchKernelGGL((syrk_mfma_kernel<64, 1>), dim3(total_tiles), dim3(256), 0, st, tasks, tiles);
-        else
-            hipLaunchKernelGGL((syrk_mfma_kernel<64, 0>), dim3(total_tiles), dim3(256), 0, st, tasks, tiles);
+    if (tag)
+        launch_syrk_t<1>(tasks, tiles, total_tiles, bt, st);
+    else
+        launch_syrk_t<0>(tasks, tiles, total_tiles, bt, st);
+    return hipGetLastError();
+}
+
+// Fills n doubles with a deterministic pseudo-random pattern in [-1, 1) (microbenchmarks:
+// zero operands run the MFMA at a higher clock than real data).
+__global__ void fill_random_kernel(double* p, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t x = (uint64_t)i * 0x9E3779B97F4A7C15ull;
+        x ^= x >> 31;
+        x *= 0xBF58476D1CE4E5B9ull;
+        x ^= x >> 29;
+        p[i] = (double)(x >> 11) * (2.0 / 9007199254740992.0) - 1.0;
     }
+}
+
+hipError_t launch_fill_random(double* p, int64_t n, hipStream_t st) {
+    hipLaunchKernelGGL(fill_random_kernel, dim3(1024), dim3(256), 0, st, p, n);
     return hipGetLastError();
 }
 

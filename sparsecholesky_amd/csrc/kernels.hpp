@@ -58,6 +58,7 @@ hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hip
 hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st);
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st);
 hipError_t launch_stamp(uint64_t* slot, hipStream_t st);
+hipError_t launch_fill_random(double* p, int64_t n, hipStream_t st);
 hipError_t launch_mfma_peak(double* out, int blocks, int iters, int nacc, hipStream_t st);
 
 // tiles of an M x N lower trapezoid with square BT tiles
