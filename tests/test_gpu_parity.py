@@ -208,3 +208,84 @@ def test_partitioned_schedule_bitwise_equal(gpu, nranks):
     assert np.array_equal(L0.x, L1.x)
     st, Lp, Li, Lx = oracle.chol(A)
     assert rel_fro(L1.x, Lx) < TOL
+
+
+def random_spd(n, density, seed, dup=False, lower_noise=False):
+    """Random sparse SPD (diagonally dominant) upper CSC through the reference's
+    triplet path (chol.hpp:308-369); optionally with duplicate triplets and with
+    explicit lower entries that must be ignored (chol.hpp:392,696)."""
+    rng = np.random.default_rng(seed)
+    nnz = max(1, int(density * n * n / 2))
+    i = rng.integers(0, n, nnz)
+    j = rng.integers(0, n, nnz)
+    v = rng.uniform(-1, 1, nnz)
+    ti = np.concatenate([i, np.arange(n)])
+    tj = np.concatenate([j, np.arange(n)])
+    deg = np.zeros(n)
+    np.add.at(deg, i, np.abs(v))
+    np.add.at(deg, j, np.abs(v))
+    tx = np.concatenate([v, deg + 1.0 + rng.uniform(0, 1, n)])
+    if dup:
+        ti = np.concatenate([ti, i[:10]])
+        tj = np.concatenate([tj, j[:10]])
+        tx = np.concatenate([tx, np.zeros(min(10, len(i)))])
+    A = sc.triplet_to_csc_matrix(ti, tj, tx, n)
+    if lower_noise:
+        # append an explicit lower entry to some columns; they must not change L
+        p, ii, xx = [0], [], []
+        for c in range(n):
+            a, b = A.p[c], A.p[c + 1]
+            ii.extend(A.i[a:b].tolist())
+            xx.extend(A.x[a:b].tolist())
+            if c + 1 < n and c % 3 == 0:
+                ii.append(n - 1)
+                xx.append(1e6)
+            p.append(len(ii))
+        A = sc.csc_matrix(n, n, np.array(p, dtype=np.int64), np.array(ii, dtype=np.int32), np.array(xx))
+    return A
+
+
+@pytest.mark.parametrize("n,density,seed", [(1, 1.0, 0), (2, 1.0, 1), (50, 0.2, 2), (300, 0.02, 3),
+                                            (700, 0.005, 4), (200, 1.0, 5)])
+def test_random_spd(gpu, n, density, seed):
+    check_parity(random_spd(n, density, seed))
+
+
+@pytest.mark.parametrize("small_front_max", [0, 32, 128])
+def test_random_spd_paths(gpu, small_front_max):
+    check_parity(random_spd(400, 0.03, 11), small_front_max=small_front_max)
+
+
+def test_duplicates_summed(gpu):
+    check_parity(random_spd(120, 0.05, 7, dup=True))
+
+
+def test_lower_entries_ignored_gpu(gpu):
+    A = random_spd(90, 0.05, 8, lower_noise=True)
+    check_parity(A)
+
+
+def test_dense_matrix_large_front(gpu):
+    # fully dense: one supernode (a dense Cholesky through POTRF/TRSM/MFMA panels)
+    n = 700
+    rng = np.random.default_rng(3)
+    M = rng.standard_normal((n, n))
+    D = M @ M.T + n * np.eye(n)
+    iu = np.triu_indices(n)
+    A = sc.triplet_to_csc_matrix(iu[0], iu[1], D[iu], n)
+    L, err = check_parity(A)
+    s = sc.Symbolic(A).stats()
+    assert s["n_supernodes"] == 1 and s["max_front_w"] == n
+
+
+def test_empty_matrix_gpu(gpu):
+    A = sc.csc_matrix(0, 0, np.zeros(1, dtype=np.int64), np.zeros(0, dtype=np.int32), np.zeros(0))
+    r = sc.chol(A)
+    assert r.has_value() and r.value().x.size == 0
+
+
+def test_missing_diagonal_not_pd(gpu):
+    # column 1 has no diagonal entry: pivot 0 - l^2 <= 0 (chol.hpp:849)
+    A = sc.triplet_to_csc_matrix([0, 0], [0, 1], [4.0, 1.0], 2)
+    r = sc.chol(A)
+    assert not r.has_value() and r.status == 2
