@@ -220,9 +220,12 @@ int64_t sc_dist_schedule(const sc_symbolic* sym, int32_t nranks, int32_t rank, i
  * pointers, column-major) through the fp64 MFMA SYRK kernel. */
 int64_t sc_debug_syrk(double* dC, int32_t ldc, const double* dA, int32_t lda, int32_t M, int32_t N,
                       int32_t K);
-/* Microbenchmarks (TFLOP/s): which=0 register-only fp64 MFMA probe (M blocks of
- * 4 waves, K iterations, arg accumulators); which=1/2 the SYRK kernel on an M x M
- * triangle with depth K, tile arg (64/128), with / without the XCD tile order. */
+/* Microbenchmarks: which=0 register-only fp64 MFMA probe (TFLOP/s; M blocks of
+ * 4 waves, K iterations, arg accumulators); which=1/5 the SYRK kernel on an M x M
+ * triangle with depth K, tile arg (64/128), with / without the XCD tile order
+ * (TFLOP/s); which=2/3 the panel POTRF / TRSM kernel variant arg on an M x 64
+ * front (microseconds per launch); which=4 max |variant 0 - variant 1| of the
+ * POTRF + TRSM result on that front. */
 int64_t sc_debug_bench(int32_t which, int32_t M, int32_t K, int32_t reps, int32_t arg, double* tflops);
 int64_t sc_device_count(void);
 /* Message of the last failing call on this thread. */

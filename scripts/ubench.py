@@ -14,7 +14,24 @@ def run(which, M, K, reps, arg):
     return round(t.value, 2) if rc == 0 else f"rc={rc}"
 
 
+def panel():
+    out = {}
+    for M in (2048, 16384):
+        out[f"M={M} potrf v0 us"] = run(2, M, 1, 20, 0)
+        out[f"M={M} potrf v1 us"] = run(2, M, 1, 20, 1)
+        out[f"M={M} trsm v0 us"] = run(3, M, 1, 20, 0)
+        out[f"M={M} trsm v1 us"] = run(3, M, 1, 20, 1)
+        t = C.c_double()
+        rc = sc.lib().sc_debug_bench(4, M, 1, 1, 0, C.byref(t))
+        out[f"M={M} max|v0-v1|"] = t.value if rc == 0 else f"rc={rc}"
+    for k, v in out.items():
+        print(f"{k:45s} {v}")
+    print(json.dumps(out))
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "panel":
+        return panel()
     out = {}
     for blocks in (1024, 2048):
         out[f"peak blocks={blocks} nacc=8"] = run(0, blocks, 20000, 3, 8)

@@ -284,6 +284,130 @@ __global__ __launch_bounds__(256) void trsm_panel_kernel(DevPlan P, const int4* 
 }
 
 // ---------------------------------------------------------------------------
+// Pipelined variants (default).  A full 64-column block runs generated
+// straight-line code (panel_gen.inc, gen_panel.py) that keeps ~24 LDS operands
+// in flight per wave; a partial last block (nb < 64) uses the template path.
+// ---------------------------------------------------------------------------
+// Buffer-resource access for the panel kernels: one VGPR lane offset plus an
+// SGPR column offset per access, so 64 column addresses never occupy VGPRs.
+// Raw buffers (stride 0) drop stores and zero loads at offsets >= nbytes, so a
+// dead lane is masked by giving it an out-of-range lane offset (BUF_DEAD).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const double* base, uint32_t nbytes = 0xffffffffu) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), 0, (int)nbytes, 0x00020000);
+}
+constexpr int BUF_DEAD = 0x7ffffff0;
+__device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
+}
+__device__ __forceinline__ void buf_st(double v, __amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0)), v), rs, voff, soff, 0);
+}
+
+// 1/sqrt(d): v_rsq_f64 seed plus two Newton steps (~1 ulp; NaN/inf for d <= 0,
+// which the callers flag separately).
+__device__ __forceinline__ double rsqrt_f64(double d) {
+    double y = __builtin_amdgcn_rsq(d);
+    const double h = 0.5 * d;
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    return y;
+}
+
+#include "panel_gen.inc"
+
+__global__ __launch_bounds__(64) void potrf_diag_g_kernel(DevPlan P, const int2* __restrict__ tasks) {
+    __shared__ double C[2 * PNB];
+    const int2 t = tasks[blockIdx.x];
+    const int s = t.x, k0 = t.y;
+    const int c0 = P.sn_start[s];
+    const int w = P.sn_start[s + 1] - c0;
+    const int m = P.sn_m[s];
+    const int nb = min(PNB, w - k0);
+    double* blk = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m + k0;
+    const int lane = threadIdx.x;
+    if (nb < PNB) {
+        potrf_block_wave(blk, m, nb, lane, C, P.info, c0 + k0);
+        return;
+    }
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(blk);
+    double r[PNB];
+#pragma unroll
+    for (int c = 0; c < PNB; ++c) r[c] = buf_ld(rs, lane * 8, c * m * 8);
+    const int bad = potrf64_full(r, C, lane);
+    if (bad >= 0 && lane == 0) report_fail(P.info, c0 + k0 + bad);
+#pragma unroll
+    for (int c = 0; c < PNB; ++c)
+        if (c <= lane) buf_st(r[c], rs, lane * 8, c * m * 8);
+}
+
+// Partial last block (nb < 64) of the panel TRSM: template path, kept out of
+// line so its registers do not constrain the generated full-block code.
+__device__ __noinline__ void trsm_partial(double* pan, int m, int k0, int nb, int r0, double* Lc, double* invd) {
+    constexpr int LD = PNB + 2;
+    const int tid = threadIdx.x;
+    const double* blk = pan + (int64_t)k0 * m + k0;
+    for (int idx = tid; idx < PNB * PNB; idx += 256) {
+        const int q = idx % PNB, j = idx / PNB;
+        const double v = (q < nb && j < nb && j <= q) ? blk[(int64_t)j * m + q] : 0.0;
+        Lc[j * LD + q] = v;
+        if (q == j) invd[j] = (j < nb) ? 1.0 / v : 0.0;
+    }
+    __syncthreads();
+    const int row = r0 + tid;
+    const bool live = row < m;
+    double* xs = pan + (int64_t)k0 * m + (live ? row : r0);
+    double r[PNB];
+#pragma unroll
+    for (int c = 0; c < PNB; ++c) r[c] = (live && c < nb) ? xs[(int64_t)c * m] : 0.0;
+    trsm_steps<0>(r, Lc, invd, nb);
+    if (live) {
+#pragma unroll
+        for (int c = 0; c < PNB; ++c)
+            if (c < nb) xs[(int64_t)c * m] = r[c];
+    }
+}
+
+// Panel TRSM, rows [r0, r0 + 256): L11 operands packed into an LDS stream in the
+// order the generated solve consumes them (1/L(J,J), then L(J+1..63, J)).
+__global__ __launch_bounds__(256) void trsm_panel_g_kernel(DevPlan P, const int4* __restrict__ tasks) {
+    __shared__ double2 S[TRSM64_STREAM / 2];
+    const int4 t = tasks[blockIdx.x];
+    const int s = t.x, k0 = t.y, r0 = t.z;
+    const int tid = threadIdx.x;
+    const int c0 = P.sn_start[s];
+    const int w = P.sn_start[s + 1] - c0;
+    const int m = P.sn_m[s];
+    const int nb = min(PNB, w - k0);
+    double* pan = P.panel_pool + P.panel_off[s];
+    if (nb < PNB) {
+        __shared__ double Lc[PNB * (PNB + 2)];
+        __shared__ double invd[PNB];
+        trsm_partial(pan, m, k0, nb, r0, Lc, invd);
+        return;
+    }
+    const double* blk = pan + (int64_t)k0 * m + k0;
+    const int row = r0 + tid;
+    // the 64 block columns, m rows each (< 2^31 bytes for m < 4M); dead lanes masked
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pan + (int64_t)k0 * m, (uint32_t)m * PNB * 8u);
+    const int voff = row < m ? row * 8 : BUF_DEAD;
+    double* Sd = reinterpret_cast<double*>(S);
+    for (int e = tid; e < PNB * PNB; e += 256) {
+        const int j = e / PNB, q = e % PNB;
+        if (q >= j) {
+            const double v = blk[(int64_t)j * m + q];
+            Sd[PNB * j - j * (j - 1) / 2 + (q - j)] = (q == j) ? 1.0 / v : v;
+        }
+    }
+    __syncthreads();
+    double r[PNB];
+#pragma unroll
+    for (int c = 0; c < PNB; ++c) r[c] = buf_ld(rs, voff, c * m * 8);
+    trsm64_full(r, S);
+#pragma unroll
+    for (int c = 0; c < PNB; ++c) buf_st(r[c], rs, voff, c * m * 8);
+}
+
+// ---------------------------------------------------------------------------
 // fp64 MFMA SYRK on a lower trapezoid: C[i,j] -= sum_k A[i,k] * A[j,k] for
 // 0 <= j < N, j <= i < M.  BT x BT output tiles (ti >= tj) on WM x WN waves, each
 // wave (BT/WM) x (BT/WN) = RTM x RTN tiles of v_mfma_f64_16x16x4_f64.  A (M x K)
@@ -401,15 +525,21 @@ hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count,
     return hipGetLastError();
 }
 
-hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hipStream_t st) {
+hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hipStream_t st, int variant) {
     if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(potrf_diag_kernel, dim3(count), dim3(64), 0, st, P, tasks);
+    if (variant == 0)
+        hipLaunchKernelGGL(potrf_diag_kernel, dim3(count), dim3(64), 0, st, P, tasks);
+    else
+        hipLaunchKernelGGL(potrf_diag_g_kernel, dim3(count), dim3(64), 0, st, P, tasks);
     return hipGetLastError();
 }
 
-hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st) {
+hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st, int variant) {
     if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(trsm_panel_kernel, dim3(count), dim3(256), 0, st, P, tasks);
+    if (variant == 0)
+        hipLaunchKernelGGL(trsm_panel_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks);
+    else
+        hipLaunchKernelGGL(trsm_panel_g_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks);
     return hipGetLastError();
 }
 

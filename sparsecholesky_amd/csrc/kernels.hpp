@@ -54,8 +54,9 @@ hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count,
                               hipStream_t st);
 hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count, const double* Ax,
                                  hipStream_t st);
-hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hipStream_t st);
-hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st);
+// variant 0: LDS-broadcast kernels (kept for A/B microbenchmarks), 1: register/SGPR kernels
+hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hipStream_t st, int variant = 1);
+hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st, int variant = 1);
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st);
 hipError_t launch_stamp(uint64_t* slot, hipStream_t st);
 hipError_t launch_fill_random(double* p, int64_t n, hipStream_t st);

@@ -391,7 +391,9 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     P.a_pos = d_apos;
     P.a_src = d_asrc;
     void* p = nullptr;
-    if ((rc = dalloc(N, (size_t)S.panel_off[ns] * sizeof(double), p))) return fail(rc);
+    // + PNB doubles: the panel TRSM reads L11 columns unconditionally (rows past the
+    // block feed only registers that are never stored)
+    if ((rc = dalloc(N, (size_t)(S.panel_off[ns] + PNB) * sizeof(double), p))) return fail(rc);
     P.panel_pool = (double*)p;
     if ((rc = dalloc(N, (size_t)S.cb_off[ns] * sizeof(double), p))) return fail(rc);
     P.cb_pool = (double*)p;
@@ -718,8 +720,103 @@ int64_t debug_syrk(double* dC, int ldc, const double* dA, int lda, int M, int Nn
 
 // Times `reps` launches of a grid of syrk tiles (M=N, K) on device buffers and of
 // the register-only MFMA peak probe; returns TFLOP/s for each.
+// Panel-kernel microbenchmarks on one synthetic front (m = M rows, w = 64):
+// which 2 = POTRF (us per launch), 3 = TRSM (us per launch), 4 = max |variant 0 -
+// variant 1| over POTRF + TRSM results.  arg = kernel variant for 2 / 3.
+static int64_t bench_panel(int which, int M, int reps, int arg, double* out) {
+    const int w = PNB;
+    if (M < w || reps < 1) return SC_ERR_ARG;
+    const size_t nel = (size_t)M * w;
+    std::vector<double> h(nel + PNB, 0.0);
+    uint64_t x = 88172645463325252ull;
+    auto rnd = [&]() {
+        x ^= x << 13;
+        x ^= x >> 7;
+        x ^= x << 17;
+        return (double)(x >> 11) / 9007199254740992.0 - 0.5;
+    };
+    for (int j = 0; j < w; ++j)
+        for (int i = 0; i < M; ++i) h[(size_t)j * M + i] = (i == j) ? 64.0 : rnd();
+    int32_t hs[2] = {0, w}, hm[1] = {M};
+    int64_t ho[2] = {0, (int64_t)nel};
+    std::vector<int4> tr;
+    for (int r0 = w; r0 < M; r0 += TRSM_ROWS) tr.push_back(make_int4(0, 0, r0, 0));
+    int2 pt = make_int2(0, 0);
+    void *d_pan = nullptr, *d_pan2 = nullptr, *d_ref = nullptr, *d_s = nullptr, *d_m = nullptr, *d_o = nullptr,
+         *d_info = nullptr, *d_pt = nullptr, *d_tr = nullptr;
+    const size_t bytes = (nel + PNB) * sizeof(double);
+    int64_t rc = SC_OK;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (hipMalloc(&d_pan, bytes) || hipMalloc(&d_pan2, bytes) || hipMalloc(&d_ref, bytes) || hipMalloc(&d_s, 8) ||
+        hipMalloc(&d_m, 4) || hipMalloc(&d_o, 16) || hipMalloc(&d_info, 4) || hipMalloc(&d_pt, 8) ||
+        hipMalloc(&d_tr, std::max<size_t>(1, tr.size()) * sizeof(int4)) || hipEventCreate(&e0) ||
+        hipEventCreate(&e1)) {
+        rc = SC_ERR_DEVMEM;
+    } else {
+        (void)hipMemcpy(d_ref, h.data(), bytes, hipMemcpyHostToDevice);
+        (void)hipMemcpy(d_s, hs, 8, hipMemcpyHostToDevice);
+        (void)hipMemcpy(d_m, hm, 4, hipMemcpyHostToDevice);
+        (void)hipMemcpy(d_o, ho, 16, hipMemcpyHostToDevice);
+        (void)hipMemset(d_info, 0, 4);
+        (void)hipMemcpy(d_pt, &pt, 8, hipMemcpyHostToDevice);
+        if (!tr.empty()) (void)hipMemcpy(d_tr, tr.data(), tr.size() * sizeof(int4), hipMemcpyHostToDevice);
+        DevPlan P {};
+        P.sn_start = (const int32_t*)d_s;
+        P.sn_m = (const int32_t*)d_m;
+        P.panel_off = (const int64_t*)d_o;
+        P.info = (int32_t*)d_info;
+        auto on = [&](void* pan) {
+            DevPlan Q = P;
+            Q.panel_pool = (double*)pan;
+            return Q;
+        };
+        const int nt = (int)tr.size();
+        if (which == 4) {
+            for (int v = 0; v < 2; ++v) {
+                void* dst = v ? d_pan2 : d_pan;
+                (void)hipMemcpy(dst, d_ref, bytes, hipMemcpyDeviceToDevice);
+                (void)launch_potrf_diag(on(dst), (const int2*)d_pt, 1, nullptr, v);
+                (void)launch_trsm_panel(on(dst), (const int4*)d_tr, nt, nullptr, v);
+            }
+            (void)hipDeviceSynchronize();
+            std::vector<double> a(nel), b(nel);
+            (void)hipMemcpy(a.data(), d_pan, nel * 8, hipMemcpyDeviceToHost);
+            (void)hipMemcpy(b.data(), d_pan2, nel * 8, hipMemcpyDeviceToHost);
+            double md = 0.0;
+            for (int j = 0; j < w; ++j)
+                for (int i = j; i < M; ++i) md = std::max(md, std::fabs(a[(size_t)j * M + i] - b[(size_t)j * M + i]));
+            *out = md;
+        } else {
+            (void)hipMemcpy(d_pan, d_ref, bytes, hipMemcpyDeviceToDevice);
+            (void)launch_potrf_diag(on(d_pan), (const int2*)d_pt, 1, nullptr, 1);
+            double tot = 0.0;
+            for (int r = 0; r < reps + 1; ++r) {
+                if (which == 2) (void)hipMemcpy(d_pan, d_ref, bytes, hipMemcpyDeviceToDevice);
+                (void)hipEventRecord(e0, nullptr);
+                if (which == 2)
+                    (void)launch_potrf_diag(on(d_pan), (const int2*)d_pt, 1, nullptr, arg);
+                else
+                    (void)launch_trsm_panel(on(d_pan), (const int4*)d_tr, nt, nullptr, arg);
+                (void)hipEventRecord(e1, nullptr);
+                (void)hipEventSynchronize(e1);
+                float ms = 0.f;
+                (void)hipEventElapsedTime(&ms, e0, e1);
+                if (r > 0) tot += ms;
+            }
+            *out = 1e3 * tot / reps;
+        }
+        if (hipGetLastError() != hipSuccess) rc = SC_ERR_HIP;
+    }
+    for (void* p : {d_pan, d_pan2, d_ref, d_s, d_m, d_o, d_info, d_pt, d_tr})
+        if (p) (void)hipFree(p);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    return rc;
+}
+
 int64_t debug_bench(int which, int M, int K, int reps, int arg, double* tflops) {
     *tflops = 0.0;
+    if (which >= 2 && which <= 4) return bench_panel(which, M, reps, arg, tflops);
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return SC_ERR_HIP;
     double flops = 0.0;
@@ -753,7 +850,7 @@ int64_t debug_bench(int which, int M, int K, int reps, int arg, double* tflops) 
             const int tb = arg == 128 ? 128 : 64;
             std::vector<int2> tiles;
             append_tiles(tiles, 0, M, M, tb);
-            if (which == 1) xcd_order(tiles.data(), (int64_t)tiles.size());
+            if (which != 5) xcd_order(tiles.data(), (int64_t)tiles.size());
             (void)hipMalloc(&bt, sizeof(GemmTask));
             (void)hipMalloc(&bl, tiles.size() * sizeof(int2));
             (void)hipMemcpy(bt, &t, sizeof(t), hipMemcpyHostToDevice);
