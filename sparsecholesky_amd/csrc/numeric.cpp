@@ -92,6 +92,37 @@ void xcd_order(int2* tiles, int64_t n) {
     }
 }
 
+// Work-balanced XCD order of a multi-task launch (workgroup b runs on XCD b % 8,
+// each XCD has its own L2).  The tiles arrive task-contiguous, each task in
+// supertile order.  Every task is cut into 8 contiguous chunks, one per XCD, with
+// the remainders dealt round robin across tasks so that each XCD receives exactly
+// its ceil((n - x) / 8) tiles; an XCD walks its chunks in decreasing K (longest
+// tiles first).  With one task this is xcd_order.
+void xcd_order_tasks(int2* tiles, int64_t n, const GemmTask* tasks, int ntasks) {
+    if (n <= 8) return;
+    std::vector<int64_t> beg((size_t)ntasks + 1, 0);
+    for (int64_t i = 0; i < n; ++i) beg[(size_t)tiles[i].x + 1]++;
+    for (int t = 0; t < ntasks; ++t) beg[t + 1] += beg[t];
+    std::vector<int> ord((size_t)ntasks);
+    for (int t = 0; t < ntasks; ++t) ord[t] = t;
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return tasks[a].K > tasks[b].K; });
+    std::vector<std::vector<int2>> per(8);
+    int p = 0;
+    for (int t : ord) {
+        const int64_t nt = beg[t + 1] - beg[t], base = nt / 8, rem = nt % 8;
+        int64_t off = beg[t];
+        for (int x = 0; x < 8; ++x) {
+            const int64_t cnt = base + (((x - p + 8) % 8) < rem ? 1 : 0);
+            per[x].insert(per[x].end(), tiles + off, tiles + off + cnt);
+            off += cnt;
+        }
+        p = (int)((p + rem) % 8);
+    }
+    for (int x = 0; x < 8; ++x)
+        if ((int64_t)per[x].size() != (n - x + 7) / 8) return xcd_order(tiles, n);  // cannot happen
+    for (int64_t b = 0; b < n; ++b) tiles[b] = per[b % 8][b / 8];
+}
+
 static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vector<int2>& asmv,
                               std::vector<int2>& potrf, std::vector<int4>& trsm,
                               std::vector<GemmTask>& gemm, std::vector<int2>& tiles) {
@@ -124,7 +155,7 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             gemm.push_back(tasks[q]);
         }
         L.count = (int32_t)((int64_t)tiles.size() - L.toff);
-        xcd_order(tiles.data() + L.toff, L.count);
+        xcd_order_tasks(tiles.data() + L.toff, L.count, tasks.data(), (int)tasks.size());
         L.ntasks = (int32_t)tasks.size();
         L.big = big;
         L.flops = flops;
