@@ -79,6 +79,8 @@ def main():
     ap.add_argument("--relax-wmax", type=int, default=None)
     ap.add_argument("--nbo", type=int, default=None, help="panel outer block (rank-k update width)")
     ap.add_argument("--lookahead", type=int, default=None)
+    ap.add_argument("--panel-variant", type=int, default=None)
+    ap.add_argument("--inner-order", type=int, default=None)
     ap.add_argument("--tile", type=int, default=None, help="SYRK tile: 0 auto, 64, 128")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
@@ -119,6 +121,10 @@ def main():
         kw["panel_nb_outer"] = args.nbo
     if args.lookahead is not None:
         kw["lookahead"] = args.lookahead
+    if args.panel_variant is not None:
+        kw["panel_variant"] = args.panel_variant
+    if args.inner_order is not None:
+        kw["inner_order"] = args.inner_order
     if args.tile is not None:
         kw["syrk_tile"] = args.tile
     symb = sc.Symbolic(A, **kw)
@@ -207,7 +213,8 @@ def main():
             "work_share_per_rank": work_share,
             "options": {"relax_wmax": symb.opt.relax_wmax, "panel_nb_outer": symb.opt.panel_nb_outer,
                         "small_front_max": symb.opt.small_front_max, "use_graph": symb.opt.use_graph,
-                        "lookahead": symb.opt.lookahead, "syrk_tile": symb.opt.syrk_tile},
+                        "lookahead": symb.opt.lookahead, "syrk_tile": symb.opt.syrk_tile,
+                        "panel_variant": symb.opt.panel_variant, "inner_order": symb.opt.inner_order},
         },
         "roofline": roof,
         "timing_s": {"generate": round(t_gen, 3), "analyze": round(t_an, 3), "numeric_create": round(t_alloc, 3)},

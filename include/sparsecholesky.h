@@ -61,8 +61,11 @@ typedef struct sc_options {
     int32_t use_graph;       /* capture the level schedule into a hipGraph and replay it */
     int32_t relax_wmax;      /* never amalgamate two supernodes that are both wider than this */
     int32_t syrk_tile;       /* 0 = auto (128x128/8 waves for wide, deep updates, else 64x64/4 waves); 64; 128 */
-    int32_t lookahead;       /* 0: none; 1: trailing panel updates on a 2nd stream; 2: same, 2nd stream CU-masked to 7/8 */
-    int32_t reserved[5];
+    int32_t lookahead;       /* 0: none; 1: trailing panel updates on a 2nd stream; 2: same, at most one of their
+                                workgroups per CU; 3: same, 2nd stream CU-masked to 7/8 */
+    int32_t panel_variant;   /* large-front POTRF/TRSM kernels: 1 pipelined substitution, 2 inverse + MFMA (0 = default) */
+    int32_t inner_order;     /* updates inside a slab: 0 right-looking (K = 64), 1 recursive (K = 64..NBO/2) */
+    int32_t reserved[3];
 } sc_options;
 
 /* Symbolic statistics (host analysis). */

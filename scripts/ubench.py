@@ -17,13 +17,14 @@ def run(which, M, K, reps, arg):
 def panel():
     out = {}
     for M in (2048, 16384):
-        out[f"M={M} potrf v0 us"] = run(2, M, 1, 20, 0)
-        out[f"M={M} potrf v1 us"] = run(2, M, 1, 20, 1)
-        out[f"M={M} trsm v0 us"] = run(3, M, 1, 20, 0)
-        out[f"M={M} trsm v1 us"] = run(3, M, 1, 20, 1)
-        t = C.c_double()
-        rc = sc.lib().sc_debug_bench(4, M, 1, 1, 0, C.byref(t))
-        out[f"M={M} max|v0-v1|"] = t.value if rc == 0 else f"rc={rc}"
+        for v in (0, 1, 2):
+            out[f"M={M} potrf v{v} us"] = run(2, M, 1, 20, v)
+        for v in (0, 1, 2):
+            out[f"M={M} trsm v{v} us"] = run(3, M, 1, 20, v)
+        for v in (1, 2):
+            t = C.c_double()
+            rc = sc.lib().sc_debug_bench(4, M, 1, 1, v, C.byref(t))
+            out[f"M={M} max|v0-v{v}|"] = t.value if rc == 0 else f"rc={rc}"
     for k, v in out.items():
         print(f"{k:45s} {v}")
     print(json.dumps(out))

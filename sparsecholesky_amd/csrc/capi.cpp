@@ -74,6 +74,8 @@ void sc_default_options(sc_options* opt) {
     opt->relax_wmax = 128;
     opt->syrk_tile = 0;
     opt->lookahead = 1;
+    opt->panel_variant = 0;
+    opt->inner_order = 1;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,

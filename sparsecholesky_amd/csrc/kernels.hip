@@ -340,9 +340,55 @@ __global__ __launch_bounds__(64) void potrf_diag_g_kernel(DevPlan P, const int2*
         if (c <= lane) buf_st(r[c], rs, lane * 8, c * m * 8);
 }
 
+// Variant 2 (default), diagonal block: POTRF as above, then the same wave forms
+// W = inv(L11)^T by running the generated row solve on the identity rows (lane q
+// solves e_q L11^-T = column q of inv(L11)), and stores the strictly upper part of
+// W into the unused strictly upper triangle of the diagonal block:
+// blk[j*m + q] = inv(L11)(j, q), q < j.  diag(W) = 1 / diag(L11).
+__global__ __launch_bounds__(64) void potrf_inv_kernel(DevPlan P, const int2* __restrict__ tasks) {
+    __shared__ double C[2 * PNB];
+    __shared__ double2 S[TRSM64_STREAM / 2 + PNB / 2];  // + one dummy slot per lane
+    const int2 t = tasks[blockIdx.x];
+    const int s = t.x, k0 = t.y;
+    const int c0 = P.sn_start[s];
+    const int w = P.sn_start[s + 1] - c0;
+    const int m = P.sn_m[s];
+    const int nb = min(PNB, w - k0);
+    double* blk = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m + k0;
+    const int lane = threadIdx.x;
+    if (nb < PNB) {
+        potrf_block_wave(blk, m, nb, lane, C, P.info, c0 + k0);
+        return;
+    }
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(blk, (uint32_t)m * PNB * 8u);
+    double r[PNB];
+#pragma unroll
+    for (int c = 0; c < PNB; ++c) r[c] = buf_ld(rs, lane * 8, c * m * 8);
+    const int bad = potrf64_full(r, C, lane);
+    if (bad >= 0 && lane == 0) report_fail(P.info, c0 + k0 + bad);
+    // L11 operand stream (1/L(c,c), L(c+1..63, c)) for the inverse; lane q owns row q
+    // (branch-free: masked stores go out of buffer range / to a dummy LDS slot)
+    double* Sd = reinterpret_cast<double*>(S);
+    double diag = 0.0;
+#pragma unroll
+    for (int c = 0; c < PNB; ++c) {
+        buf_st(r[c], rs, c <= lane ? lane * 8 : BUF_DEAD, c * m * 8);
+        Sd[c < lane ? PNB * c - c * (c - 1) / 2 + (lane - c) : TRSM64_STREAM + lane] = r[c];
+        diag = (c == lane) ? r[c] : diag;
+    }
+    Sd[PNB * lane - lane * (lane - 1) / 2] = 1.0 / diag;
+#pragma unroll
+    for (int c = 0; c < PNB; ++c) r[c] = (c == lane) ? 1.0 : 0.0;
+    trsm64_full(r, S);  // r[i] = inv(L11)(i, lane), i >= lane
+#pragma unroll
+    for (int c = 0; c < PNB; ++c) buf_st(r[c], rs, c > lane ? lane * 8 : BUF_DEAD, c * m * 8);
+}
+
 // Partial last block (nb < 64) of the panel TRSM: template path, kept out of
 // line so its registers do not constrain the generated full-block code.
-__device__ __noinline__ void trsm_partial(double* pan, int m, int k0, int nb, int r0, double* Lc, double* invd) {
+// Rows [r0, r0 + nrows).
+__device__ __forceinline__ void trsm_partial(double* pan, int m, int k0, int nb, int r0, int nrows, double* Lc,
+                                             double* invd) {
     constexpr int LD = PNB + 2;
     const int tid = threadIdx.x;
     const double* blk = pan + (int64_t)k0 * m + k0;
@@ -354,7 +400,7 @@ __device__ __noinline__ void trsm_partial(double* pan, int m, int k0, int nb, in
     }
     __syncthreads();
     const int row = r0 + tid;
-    const bool live = row < m;
+    const bool live = row < m && tid < nrows;
     double* xs = pan + (int64_t)k0 * m + (live ? row : r0);
     double r[PNB];
 #pragma unroll
@@ -365,6 +411,19 @@ __device__ __noinline__ void trsm_partial(double* pan, int m, int k0, int nb, in
         for (int c = 0; c < PNB; ++c)
             if (c < nb) xs[(int64_t)c * m] = r[c];
     }
+}
+
+// Partial last blocks (nb < 64) of the panel TRSM, launched separately so the
+// full-block kernels keep their own register budgets.  Rows [r0, r0 + nrows).
+__global__ __launch_bounds__(256) void trsm_partial_kernel(DevPlan P, const int4* __restrict__ tasks, int nrows) {
+    __shared__ double Lc[PNB * (PNB + 2)];
+    __shared__ double invd[PNB];
+    const int4 t = tasks[blockIdx.x];
+    const int s = t.x, k0 = t.y, r0 = t.z;
+    const int c0 = P.sn_start[s];
+    const int w = P.sn_start[s + 1] - c0;
+    const int m = P.sn_m[s];
+    trsm_partial(P.panel_pool + P.panel_off[s], m, k0, min(PNB, w - k0), r0, nrows, Lc, invd);
 }
 
 // Panel TRSM, rows [r0, r0 + 256): L11 operands packed into an LDS stream in the
@@ -379,12 +438,7 @@ __global__ __launch_bounds__(256) void trsm_panel_g_kernel(DevPlan P, const int4
     const int m = P.sn_m[s];
     const int nb = min(PNB, w - k0);
     double* pan = P.panel_pool + P.panel_off[s];
-    if (nb < PNB) {
-        __shared__ double Lc[PNB * (PNB + 2)];
-        __shared__ double invd[PNB];
-        trsm_partial(pan, m, k0, nb, r0, Lc, invd);
-        return;
-    }
+    if (nb < PNB) return;  // partial blocks: trsm_partial_kernel
     const double* blk = pan + (int64_t)k0 * m + k0;
     const int row = r0 + tid;
     // the 64 block columns, m rows each (< 2^31 bytes for m < 4M); dead lanes masked
@@ -405,6 +459,58 @@ __global__ __launch_bounds__(256) void trsm_panel_g_kernel(DevPlan P, const int4
     trsm64_full(r, S);
 #pragma unroll
     for (int c = 0; c < PNB; ++c) buf_st(r[c], rs, voff, c * m * 8);
+}
+
+// Variant 2 (default) panel TRSM: X := X W with W = inv(L11)^T from
+// potrf_inv_kernel, on fp64 MFMA (v_mfma_f64_16x16x4_f64).  Rows [r0, r0 + 64):
+// wave v owns rows r0 + 16v .. + 16 (A fragments = its 16 x 64 block of X in
+// registers), 4 column tiles of 16, k-blocks above the triangle skipped (40 MFMAs
+// per wave).  No dependent chain: the solve is one small GEMM per row block.
+__global__ __launch_bounds__(256) void trsm_panel_mfma_kernel(DevPlan P, const int4* __restrict__ tasks) {
+    __shared__ double dinv[PNB];  // 1 / L11(q, q) = W(q, q); the rest of W is read from L2
+    const int4 t = tasks[blockIdx.x];
+    const int s = t.x, k0 = t.y, r0 = t.z;
+    const int tid = threadIdx.x;
+    const int c0 = P.sn_start[s];
+    const int w = P.sn_start[s + 1] - c0;
+    const int m = P.sn_m[s];
+    const int nb = min(PNB, w - k0);
+    double* pan = P.panel_pool + P.panel_off[s];
+    if (nb < PNB) return;  // partial blocks: trsm_partial_kernel
+    const double* blk = pan + (int64_t)k0 * m + k0;
+    if (tid < PNB) dinv[tid] = 1.0 / blk[(int64_t)tid * m + tid];
+    __syncthreads();
+    const int lane = tid & 63;
+    const int i0 = r0 + 16 * (tid >> 6);
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pan + (int64_t)k0 * m, (uint32_t)m * PNB * 8u);
+    // A(i, k) = X(i0 + (lane & 15), 4 kk + (lane >> 4))
+    const int arow = i0 + (lane & 15);
+    const int avoff = arow < m ? arow * 8 + (lane >> 4) * m * 8 : BUF_DEAD;
+    double a[16];
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) a[kk] = buf_ld(rs, avoff, 4 * kk * m * 8);
+    double4_t acc[4];
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt) acc[jt] = (double4_t){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+        for (int jt = kk / 4; jt < 4; ++jt) {
+            // B(k, j) = W(q, j), q = 4 kk + (lane >> 4), j = 16 jt + (lane & 15):
+            // inv(L11)(j, q) in the upper triangle for q < j, 1/L(q,q) on the diagonal
+            const int q = 4 * kk + (lane >> 4), j = 16 * jt + (lane & 15);
+            const double v = blk[(int64_t)j * m + q];
+            const double b = (q < j) ? v : ((q == j) ? dinv[q] : 0.0);
+            acc[jt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kk], b, acc[jt], 0, 0, 0);
+        }
+    // D(row, col): col = lane & 15, row = (lane >> 4) + 4 r
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int row = i0 + MFMA_F64_ROW(lane, r);
+        const int voff = row < m ? row * 8 + (lane & 15) * m * 8 : BUF_DEAD;
+#pragma unroll
+        for (int jt = 0; jt < 4; ++jt) buf_st(acc[jt][r], rs, voff, 16 * jt * m * 8);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -529,36 +635,53 @@ hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hip
     if (count <= 0) return hipSuccess;
     if (variant == 0)
         hipLaunchKernelGGL(potrf_diag_kernel, dim3(count), dim3(64), 0, st, P, tasks);
-    else
+    else if (variant == 1)
         hipLaunchKernelGGL(potrf_diag_g_kernel, dim3(count), dim3(64), 0, st, P, tasks);
+    else
+        hipLaunchKernelGGL(potrf_inv_kernel, dim3(count), dim3(64), 0, st, P, tasks);
     return hipGetLastError();
 }
 
-hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st, int variant) {
+hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st, int variant,
+                             bool partial) {
     if (count <= 0) return hipSuccess;
-    if (variant == 0)
+    if (partial && variant > 0)
+        hipLaunchKernelGGL(trsm_partial_kernel, dim3(count), dim3(256), 0, st, P, tasks, trsm_task_rows(variant));
+    else if (variant == 0)
         hipLaunchKernelGGL(trsm_panel_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks);
-    else
+    else if (variant == 1)
         hipLaunchKernelGGL(trsm_panel_g_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks);
+    else
+        hipLaunchKernelGGL(trsm_panel_mfma_kernel, dim3(count), dim3(256), 0, st, P, tasks);
     return hipGetLastError();
 }
 
 // TAG only separates the launches in profiles: 0 = panel update, 1 = CB update.
 // bt = 64: 64x64 tiles on 4 waves (2x2); bt = 128: 128x128 tiles on 8 waves (2x4).
+// one_per_cu: reserve unused dynamic LDS so that at most one workgroup of this
+// launch sits on a CU (the overlapped lookahead GEMMs leave room for the panel
+// chain's kernels instead of filling every CU twice).
 template <int TAG>
-static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int bt, hipStream_t st) {
-    if (bt == 128)
-        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG>), dim3(n), dim3(512), 0, st, tasks, tiles);
-    else
-        hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG>), dim3(n), dim3(256), 0, st, tasks, tiles);
+static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int bt, bool one_per_cu, hipStream_t st) {
+    constexpr size_t kHalfLds = 80 * 1024;
+    if (bt == 128) {
+        constexpr size_t stat = 2 * 2 * 16 * (128 + 16) * sizeof(double);
+        const size_t dyn = one_per_cu ? kHalfLds + 1024 - stat : 0;
+        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG>), dim3(n), dim3(512), dyn, st, tasks, tiles);
+    } else {
+        constexpr size_t stat = 2 * 2 * 16 * (64 + 16) * sizeof(double);
+        const size_t dyn = one_per_cu ? kHalfLds + 1024 - stat : 0;
+        hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG>), dim3(n), dim3(256), dyn, st, tasks, tiles);
+    }
 }
 
-hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st) {
+hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
+                       bool one_per_cu) {
     if (total_tiles <= 0) return hipSuccess;
     if (tag)
-        launch_syrk_t<1>(tasks, tiles, total_tiles, bt, st);
+        launch_syrk_t<1>(tasks, tiles, total_tiles, bt, one_per_cu, st);
     else
-        launch_syrk_t<0>(tasks, tiles, total_tiles, bt, st);
+        launch_syrk_t<0>(tasks, tiles, total_tiles, bt, one_per_cu, st);
     return hipGetLastError();
 }
 

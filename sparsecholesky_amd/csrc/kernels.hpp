@@ -54,10 +54,21 @@ hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count,
                               hipStream_t st);
 hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count, const double* Ax,
                                  hipStream_t st);
-// variant 0: LDS-broadcast kernels (kept for A/B microbenchmarks), 1: register/SGPR kernels
-hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hipStream_t st, int variant = 1);
-hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st, int variant = 1);
-hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st);
+// Panel kernel variants: 0 LDS-broadcast substitution, 1 generated pipelined
+// substitution (256 rows per TRSM task), 2 (default) POTRF + inv(L11) and MFMA TRSM
+// (TRSM_MFMA_ROWS rows per task; needs variant-2 POTRF output).  0/1 are kept
+// for A/B microbenchmarks (sc_debug_bench).
+constexpr int PANEL_VARIANT = 1;
+constexpr int TRSM_MFMA_ROWS = 64;
+inline int trsm_task_rows(int variant) { return variant >= 2 ? TRSM_MFMA_ROWS : TRSM_ROWS; }
+hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hipStream_t st,
+                             int variant = PANEL_VARIANT);
+// partial: every task is a partial last block (nb < 64); variants 1/2 need those
+// in a separate launch (the full-block kernels skip them)
+hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st,
+                             int variant = PANEL_VARIANT, bool partial = false);
+hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
+                       bool one_per_cu = false);
 hipError_t launch_stamp(uint64_t* slot, hipStream_t st);
 hipError_t launch_fill_random(double* p, int64_t n, hipStream_t st);
 hipError_t launch_mfma_peak(double* out, int blocks, int iters, int nacc, hipStream_t st);

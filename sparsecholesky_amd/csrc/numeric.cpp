@@ -238,6 +238,7 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             Lt.level = lev;
             Lt.off = (int64_t)trsm.size();
             std::vector<GemmTask> upd, outer_a, outer_b;
+            std::vector<int4> trsm_part;  // partial last blocks: own launch (big = 1)
             double uflops = 0.0, afl = 0.0, bfl = 0.0;
             for (int32_t s : large) {
                 const int w = S.w(s), m = S.sn_m[s];
@@ -245,11 +246,20 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
                 const int nb = std::min(PNB, w - k0);
                 const int k1 = k0 + nb;
                 potrf.push_back(make_int2(s, k0));
-                for (int r0 = k1; r0 < m; r0 += TRSM_ROWS) trsm.push_back(make_int4(s, k0, r0, 0));
+                for (int r0 = k1; r0 < m; r0 += trsm_task_rows(N.panel_variant))
+                    (nb < PNB ? trsm_part : trsm).push_back(make_int4(s, k0, r0, 0));
                 double* pan = panel_pool + S.panel_off[s];
                 const int slab0 = (k0 / NBO) * NBO;
                 const int slab1 = std::min(w, slab0 + NBO);
-                if (k1 < slab1) {
+                if (k1 < slab1 && S.opt.inner_order == 1) {
+                    // recursive order: block b of the slab closes a run of 2^t blocks
+                    // (t = trailing zeros of b + 1); that run updates the next 2^t
+                    // blocks (K = 64 * 2^t).  Same flops and dependencies as
+                    // right-looking, 768 instead of 1792 C columns rewritten per slab.
+                    const int b = (k0 - slab0) / PNB;
+                    const int span = PNB << __builtin_ctz((unsigned)(b + 1));
+                    add_update(upd, uflops, pan, m, k1, std::min(slab1, k1 + span), k1 - span, k1);
+                } else if (k1 < slab1) {
                     add_update(upd, uflops, pan, m, k1, slab1, k0, k1);
                 } else if (k1 == slab1 && slab1 < w) {
                     const int nxt = S.opt.lookahead ? std::min(w, slab1 + NBO) : w;
@@ -261,6 +271,14 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             Lt.count = (int32_t)((int64_t)trsm.size() - Lt.off);
             if (Lp.count > 0) N.sched.push_back(Lp);
             if (Lt.count > 0) N.sched.push_back(Lt);
+            if (!trsm_part.empty()) {
+                Launch Lq = Lt;
+                Lq.off = (int64_t)trsm.size();
+                Lq.count = (int32_t)trsm_part.size();
+                Lq.big = 1;
+                trsm.insert(trsm.end(), trsm_part.begin(), trsm_part.end());
+                N.sched.push_back(Lq);
+            }
             push_gemm_launch(L_PANEL, lev, upd, 0, uflops);
             int e_trsm = -1;
             if (!outer_b.empty()) e_trsm = push_record(0);
@@ -381,7 +399,7 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     int prio_lo = 0, prio_hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     bool ok = hipStreamCreateWithPriority(&N.stream, hipStreamNonBlocking, prio_hi) == hipSuccess;
-    if (ok && S.opt.lookahead == 2) {
+    if (ok && S.opt.lookahead == 3) {
         // trailing updates may not use every 8th CU: the critical path always finds room
         hipDeviceProp_t prop;
         (void)hipGetDeviceProperties(&prop, device);
@@ -398,6 +416,7 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
         return fail(SC_ERR_HIP);
     }
     N.use_graph = S.opt.use_graph != 0;
+    N.panel_variant = (S.opt.panel_variant == 1 || S.opt.panel_variant == 2) ? S.opt.panel_variant : PANEL_VARIANT;
     const int32_t ns = S.ns;
     int64_t rc;
     DevPlan& P = N.P;
@@ -470,12 +489,13 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
         case L_ASM:
             return launch_assemble_large(N.P, N.d_asm + L.off, L.count, d_Ax, N.stream);
         case L_POTRF:
-            return launch_potrf_diag(N.P, N.d_potrf + L.off, L.count, N.stream);
+            return launch_potrf_diag(N.P, N.d_potrf + L.off, L.count, N.stream, N.panel_variant);
         case L_TRSM:
-            return launch_trsm_panel(N.P, N.d_trsm + L.off, L.count, N.stream);
+            return launch_trsm_panel(N.P, N.d_trsm + L.off, L.count, N.stream, N.panel_variant, L.big != 0);
         case L_PANEL:
         case L_CB:
-            return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st);
+            return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st,
+                               L.strm == 1 && N.S->opt.lookahead == 2);
         case L_COMM:
             return comm_launch(N, L);
     }
@@ -770,17 +790,22 @@ static int64_t bench_panel(int which, int M, int reps, int arg, double* out) {
         for (int i = 0; i < M; ++i) h[(size_t)j * M + i] = (i == j) ? 64.0 : rnd();
     int32_t hs[2] = {0, w}, hm[1] = {M};
     int64_t ho[2] = {0, (int64_t)nel};
-    std::vector<int4> tr;
-    for (int r0 = w; r0 < M; r0 += TRSM_ROWS) tr.push_back(make_int4(0, 0, r0, 0));
+    // which 3: TRSM variant arg (after a POTRF of the matching variant); which 4:
+    // variant 0 vs variant arg (1 or 2)
+    const int var = std::max(1, std::min(2, arg));
+    std::vector<int4> tr, tr0;
+    for (int r0 = w; r0 < M; r0 += trsm_task_rows(var)) tr.push_back(make_int4(0, 0, r0, 0));
+    for (int r0 = w; r0 < M; r0 += trsm_task_rows(0)) tr0.push_back(make_int4(0, 0, r0, 0));
     int2 pt = make_int2(0, 0);
     void *d_pan = nullptr, *d_pan2 = nullptr, *d_ref = nullptr, *d_s = nullptr, *d_m = nullptr, *d_o = nullptr,
-         *d_info = nullptr, *d_pt = nullptr, *d_tr = nullptr;
+         *d_info = nullptr, *d_pt = nullptr, *d_tr = nullptr, *d_tr0 = nullptr;
     const size_t bytes = (nel + PNB) * sizeof(double);
     int64_t rc = SC_OK;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (hipMalloc(&d_pan, bytes) || hipMalloc(&d_pan2, bytes) || hipMalloc(&d_ref, bytes) || hipMalloc(&d_s, 8) ||
         hipMalloc(&d_m, 4) || hipMalloc(&d_o, 16) || hipMalloc(&d_info, 4) || hipMalloc(&d_pt, 8) ||
-        hipMalloc(&d_tr, std::max<size_t>(1, tr.size()) * sizeof(int4)) || hipEventCreate(&e0) ||
+        hipMalloc(&d_tr, std::max<size_t>(1, tr.size()) * sizeof(int4)) ||
+        hipMalloc(&d_tr0, std::max<size_t>(1, tr0.size()) * sizeof(int4)) || hipEventCreate(&e0) ||
         hipEventCreate(&e1)) {
         rc = SC_ERR_DEVMEM;
     } else {
@@ -791,6 +816,7 @@ static int64_t bench_panel(int which, int M, int reps, int arg, double* out) {
         (void)hipMemset(d_info, 0, 4);
         (void)hipMemcpy(d_pt, &pt, 8, hipMemcpyHostToDevice);
         if (!tr.empty()) (void)hipMemcpy(d_tr, tr.data(), tr.size() * sizeof(int4), hipMemcpyHostToDevice);
+        if (!tr0.empty()) (void)hipMemcpy(d_tr0, tr0.data(), tr0.size() * sizeof(int4), hipMemcpyHostToDevice);
         DevPlan P {};
         P.sn_start = (const int32_t*)d_s;
         P.sn_m = (const int32_t*)d_m;
@@ -801,13 +827,16 @@ static int64_t bench_panel(int which, int M, int reps, int arg, double* out) {
             Q.panel_pool = (double*)pan;
             return Q;
         };
-        const int nt = (int)tr.size();
+        const int nt = (int)tr.size(), nt0 = (int)tr0.size();
         if (which == 4) {
             for (int v = 0; v < 2; ++v) {
                 void* dst = v ? d_pan2 : d_pan;
                 (void)hipMemcpy(dst, d_ref, bytes, hipMemcpyDeviceToDevice);
-                (void)launch_potrf_diag(on(dst), (const int2*)d_pt, 1, nullptr, v);
-                (void)launch_trsm_panel(on(dst), (const int4*)d_tr, nt, nullptr, v);
+                (void)launch_potrf_diag(on(dst), (const int2*)d_pt, 1, nullptr, v ? var : 0);
+                if (v)
+                    (void)launch_trsm_panel(on(dst), (const int4*)d_tr, nt, nullptr, var);
+                else
+                    (void)launch_trsm_panel(on(dst), (const int4*)d_tr0, nt0, nullptr, 0);
             }
             (void)hipDeviceSynchronize();
             std::vector<double> a(nel), b(nel);
@@ -819,13 +848,15 @@ static int64_t bench_panel(int which, int M, int reps, int arg, double* out) {
             *out = md;
         } else {
             (void)hipMemcpy(d_pan, d_ref, bytes, hipMemcpyDeviceToDevice);
-            (void)launch_potrf_diag(on(d_pan), (const int2*)d_pt, 1, nullptr, 1);
+            (void)launch_potrf_diag(on(d_pan), (const int2*)d_pt, 1, nullptr, arg >= 2 ? 2 : 1);
             double tot = 0.0;
             for (int r = 0; r < reps + 1; ++r) {
                 if (which == 2) (void)hipMemcpy(d_pan, d_ref, bytes, hipMemcpyDeviceToDevice);
                 (void)hipEventRecord(e0, nullptr);
                 if (which == 2)
                     (void)launch_potrf_diag(on(d_pan), (const int2*)d_pt, 1, nullptr, arg);
+                else if (arg == 0)
+                    (void)launch_trsm_panel(on(d_pan), (const int4*)d_tr0, nt0, nullptr, 0);
                 else
                     (void)launch_trsm_panel(on(d_pan), (const int4*)d_tr, nt, nullptr, arg);
                 (void)hipEventRecord(e1, nullptr);
@@ -838,7 +869,7 @@ static int64_t bench_panel(int which, int M, int reps, int arg, double* out) {
         }
         if (hipGetLastError() != hipSuccess) rc = SC_ERR_HIP;
     }
-    for (void* p : {d_pan, d_pan2, d_ref, d_s, d_m, d_o, d_info, d_pt, d_tr})
+    for (void* p : {d_pan, d_pan2, d_ref, d_s, d_m, d_o, d_info, d_pt, d_tr, d_tr0})
         if (p) (void)hipFree(p);
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);

@@ -50,6 +50,7 @@ struct Launch {
 struct Numeric {
     const Symbolic* S = nullptr;
     int device = 0;
+    int panel_variant = PANEL_VARIANT;  // large-front POTRF/TRSM kernels (kernels.hpp)
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;  // trailing panel updates overlapped with the next slab
     std::vector<hipEvent_t> sync_ev;

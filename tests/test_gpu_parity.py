@@ -278,6 +278,24 @@ def test_dense_matrix_large_front(gpu):
     assert s["n_supernodes"] == 1 and s["max_front_w"] == n
 
 
+# large-front schedule variants: panel kernels (1 substitution, 2 inverse + MFMA
+# TRSM), inner slab update order (0 right-looking, 1 recursive), lookahead modes
+PANEL_OPTS = [dict(panel_variant=2), dict(inner_order=0), dict(panel_variant=2, inner_order=0, lookahead=0),
+              dict(lookahead=2), dict(panel_variant=2, lookahead=3), dict(lookahead=0)]
+
+
+@pytest.mark.parametrize("opts", PANEL_OPTS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
+def test_panel_schedule_variants(gpu, opts):
+    check_parity(sc.laplacian3d(16), small_front_max=0, **opts)
+    # one dense front of 1350 columns: three slabs, the last partial, recursive runs of 1..4 blocks
+    n = 1350
+    rng = np.random.default_rng(5)
+    M = rng.standard_normal((n, n))
+    D = M @ M.T + n * np.eye(n)
+    iu = np.triu_indices(n)
+    check_parity(sc.triplet_to_csc_matrix(iu[0], iu[1], D[iu], n), **opts)
+
+
 def test_empty_matrix_gpu(gpu):
     A = sc.csc_matrix(0, 0, np.zeros(1, dtype=np.int64), np.zeros(0, dtype=np.int32), np.zeros(0))
     r = sc.chol(A)
