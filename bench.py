@@ -67,6 +67,21 @@ def cpu_baseline(k=32, reps=2):
     }
 
 
+def cb_syrk_traffic():
+    """HBM bytes per CB SYRK launch from the committed PMC profile
+    (scripts/gpu_pmc.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE
+    doubled per the gfx950 note); None when the profile is absent."""
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01", "pmc_summary.json")
+    try:
+        with open(p) as f:
+            cb = json.load(f)["cb_syrk_128"]
+    except (OSError, KeyError, ValueError):
+        return None, None
+    b = cb["fetch_bytes_per_launch"] + cb["write_bytes_per_launch"]
+    return round(b), ("bytes per syrk_mfma_kernel<128,2,4,1> launch (FETCH_SIZE x2 + WRITE_SIZE), "
+                      "profiles/r01/pmc_summary.json; L2-miss bytes incl. Infinity-Cache hits")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -174,15 +189,22 @@ def main():
     phases = None
     if not args.graph:
         phases = [round(x, 3) for x in num.timing().tolist()]
-    fl, ms, nl = num.syrk_stats(256)
+    # dominant kernel = the CB SYRK instance on 128 x 128 tiles (the dispatches the
+    # rocprofv3 kernel trace lists as syrk_mfma_kernel<128, 2, 4, 1>)
+    fl, ms, nl = num.syrk_stats(-2)
+    gfl, gms, gnl = num.syrk_stats(256)
     if ms > 0 and nl > 0:
         ach = fl / (ms * 1e-3) / 1e12
+        traffic, tnote = cb_syrk_traffic()
         roof = {
             "bound": "mfma", "achieved": round(ach, 3), "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(ach / FP64_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-            "kernel": "syrk_mfma_kernel<*,1> (CB update, fronts w>=256)" + (" on rank 0" if world > 1 else ""),
+            "frac": round(ach / FP64_MFMA_PEAK_TFLOPS, 4), "traffic": traffic, "traffic_note": tnote,
+            "kernel": "syrk_mfma_kernel<128,2,4,1> (CB update)" + (" on rank 0" if world > 1 else ""),
             "flops_per_step": fl, "kernel_ms_per_step": round(ms, 3), "launches_per_step": nl,
+            "avg_launch_ms": round(ms / nl, 3),
         }
+        if gms > 0:
+            roof["gate_w256_tflops"] = round(gfl / (gms * 1e-3) / 1e12, 3)
     pfl, pms, pnl = num.syrk_stats(-1) if not args.graph else (0.0, -1.0, 0)
     cfl, cms, cnl = num.syrk_stats(0)
     if roof is not None and pms > 0 and cms > 0:

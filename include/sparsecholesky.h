@@ -154,7 +154,8 @@ int64_t sc_numeric_launch_trace(sc_numeric* num, int32_t* kind, int32_t* level, 
                                 double* flops, int64_t cap);
 /* SYRK flops and kernel time (ms) of the last factorization restricted to
  * fronts with w >= wmin (north-star gate: wmin = 256); wmin = 0: every CB launch;
- * wmin = -1: the panel-update launches. */
+ * wmin = -1: the panel-update launches; wmin = -2: the CB launches on 128 x 128
+ * tiles (one kernel instance, comparable with a kernel trace). */
 int64_t sc_numeric_syrk_stats(sc_numeric* num, int32_t wmin, double* flops, double* ms,
                               int64_t* launches);
 void sc_free_numeric(sc_numeric* num);

@@ -678,15 +678,17 @@ int64_t numeric_timing(Numeric& N, double* t, int nt) {
 
 int64_t numeric_syrk_stats(Numeric& N, int wmin, double* flops, double* ms, int64_t* launches) {
     // CB SYRK launches are split by w >= 256; wmin selects them (0: all CB launches,
-    // -1: the panel-update launches instead)
+    // -1: the panel-update launches instead, -2: the CB launches on 128 x 128 tiles,
+    // i.e. exactly the syrk_mfma_kernel<128,2,4,1> dispatches a kernel trace lists)
     double fl = 0.0, t = 0.0;
     int64_t cnt = 0;
     bool have_t = N.status_valid && N.profile != 0;
     const std::vector<uint64_t> stamps = read_stamps(N);
     for (size_t i = 0; i < N.sched.size(); ++i) {
         const Launch& L = N.sched[i];
-        if (L.kind != (wmin < 0 ? L_PANEL : L_CB)) continue;
+        if (L.kind != (wmin == -1 ? L_PANEL : L_CB)) continue;
         if (wmin >= 256 && !L.big) continue;
+        if (wmin == -2 && L.bt != SYRK_BT_LARGE) continue;
         fl += L.flops;
         ++cnt;
         if (have_t) {
