@@ -65,7 +65,8 @@ typedef struct sc_options {
                                 workgroups per CU; 3: same, 2nd stream CU-masked to 7/8 */
     int32_t panel_variant;   /* large-front POTRF/TRSM kernels: 1 pipelined substitution, 2 inverse + MFMA (0 = default) */
     int32_t inner_order;     /* updates inside a slab: 0 right-looking (K = 64), 1 recursive (K = 64..NBO/2) */
-    int32_t reserved[3];
+    int32_t asm_tile_min_m;  /* fronts with m >= this use the write-once tiled assembly (0 = default 8192) */
+    int32_t reserved[2];
 } sc_options;
 
 /* Symbolic statistics (host analysis). */

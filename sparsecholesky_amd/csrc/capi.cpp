@@ -76,6 +76,7 @@ void sc_default_options(sc_options* opt) {
     opt->lookahead = 1;
     opt->panel_variant = 0;
     opt->inner_order = 1;
+    opt->asm_tile_min_m = 0;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,

@@ -113,7 +113,11 @@ __device__ __forceinline__ int lower_bound_i32(const int32_t* a, int n, int v) {
     return lo;
 }
 
-__global__ __launch_bounds__(256) void assemble_large_kernel(DevPlan P, const int2* __restrict__ tasks,
+// Column-streaming assembly (fronts with m < ASM_TILE_MIN_M): one workgroup per
+// (front, 16-column block), one wave per column.  Zeroes its columns, stores the A
+// entries, then adds every child's CB entries whose parent column falls in the
+// block (children in fixed order: deterministic).
+__global__ __launch_bounds__(256) void assemble_cols_kernel(DevPlan P, const int2* __restrict__ tasks,
                                                               const double* __restrict__ Ax) {
     const int2 t = tasks[blockIdx.x];
     const int s = t.x;
@@ -156,6 +160,66 @@ __global__ __launch_bounds__(256) void assemble_large_kernel(DevPlan P, const in
             for (int ic = jc + lane; ic < mbc; ic += 64) dst[rel[ic]] += src[ic];
         }
         __syncthreads();
+    }
+}
+
+// Write-once assembly, one workgroup per (front, 16 columns, 256-row tile): the
+// tile is built in LDS (zero, A entries, then each child's rows that map into it,
+// children in fixed order; relative indices are injective and increasing, so a
+// child's rows for the tile are one contiguous run, precomputed on the host in
+// rel_bnd) and its lower part is stored once.  HBM traffic: one write per front
+// entry plus one read per child entry (zero-then-add paid 8 + 24 B).
+__global__ __launch_bounds__(256) void assemble_tile_kernel(DevPlan P, const int2* __restrict__ tasks,
+                                                             const double* __restrict__ Ax) {
+    __shared__ double T[ASM_COLS * ASM_ROWS];  // T[(j - j0) * ASM_ROWS + (r - r0)]
+    const int2 t = tasks[blockIdx.x];
+    const int s = t.x;
+    const int k = t.y >> 16;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wid = tid >> 6;
+    const int c0 = P.sn_start[s];
+    const int w = P.sn_start[s + 1] - c0;
+    const int m = P.sn_m[s];
+    const int mb = m - w;
+    const int j0 = (t.y & 0xffff) * ASM_COLS;
+    const int j1 = min(m, j0 + ASM_COLS);
+    const int r0 = k * ASM_ROWS, r1 = min(m, r0 + ASM_ROWS);
+    double* panel = P.panel_pool + P.panel_off[s];
+    double* cbs = P.cb_pool + P.cb_off[s];
+    for (int idx = tid; idx < ASM_COLS * ASM_ROWS; idx += 256) T[idx] = 0.0;
+    __syncthreads();
+    for (int j = j0 + wid; j < min(j1, w); j += 4) {
+        const int64_t a0 = P.a_ptr[c0 + j], a1 = P.a_ptr[c0 + j + 1];
+        for (int64_t q = a0 + lane; q < a1; q += 64) {
+            const int p = P.a_pos[q];
+            if (p >= r0 && p < r1) T[(j - j0) * ASM_ROWS + (p - r0)] = Ax[P.a_src[q]];
+        }
+    }
+    __syncthreads();
+    for (int ci = P.child_ptr[s]; ci < P.child_ptr[s + 1]; ++ci) {
+        const int c = P.child_list[ci];
+        const int mbc = P.sn_m[c] - (P.sn_start[c + 1] - P.sn_start[c]);
+        const int32_t* __restrict__ rel = P.relind + P.rel_ptr[c];
+        const int32_t* __restrict__ bnd = P.rel_bnd + P.rb_ptr[c];
+        const int ilo = bnd[k], ihi = bnd[k + 1];
+        if (ilo < ihi) {
+            // child columns landing in [j0, j1) lie in row tile j0 / ASM_ROWS
+            const int u0 = bnd[j0 / ASM_ROWS], u1 = bnd[j0 / ASM_ROWS + 1];
+            const int jlo = u0 + lower_bound_i32(rel + u0, u1 - u0, j0);
+            const int jhi = u0 + lower_bound_i32(rel + u0, u1 - u0, j1);
+            const double* __restrict__ cb = P.cb_pool + P.cb_off[c];
+            for (int jc = jlo + wid; jc < jhi; jc += 4) {
+                const double* __restrict__ src = cb + (int64_t)jc * mbc;
+                double* Tc = T + (rel[jc] - j0) * ASM_ROWS - r0;
+                for (int ic = max(jc, ilo) + lane; ic < ihi; ic += 64) Tc[rel[ic]] += src[ic];
+            }
+        }
+        __syncthreads();
+    }
+    for (int j = j0 + wid; j < j1; j += 4) {
+        double* col = (j < w) ? panel + (int64_t)j * m : cbs + (int64_t)(j - w) * mb - w;
+        const double* Tc = T + (j - j0) * ASM_ROWS - r0;
+        for (int r = max(r0, j) + lane; r < r1; r += 64) col[r] = Tc[r];
     }
 }
 
@@ -625,9 +689,12 @@ hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count,
 }
 
 hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count, const double* Ax,
-                                 hipStream_t st) {
+                                 hipStream_t st, bool tiled) {
     if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(assemble_large_kernel, dim3(count), dim3(256), 0, st, P, tasks, Ax);
+    if (tiled)
+        hipLaunchKernelGGL(assemble_tile_kernel, dim3(count), dim3(256), 0, st, P, tasks, Ax);
+    else
+        hipLaunchKernelGGL(assemble_cols_kernel, dim3(count), dim3(256), 0, st, P, tasks, Ax);
     return hipGetLastError();
 }
 

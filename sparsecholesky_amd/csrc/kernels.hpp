@@ -14,6 +14,8 @@ constexpr int PNB = 64;
 constexpr int TRSM_ROWS = 256;
 // Columns owned by one assembly workgroup (one wave per column at a time).
 constexpr int ASM_COLS = 16;
+constexpr int ASM_ROWS = 256;  // rows per LDS tile of the write-once assembly
+constexpr int ASM_TILE_MIN_M = 8192;  // fronts at least this tall use the write-once tile kernel
 // Output tile edges of the MFMA SYRK kernel (per launch).
 constexpr int SYRK_BT_SMALL = 64;
 constexpr int SYRK_BT_LARGE = 128;
@@ -32,6 +34,8 @@ struct DevPlan {
     const int32_t* child_list;
     const int64_t* rel_ptr;     // ns+1
     const int32_t* relind;
+    const int64_t* rb_ptr;      // ns+1
+    const int32_t* rel_bnd;     // per child: CB row bounds of the parent's ASM_ROWS row tiles
     const int64_t* a_ptr;       // n+1 (internal columns)
     const int32_t* a_pos;       // row position in the column's front
     const int64_t* a_src;       // index into the input value array
@@ -52,8 +56,10 @@ struct GemmTask {
 
 hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count, int maxm, const double* Ax,
                               hipStream_t st);
+// tiled: tasks are (front, (row tile << 16) | 16-column block) for the write-once
+// tile kernel (fronts with m >= ASM_TILE_MIN_M), else (front, column block)
 hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count, const double* Ax,
-                                 hipStream_t st);
+                                 hipStream_t st, bool tiled);
 // Panel kernel variants: 0 LDS-broadcast substitution, 1 generated pipelined
 // substitution (256 rows per TRSM task), 2 (default) POTRF + inv(L11) and MFMA TRSM
 // (TRSM_MFMA_ROWS rows per task; needs variant-2 POTRF output).  0/1 are kept

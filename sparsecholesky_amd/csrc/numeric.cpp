@@ -195,17 +195,30 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         for (int32_t s : nodes)
             if (S.fclass[s] == FRONT_LARGE) large.push_back(s);
         if (large.empty()) return;
-        {
+        // assembly: fronts with m >= ASM_TILE_MIN_M one workgroup per (front, 16
+        // columns, 256-row tile), write-once (big = 1); smaller fronts one workgroup per
+        // (front, 16 columns) streaming child columns (measured faster below ~8k rows)
+        const int tile_min_m = S.opt.asm_tile_min_m > 0 ? S.opt.asm_tile_min_m : ASM_TILE_MIN_M;
+        for (int tiled = 1; tiled >= 0; --tiled) {
             Launch L {};
             L.kind = L_ASM;
             L.level = lev;
+            L.big = tiled;
             L.off = (int64_t)asmv.size();
             for (int32_t s : large) {
                 const int m = S.sn_m[s];
-                for (int cb = 0; cb * ASM_COLS < m; ++cb) asmv.push_back(make_int2(s, cb));
+                if ((m >= tile_min_m) != (tiled == 1)) continue;
+                for (int cb = 0; cb * ASM_COLS < m; ++cb) {
+                    if (!tiled) {
+                        asmv.push_back(make_int2(s, cb));
+                        continue;
+                    }
+                    for (int k = cb * ASM_COLS / ASM_ROWS; k * ASM_ROWS < m; ++k)
+                        asmv.push_back(make_int2(s, (k << 16) | cb));
+                }
             }
             L.count = (int32_t)((int64_t)asmv.size() - L.off);
-            N.sched.push_back(L);
+            if (L.count > 0) N.sched.push_back(L);
         }
         int maxw = 0;
         for (int32_t s : large) maxw = std::max(maxw, S.w(s));
@@ -420,12 +433,19 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     const int32_t ns = S.ns;
     int64_t rc;
     DevPlan& P = N.P;
-    int32_t *d_sn_start, *d_sn_m, *d_child_ptr, *d_child_list, *d_relind, *d_apos;
-    int64_t *d_panel_off, *d_cb_off, *d_rel_ptr, *d_aptr, *d_asrc;
+    static_assert(ASM_ROWS == kAsmRows, "assembly row tile");
+    for (int32_t s = 0; s < S.ns; ++s)
+        if (S.sn_m[s] >= (1 << 20)) {  // assembly task encoding: 16-bit column block index
+            N.err = "front with >= 2^20 rows is not supported";
+            return fail(SC_ERR_NOTIMPL);
+        }
+    int32_t *d_sn_start, *d_sn_m, *d_child_ptr, *d_child_list, *d_relind, *d_apos, *d_relbnd;
+    int64_t *d_panel_off, *d_cb_off, *d_rel_ptr, *d_aptr, *d_asrc, *d_rbptr;
     if ((rc = upload(N, S.sn_start, d_sn_start)) || (rc = upload(N, S.sn_m, d_sn_m)) ||
         (rc = upload(N, S.panel_off, d_panel_off)) || (rc = upload(N, S.cb_off, d_cb_off)) ||
         (rc = upload(N, S.child_ptr, d_child_ptr)) || (rc = upload(N, S.child_list, d_child_list)) ||
         (rc = upload(N, S.rel_ptr, d_rel_ptr)) || (rc = upload(N, S.relind, d_relind)) ||
+        (rc = upload(N, S.rb_ptr, d_rbptr)) || (rc = upload(N, S.rel_bnd, d_relbnd)) ||
         (rc = upload(N, S.a_ptr, d_aptr)) || (rc = upload(N, S.a_pos, d_apos)) ||
         (rc = upload(N, S.a_src, d_asrc)))
         return fail(rc);
@@ -437,6 +457,8 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     P.child_list = d_child_list;
     P.rel_ptr = d_rel_ptr;
     P.relind = d_relind;
+    P.rb_ptr = d_rbptr;
+    P.rel_bnd = d_relbnd;
     P.a_ptr = d_aptr;
     P.a_pos = d_apos;
     P.a_src = d_asrc;
@@ -487,7 +509,7 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
         case L_SMALL:
             return launch_front_small(N.P, N.d_small + L.off, L.count, L.maxm, d_Ax, N.stream);
         case L_ASM:
-            return launch_assemble_large(N.P, N.d_asm + L.off, L.count, d_Ax, N.stream);
+            return launch_assemble_large(N.P, N.d_asm + L.off, L.count, d_Ax, N.stream, L.big != 0);
         case L_POTRF:
             return launch_potrf_diag(N.P, N.d_potrf + L.off, L.count, N.stream, N.panel_variant);
         case L_TRSM:

@@ -400,6 +400,19 @@ i64 analyze(i64 n, const i64* Ap, const i32* Ai, const sc_options& opt, Symbolic
                 S.a_pos[q] = pos[a_row[q]];
     }
     S.relind.resize((size_t)S.rel_ptr[ns]);
+    S.rb_ptr.assign((size_t)ns + 1, 0);
+    S.rel_bnd.clear();
+    for (i32 s = 0; s < ns; ++s) {
+        const i32 p = S.sn_parent[s];
+        if (p >= 0) {
+            const i32 nk = (S.sn_m[p] + kAsmRows - 1) / kAsmRows;
+            const i32* rel = S.relind.data() + S.rel_ptr[s];
+            const i32 mbc = (i32)(S.rel_ptr[s + 1] - S.rel_ptr[s]);
+            for (i32 k = 0; k <= nk; ++k)
+                S.rel_bnd.push_back((i32)(std::lower_bound(rel, rel + mbc, k * kAsmRows) - rel));
+        }
+        S.rb_ptr[s + 1] = (i64)S.rel_bnd.size();
+    }
     S.child_ptr.assign((size_t)ns + 1, 0);
     S.child_list.clear();
     for (i32 s = 0; s < ns; ++s) {

@@ -38,6 +38,8 @@ i64 etree_depth(i64 n, const i32* parent);
 // Front size classes
 enum FrontClass : int32_t { FRONT_SMALL = 0, FRONT_LARGE = 1 };
 
+constexpr int kAsmRows = 256;  // row tile of the large-front assembly (kernels.hpp ASM_ROWS)
+
 struct Symbolic {
     sc_options opt {};
     i64 n = 0;
@@ -68,6 +70,10 @@ struct Symbolic {
     std::vector<i32> child_list;
     std::vector<i64> rel_ptr;    // ns+1, CB row -> position in parent front
     std::vector<i32> relind;
+    // per child: first CB row whose parent position is >= k * kAsmRows, for
+    // k = 0 .. ceil(m_parent / kAsmRows) (the assembly's row tiles)
+    std::vector<i64> rb_ptr;     // ns+1
+    std::vector<i32> rel_bnd;
     std::vector<i64> panel_off;  // ns+1 (doubles), L panel m x w, ld = m
     std::vector<i64> cb_off;     // ns+1 (doubles), CB mb x mb, ld = mb
     std::vector<i64> a_ptr;      // n+1: A entries grouped by internal column (lower part)

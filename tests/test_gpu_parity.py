@@ -281,7 +281,8 @@ def test_dense_matrix_large_front(gpu):
 # large-front schedule variants: panel kernels (1 substitution, 2 inverse + MFMA
 # TRSM), inner slab update order (0 right-looking, 1 recursive), lookahead modes
 PANEL_OPTS = [dict(panel_variant=2), dict(inner_order=0), dict(panel_variant=2, inner_order=0, lookahead=0),
-              dict(lookahead=2), dict(panel_variant=2, lookahead=3), dict(lookahead=0)]
+              dict(lookahead=2), dict(panel_variant=2, lookahead=3), dict(lookahead=0), dict(asm_tile_min_m=1),
+              dict(asm_tile_min_m=300)]
 
 
 @pytest.mark.parametrize("opts", PANEL_OPTS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
@@ -294,6 +295,16 @@ def test_panel_schedule_variants(gpu, opts):
     D = M @ M.T + n * np.eye(n)
     iu = np.triu_indices(n)
     check_parity(sc.triplet_to_csc_matrix(iu[0], iu[1], D[iu], n), **opts)
+
+
+@pytest.mark.parametrize("name", ["bcsstk01", "1138_bus"])
+def test_reference_matrices_tiled_assembly(gpu, name, mtx):
+    # every front through the large path and the write-once tiled assembly
+    check_parity(mtx(name), small_front_max=0, asm_tile_min_m=1)
+
+
+def test_random_spd_tiled_assembly(gpu):
+    check_parity(random_spd(400, 0.03, 11), small_front_max=0, asm_tile_min_m=1)
 
 
 def test_empty_matrix_gpu(gpu):
