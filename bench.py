@@ -96,6 +96,8 @@ def main():
     ap.add_argument("--lookahead", type=int, default=None)
     ap.add_argument("--panel-variant", type=int, default=None)
     ap.add_argument("--inner-order", type=int, default=None)
+    ap.add_argument("--opt", action="append", default=[],
+                    help="extra sc_options field, key=value (lists comma-separated), e.g. nrelax=4,16,48")
     ap.add_argument("--tile", type=int, default=None, help="SYRK tile: 0 auto, 64, 128")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
@@ -142,6 +144,10 @@ def main():
         kw["inner_order"] = args.inner_order
     if args.tile is not None:
         kw["syrk_tile"] = args.tile
+    for kv in args.opt:
+        key, val = kv.split("=", 1)
+        vals = [float(x) if "." in x else int(x) for x in val.split(",")]
+        kw[key] = vals if len(vals) > 1 else vals[0]
     symb = sc.Symbolic(A, **kw)
     t_an = time.perf_counter() - t0
     st = symb.stats()

@@ -59,7 +59,8 @@ typedef struct sc_options {
     int32_t panel_nb;        /* inner panel block (potrf/trsm width), 64 */
     int32_t panel_nb_outer;  /* outer panel block (rank-k panel update width), 256 */
     int32_t use_graph;       /* capture the level schedule into a hipGraph and replay it */
-    int32_t relax_wmax;      /* never amalgamate two supernodes that are both wider than this */
+    int32_t relax_wmax;      /* a child and its parent that are both wider than this are not amalgamated when
+                                the parent has other children (chains still merge; 0 = no limit; default 1) */
     int32_t syrk_tile;       /* 0 = auto (128x128/8 waves for wide, deep updates, else 64x64/4 waves); 64; 128 */
     int32_t lookahead;       /* 0: none; 1: trailing panel updates on a 2nd stream; 2: same, at most one of their
                                 workgroups per CU; 3: same, 2nd stream CU-masked to 7/8 */

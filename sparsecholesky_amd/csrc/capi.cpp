@@ -71,7 +71,7 @@ void sc_default_options(sc_options* opt) {
     opt->panel_nb = 64;
     opt->panel_nb_outer = 512;
     opt->use_graph = 0;
-    opt->relax_wmax = 128;
+    opt->relax_wmax = 1;
     opt->syrk_tile = 0;
     opt->lookahead = 1;
     opt->panel_variant = 0;
