@@ -57,7 +57,7 @@ typedef struct sc_options {
     double zrelax[3];        /* zero-fraction thresholds for amalgamation */
     int32_t small_front_max; /* fronts with m <= this run in the fused one-workgroup kernel */
     int32_t panel_nb;        /* inner panel block (potrf/trsm width), 64 */
-    int32_t panel_nb_outer;  /* outer panel block (rank-k panel update width), 256 */
+    int32_t panel_nb_outer;  /* slab width NBO: rank-NBO outer panel updates at slab ends (default 1024) */
     int32_t use_graph;       /* capture the level schedule into a hipGraph and replay it */
     int32_t relax_wmax;      /* a child and its parent that are both wider than this are not amalgamated when
                                 the parent has other children (chains still merge; 0 = no limit; default 1) */

@@ -69,7 +69,7 @@ void sc_default_options(sc_options* opt) {
     opt->zrelax[2] = 0.05;
     opt->small_front_max = 128;
     opt->panel_nb = 64;
-    opt->panel_nb_outer = 512;
+    opt->panel_nb_outer = 1024;
     opt->use_graph = 0;
     opt->relax_wmax = 1;
     opt->syrk_tile = 0;
