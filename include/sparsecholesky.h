@@ -67,7 +67,9 @@ typedef struct sc_options {
     int32_t panel_variant;   /* large-front POTRF/TRSM kernels: 1 pipelined substitution, 2 inverse + MFMA (0 = default) */
     int32_t inner_order;     /* updates inside a slab: 0 right-looking (K = 64), 1 recursive (K = 64..NBO/2) */
     int32_t asm_tile_min_m;  /* fronts with m >= this use the write-once tiled assembly (0 = default 8192) */
-    int32_t reserved[2];
+    int32_t fuse_potrf;      /* 1: the update that completes a panel block also factors its diagonal block
+                                (default 0: measured slower, 625 vs 602 ms at 128^3) */
+    int32_t reserved[1];
 } sc_options;
 
 /* Symbolic statistics (host analysis). */

@@ -68,7 +68,7 @@ class Options(C.Structure):
         ("small_front_max", C.c_int32), ("panel_nb", C.c_int32), ("panel_nb_outer", C.c_int32),
         ("use_graph", C.c_int32), ("relax_wmax", C.c_int32), ("syrk_tile", C.c_int32),
         ("lookahead", C.c_int32), ("panel_variant", C.c_int32), ("inner_order", C.c_int32),
-        ("asm_tile_min_m", C.c_int32), ("reserved", C.c_int32 * 2),
+        ("asm_tile_min_m", C.c_int32), ("fuse_potrf", C.c_int32), ("reserved", C.c_int32 * 1),
     ]
 
 

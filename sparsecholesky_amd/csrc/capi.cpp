@@ -77,6 +77,7 @@ void sc_default_options(sc_options* opt) {
     opt->panel_variant = 0;
     opt->inner_order = 1;
     opt->asm_tile_min_m = 0;
+    opt->fuse_potrf = 0;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,

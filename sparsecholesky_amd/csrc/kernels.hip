@@ -584,15 +584,22 @@ __global__ __launch_bounds__(256) void trsm_panel_mfma_kernel(DevPlan P, const i
 // and the B operand (its first N rows) share one column-major array.  K is
 // staged through double-buffered LDS (register staging, BK = 16).
 // ---------------------------------------------------------------------------
-template <int BT, int WM, int WN, int TAG>
+// FUSE: a task with potrf_col > 0 finishes the 64 x 64 diagonal block at the
+// top-left of its C (the next panel block, complete after this update): tile
+// (0, 0) keeps that quadrant in LDS instead of storing it, and one wave factors it
+// in registers (potrf64_full) and stores L11, so the block needs no POTRF launch.
+template <int BT, int WM, int WN, int TAG, bool FUSE = false>
 __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
-                                                                  const int2* __restrict__ tiles) {
+                                                                  const int2* __restrict__ tiles,
+                                                                  int32_t* __restrict__ info) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BK = 16;
     constexpr int LDT = BT + 16;  // +128 B row pad: the two k-rows read by a half-wave hit disjoint banks
     constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
-    __shared__ double As[2][BK * LDT];
-    __shared__ double Bs[2][BK * LDT];
+    __shared__ double smem[2 * 2 * BK * LDT];  // A and B stages; after the K loop: the fused POTRF block
+    static_assert(!FUSE || 2 * 2 * BK * LDT >= PNB * PNB + 2 * PNB, "LDS for the fused POTRF");
+    double(*As)[BK * LDT] = reinterpret_cast<double(*)[BK * LDT]>(smem);
+    double(*Bs)[BK * LDT] = reinterpret_cast<double(*)[BK * LDT]>(smem + 2 * BK * LDT);
 
     // host-ordered tile list: blocks sharing an XCD walk a contiguous, L2-blocked run of tiles
     const int2 tl = tiles[blockIdx.x];
@@ -673,8 +680,28 @@ __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask*
             for (int r = 0; r < 4; ++r) {
                 const int gi = row0 + wr * (BT / WM) + a * 16 + MFMA_F64_ROW(lane, r);
                 const int gj = col0 + wc * (BT / WN) + b * 16 + (lane & 15);
-                if (gi < T.M && gj < T.N && gi >= gj) C[gi + gj * ldc] -= acc[a][b][r];
+                if (gi < T.M && gj < T.N && gi >= gj) {
+                    if (FUSE && T.potrf_col > 0 && gi < PNB && gj < PNB)
+                        smem[gj * PNB + gi] = C[gi + gj * ldc] - acc[a][b][r];  // rows/cols < 64 => tile (0, 0)
+                    else
+                        C[gi + gj * ldc] -= acc[a][b][r];
+                }
             }
+    if constexpr (FUSE) {
+        if (T.potrf_col > 0 && row0 == 0 && col0 == 0) {
+            __syncthreads();
+            if (wid == 0) {
+                double r[PNB];
+#pragma unroll
+                for (int c = 0; c < PNB; ++c) r[c] = (c <= lane) ? smem[c * PNB + lane] : 0.0;
+                const int bad = potrf64_full(r, smem + PNB * PNB, lane);
+                if (bad >= 0 && lane == 0) report_fail(info, T.potrf_col - 1 + bad);
+#pragma unroll
+                for (int c = 0; c < PNB; ++c)
+                    if (c <= lane) C[lane + (int64_t)c * ldc] = r[c];
+            }
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -728,27 +755,32 @@ hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hip
 // one_per_cu: reserve unused dynamic LDS so that at most one workgroup of this
 // launch sits on a CU (the overlapped lookahead GEMMs leave room for the panel
 // chain's kernels instead of filling every CU twice).
-template <int TAG>
-static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int bt, bool one_per_cu, hipStream_t st) {
+template <int TAG, bool FUSE>
+static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int bt, bool one_per_cu, int32_t* info,
+                          hipStream_t st) {
     constexpr size_t kHalfLds = 80 * 1024;
     if (bt == 128) {
         constexpr size_t stat = 2 * 2 * 16 * (128 + 16) * sizeof(double);
         const size_t dyn = one_per_cu ? kHalfLds + 1024 - stat : 0;
-        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG>), dim3(n), dim3(512), dyn, st, tasks, tiles);
+        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, FUSE>), dim3(n), dim3(512), dyn, st, tasks, tiles,
+                           info);
     } else {
         constexpr size_t stat = 2 * 2 * 16 * (64 + 16) * sizeof(double);
         const size_t dyn = one_per_cu ? kHalfLds + 1024 - stat : 0;
-        hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG>), dim3(n), dim3(256), dyn, st, tasks, tiles);
+        hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG, FUSE>), dim3(n), dim3(256), dyn, st, tasks, tiles,
+                           info);
     }
 }
 
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
-                       bool one_per_cu) {
+                       bool one_per_cu, int32_t* fuse_info) {
     if (total_tiles <= 0) return hipSuccess;
     if (tag)
-        launch_syrk_t<1>(tasks, tiles, total_tiles, bt, one_per_cu, st);
+        launch_syrk_t<1, false>(tasks, tiles, total_tiles, bt, one_per_cu, nullptr, st);
+    else if (fuse_info)
+        launch_syrk_t<0, true>(tasks, tiles, total_tiles, bt, one_per_cu, fuse_info, st);
     else
-        launch_syrk_t<0>(tasks, tiles, total_tiles, bt, one_per_cu, st);
+        launch_syrk_t<0, false>(tasks, tiles, total_tiles, bt, one_per_cu, nullptr, st);
     return hipGetLastError();
 }
 

@@ -51,7 +51,8 @@ struct GemmTask {
     int64_t ldc;
     int64_t lda;
     int32_t M, N, K;
-    int32_t pad;
+    int32_t potrf_col;  // > 0: tile (0, 0) also factors the 64 x 64 block at C (fused POTRF);
+                        // value = internal column of the block + 1 (for non-PD reporting)
 };
 
 hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count, int maxm, const double* Ax,
@@ -73,8 +74,9 @@ hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hip
 // in a separate launch (the full-block kernels skip them)
 hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st,
                              int variant = PANEL_VARIANT, bool partial = false);
+// fuse_info != nullptr: panel-update launch whose tasks may carry a fused POTRF
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
-                       bool one_per_cu = false);
+                       bool one_per_cu = false, int32_t* fuse_info = nullptr);
 hipError_t launch_stamp(uint64_t* slot, hipStream_t st);
 hipError_t launch_fill_random(double* p, int64_t n, hipStream_t st);
 hipError_t launch_mfma_peak(double* out, int blocks, int iters, int nacc, hipStream_t st);

@@ -132,6 +132,7 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
     for (int32_t s = 0; s < S.ns; ++s) by_level[S.level[s]].push_back(s);
     double* panel_pool = N.P.panel_pool;
     double* cb_pool = N.P.cb_pool;
+    std::vector<int32_t> fused_at((size_t)S.ns, -1);
     auto push_gemm_launch = [&](int kind, int level, const std::vector<GemmTask>& tasks, int big,
                                 double flops, int strm = 0) {
         if (tasks.empty()) return;
@@ -139,6 +140,7 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         L.kind = kind;
         L.level = level;
         L.strm = strm;
+        for (auto& t : tasks) L.fuse |= t.potrf_col > 0 ? 1 : 0;
         L.off = (int64_t)gemm.size();
         // 128x128 tiles on 8 waves when every task is at least 256 wide (random data,
         // 16384 x 4096: 61 vs 52 TF/s for 64x64); 64x64 on 4 waves for narrow updates
@@ -227,10 +229,18 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         // (stream 1), which overlaps the next slab's factorization.  A later outer
         // update of overlapping columns waits for the stream-1 work first.
         int b_pending = -1;
+        // fused POTRF: the update that completes block [c_lo, c_lo + 64) of front s
+        // (its last update before its POTRF) factors that diagonal block in its tile
+        // (0, 0); the block then gets no POTRF task.  fused_at[s] = that block's start.
         auto add_update = [&](std::vector<GemmTask>& v, double& fl, double* pan, int m, int c_lo, int c_hi, int ka,
-                              int kb) {
+                              int kb, int s = -1) {
             if (c_hi <= c_lo || kb <= ka) return;
             GemmTask t {};
+            // (not with panel variant 2: its TRSM needs the inverse only potrf_inv_kernel forms)
+            if (s >= 0 && S.opt.fuse_potrf && N.panel_variant != 2 && S.w(s) - c_lo >= PNB && c_hi - c_lo >= PNB) {
+                t.potrf_col = S.sn_start[s] + c_lo + 1;
+                fused_at[s] = c_lo;
+            }
             t.C = pan + (int64_t)c_lo * m + c_lo;
             t.A = pan + (int64_t)ka * m + c_lo;
             t.ldc = m;
@@ -258,7 +268,7 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
                 if (w <= k0) continue;
                 const int nb = std::min(PNB, w - k0);
                 const int k1 = k0 + nb;
-                potrf.push_back(make_int2(s, k0));
+                if (fused_at[s] != k0) potrf.push_back(make_int2(s, k0));
                 for (int r0 = k1; r0 < m; r0 += trsm_task_rows(N.panel_variant))
                     (nb < PNB ? trsm_part : trsm).push_back(make_int4(s, k0, r0, 0));
                 double* pan = panel_pool + S.panel_off[s];
@@ -271,12 +281,14 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
                     // right-looking, 768 instead of 1792 C columns rewritten per slab.
                     const int b = (k0 - slab0) / PNB;
                     const int span = PNB << __builtin_ctz((unsigned)(b + 1));
-                    add_update(upd, uflops, pan, m, k1, std::min(slab1, k1 + span), k1 - span, k1);
+                    add_update(upd, uflops, pan, m, k1, std::min(slab1, k1 + span), k1 - span, k1, s);
                 } else if (k1 < slab1) {
-                    add_update(upd, uflops, pan, m, k1, slab1, k0, k1);
+                    add_update(upd, uflops, pan, m, k1, slab1, k0, k1, s);
                 } else if (k1 == slab1 && slab1 < w) {
+                    // outer_a is the last update of block slab1: a pending stream-1 outer
+                    // update of those columns is waited for before outer_a runs
                     const int nxt = S.opt.lookahead ? std::min(w, slab1 + NBO) : w;
-                    add_update(outer_a, afl, pan, m, slab1, nxt, slab0, slab1);
+                    add_update(outer_a, afl, pan, m, slab1, nxt, slab0, slab1, s);
                     add_update(outer_b, bfl, pan, m, nxt, w, slab0, slab1);
                 }
             }
@@ -517,7 +529,7 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
         case L_PANEL:
         case L_CB:
             return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st,
-                               L.strm == 1 && N.S->opt.lookahead == 2);
+                               L.strm == 1 && N.S->opt.lookahead == 2, L.fuse ? N.P.info : nullptr);
         case L_COMM:
             return comm_launch(N, L);
     }

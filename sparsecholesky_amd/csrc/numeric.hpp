@@ -44,6 +44,7 @@ struct Launch {
     int32_t big;      // CB launch covering fronts with w >= 256
     int32_t bt;       // SYRK tile edge (64 or 128)
     int32_t strm;     // 0 = main stream, 1 = lookahead stream
+    int32_t fuse;     // panel launch whose tasks may factor the next diagonal block (potrf_col)
     double flops;     // algorithmic SYRK flops (CB launches: mb*(mb+1)*w)
 };
 
