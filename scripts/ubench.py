@@ -37,7 +37,7 @@ def main():
     for blocks in (1024, 2048):
         out[f"peak blocks={blocks} nacc=8"] = run(0, blocks, 20000, 3, 8)
     for M, K in ((4096, 256), (4096, 1024), (8192, 2048), (16384, 4096), (16384, 8192)):
-        for tile in (64, 128):
+        for tile in (64, 128, 1128):
             out[f"syrk M={M} K={K} tile={tile}"] = run(1, M, K, 3, tile)
     for k, v in out.items():
         print(f"{k:45s} {v}")

@@ -622,16 +622,20 @@ __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask*
 
     // staging: BK x BT doubles per operand over NT threads
     constexpr int PER = BT * BK / NT;
+    // Operands through a per-stage buffer resource (columns k0 .. k0 + BK of A):
+    // K past the end and rows past M / N fall outside it and load 0 -- no branches,
+    // and buffer loads count only vmcnt, so the LDS waits of the MFMA loop do not
+    // also wait for the next stage's prefetch (flat loads count both).
     double ra[PER], rb[PER];
     auto gload = [&](int k0) {
+        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(A + (int64_t)k0 * lda, (uint32_t)(min(BK, T.K - k0) * lda * 8));
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
             const int e = tid + q * NT;
             const int r = e % BT, kk = e / BT;
-            const int gk = k0 + kk;
             const int gr = row0 + r, gc = col0 + r;
-            ra[q] = (gr < T.M && gk < T.K) ? A[gr + gk * lda] : 0.0;
-            rb[q] = (gc < T.N && gk < T.K) ? A[gc + gk * lda] : 0.0;
+            ra[q] = buf_ld(rs, gr < T.M ? (int)((gr + kk * lda) * 8) : BUF_DEAD, 0);
+            rb[q] = buf_ld(rs, gc < T.N ? (int)((gc + kk * lda) * 8) : BUF_DEAD, 0);
         }
     };
     auto sstore = [&](int buf) {
@@ -669,9 +673,13 @@ __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask*
         __syncthreads();
     }
 
-    // epilogue: f64 16x16x4 C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
+    // epilogue: f64 16x16x4 C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg.
+    // C read-modify-write through a buffer resource over the tile's columns (dead
+    // elements -- above the diagonal, past M / N -- masked by range, no branches).
     double* __restrict__ C = T.C;
     const int64_t ldc = T.ldc;
+    const __amdgpu_buffer_rsrc_t rc =
+        buf_rsrc(C + (int64_t)col0 * ldc, (uint32_t)(min(BT, T.N - col0) * ldc * 8));
 #pragma unroll
     for (int a = 0; a < RTM; ++a)
 #pragma unroll
@@ -680,11 +688,12 @@ __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask*
             for (int r = 0; r < 4; ++r) {
                 const int gi = row0 + wr * (BT / WM) + a * 16 + MFMA_F64_ROW(lane, r);
                 const int gj = col0 + wc * (BT / WN) + b * 16 + (lane & 15);
-                if (gi < T.M && gj < T.N && gi >= gj) {
-                    if (FUSE && T.potrf_col > 0 && gi < PNB && gj < PNB)
-                        smem[gj * PNB + gi] = C[gi + gj * ldc] - acc[a][b][r];  // rows/cols < 64 => tile (0, 0)
-                    else
-                        C[gi + gj * ldc] -= acc[a][b][r];
+                const bool live = gi < T.M && gi >= gj;
+                const int off = live ? (int)((gi + (int64_t)(gj - col0) * ldc) * 8) : BUF_DEAD;
+                if (FUSE && T.potrf_col > 0 && gi < PNB && gj < PNB) {
+                    if (live) smem[gj * PNB + gi] = buf_ld(rc, off, 0) - acc[a][b][r];  // tile (0, 0) only
+                } else {
+                    buf_st(buf_ld(rc, off, 0) - acc[a][b][r], rc, off, 0);
                 }
             }
     if constexpr (FUSE) {
@@ -759,7 +768,9 @@ template <int TAG, bool FUSE>
 static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int bt, bool one_per_cu, int32_t* info,
                           hipStream_t st) {
     constexpr size_t kHalfLds = 80 * 1024;
-    if (bt == 128) {
+    if (bt == SYRK_BT_LARGE_W4) {  // 128 x 128 on 4 waves of 64 x 64 (experimental)
+        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 2, TAG, FUSE>), dim3(n), dim3(256), 0, st, tasks, tiles, info);
+    } else if (bt == 128) {
         constexpr size_t stat = 2 * 2 * 16 * (128 + 16) * sizeof(double);
         const size_t dyn = one_per_cu ? kHalfLds + 1024 - stat : 0;
         hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, FUSE>), dim3(n), dim3(512), dyn, st, tasks, tiles,

@@ -19,6 +19,7 @@ constexpr int ASM_TILE_MIN_M = 8192;  // fronts at least this tall use the write
 // Output tile edges of the MFMA SYRK kernel (per launch).
 constexpr int SYRK_BT_SMALL = 64;
 constexpr int SYRK_BT_LARGE = 128;
+constexpr int SYRK_BT_LARGE_W4 = 1128;  // launch code: 128 x 128 tiles on 4 waves (64 x 64 each)
 
 // C/D register map of v_mfma_f64_16x16x4_f64 on gfx950 (cdna_hip_programming.md
 // section 3): col = lane & 15, row = (lane >> 4) + 4 * reg.
