@@ -655,19 +655,28 @@ __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask*
     for (int kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
         if (kt + 1 < nk) gload((kt + 1) * BK);
-#pragma unroll
-        for (int kk = 0; kk < BK; kk += 4) {
-            double av[RTM], bv[RTN];
+        // LDS operand fragments double-buffered across the 4-deep k sub-steps: the
+        // reads of sub-step kk + 1 are in flight while sub-step kk's MFMAs issue
+        double av[2][RTM], bv[2][RTN];
+        auto lread = [&](int kk, int slot) {
             const int krow = kk + (lane >> 4);
 #pragma unroll
-            for (int a = 0; a < RTM; ++a) av[a] = As[cur][krow * LDT + wr * (BT / WM) + a * 16 + (lane & 15)];
+            for (int a = 0; a < RTM; ++a)
+                av[slot][a] = As[cur][krow * LDT + wr * (BT / WM) + a * 16 + (lane & 15)];
 #pragma unroll
-            for (int b = 0; b < RTN; ++b) bv[b] = Bs[cur][krow * LDT + wc * (BT / WN) + b * 16 + (lane & 15)];
+            for (int b = 0; b < RTN; ++b)
+                bv[slot][b] = Bs[cur][krow * LDT + wc * (BT / WN) + b * 16 + (lane & 15)];
+        };
+        lread(0, 0);
+#pragma unroll
+        for (int kk = 0; kk < BK; kk += 4) {
+            const int slot = (kk / 4) & 1;
+            if (kk + 4 < BK) lread(kk + 4, slot ^ 1);
 #pragma unroll
             for (int a = 0; a < RTM; ++a)
 #pragma unroll
                 for (int b = 0; b < RTN; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[slot][a], bv[slot][b], acc[a][b], 0, 0, 0);
         }
         if (kt + 1 < nk) sstore(cur ^ 1);
         __syncthreads();
