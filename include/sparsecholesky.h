@@ -69,7 +69,11 @@ typedef struct sc_options {
     int32_t asm_tile_min_m;  /* fronts with m >= this use the write-once tiled assembly (0 = default 8192) */
     int32_t fuse_potrf;      /* 1: the update that completes a panel block also factors its diagonal block
                                 (default 0: measured slower, 625 vs 602 ms at 128^3) */
-    int32_t reserved[1];
+    int32_t dist_split;      /* multi-GPU: a shared front with a contribution block keeps its panel on one rank and
+                                has its contribution block computed by the other ranks of its group, slab-streamed
+                                (1, default); 0: every front on one rank */
+    int32_t dist_cbb;        /* multi-GPU: column-block width of contribution-block ownership and transfers (1024) */
+    int32_t reserved[2];
 } sc_options;
 
 /* Symbolic statistics (host analysis). */
@@ -219,9 +223,27 @@ int64_t sc_dist_owner_map(const sc_symbolic* sym, int32_t nranks, int32_t* owner
 int64_t sc_numeric_create_dist(const sc_symbolic* sym, int32_t device, int32_t rank,
                                int32_t nranks, const void* id128, sc_numeric** out);
 /* Per-rank message schedule for tests: returns number of messages; if the
- * arrays are non-NULL fills (level, peer, bytes, is_send) per message. */
-int64_t sc_dist_schedule(const sc_symbolic* sym, int32_t nranks, int32_t rank, int32_t* level,
+ * arrays are non-NULL fills (comm step, peer, bytes, is_send) per message, in
+ * posting order (comm steps ascending; all ranks follow one global step order). */
+int64_t sc_dist_schedule(const sc_symbolic* sym, int32_t nranks, int32_t rank, int32_t* step,
                          int32_t* peer, int64_t* bytes, int32_t* is_send, int64_t cap);
+/* Plan summary: per supernode the rank-group size (1 = inside one rank's subtree)
+ * and, for split fronts, the number of ranks computing its contribution block
+ * (0 = not split); *n_steps = comm steps.  Returns the total message count. */
+int64_t sc_dist_plan_info(const sc_symbolic* sym, int32_t nranks, int32_t* gsize, int32_t* split_cb_ranks,
+                          int64_t* n_steps);
+/* Host-staged transport (tests / debugging without RCCL: several processes may
+ * share one GPU).  The library calls fn(ctx, op, peer, buf, bytes) with op 0 =
+ * post a send of host buffer buf, 1 = post a receive into buf, 2 = complete every
+ * posted operation (buffers stay valid until then); nonzero return = failure. */
+typedef int32_t (*sc_transport_fn)(void* ctx, int32_t op, int32_t peer, void* buf, int64_t bytes);
+int64_t sc_numeric_create_dist_host(const sc_symbolic* sym, int32_t device, int32_t rank,
+                                    int32_t nranks, sc_transport_fn fn, void* ctx, sc_numeric** out);
+/* Timing projection: rank `rank`'s part of an nranks-GPU factorization alone on
+ * this device; comm steps pack and unpack but move nothing (received blocks hold
+ * stale values, so the numbers are not a factor). */
+int64_t sc_numeric_create_dist_dry(const sc_symbolic* sym, int32_t device, int32_t rank, int32_t nranks,
+                                   sc_numeric** out);
 
 /* ---------------- debug / unit-test hooks ---------------- */
 /* C[i,j] -= sum_k A[i,k] A[j,k] for i>=j over an M x N trapezoid (device

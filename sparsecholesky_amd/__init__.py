@@ -68,7 +68,8 @@ class Options(C.Structure):
         ("small_front_max", C.c_int32), ("panel_nb", C.c_int32), ("panel_nb_outer", C.c_int32),
         ("use_graph", C.c_int32), ("relax_wmax", C.c_int32), ("syrk_tile", C.c_int32),
         ("lookahead", C.c_int32), ("panel_variant", C.c_int32), ("inner_order", C.c_int32),
-        ("asm_tile_min_m", C.c_int32), ("fuse_potrf", C.c_int32), ("reserved", C.c_int32 * 1),
+        ("asm_tile_min_m", C.c_int32), ("fuse_potrf", C.c_int32), ("dist_split", C.c_int32), ("dist_cbb", C.c_int32),
+        ("reserved", C.c_int32 * 2),
     ]
 
 
@@ -131,6 +132,9 @@ _SIGS = [
     ("sc_dist_owner_map", _I64, [_P, _I32, _P, _P]),
     ("sc_numeric_create_dist", _I64, [_P, _I32, _I32, _I32, _P, C.POINTER(_P)]),
     ("sc_dist_schedule", _I64, [_P, _I32, _I32, _P, _P, _P, _P, _I64]),
+    ("sc_dist_plan_info", _I64, [_P, _I32, _P, _P, C.POINTER(_I64)]),
+    ("sc_numeric_create_dist_host", _I64, [_P, _I32, _I32, _I32, C.c_void_p, _P, C.POINTER(_P)]),
+    ("sc_numeric_create_dist_dry", _I64, [_P, _I32, _I32, _I32, C.POINTER(_P)]),
     ("sc_debug_syrk", _I64, [_P, _I32, _P, _I32, _I32, _I32, _I32]),
     ("sc_debug_bench", _I64, [_I32, _I32, _I32, _I32, _I32, C.POINTER(_D)]),
     ("sc_device_count", _I64, []),
@@ -467,7 +471,18 @@ class Symbolic:
         _check(lib().sc_dist_owner_map(self.h, nranks, _ptr(own), _ptr(work)), "owner_map")
         return own[:ns], work
 
+    def dist_plan_info(self, nranks: int) -> dict:
+        """Multi-GPU plan summary: rank-group size per supernode, CB ranks of split fronts,
+        comm steps and total messages."""
+        ns = self.stats()["n_supernodes"]
+        g = np.zeros(max(ns, 1), dtype=np.int32)
+        cbr = np.zeros(max(ns, 1), dtype=np.int32)
+        nst = C.c_int64()
+        nmsg = _check(lib().sc_dist_plan_info(self.h, nranks, _ptr(g), _ptr(cbr), C.byref(nst)), "dist_plan_info")
+        return dict(gsize=g[:ns], split_cb_ranks=cbr[:ns], n_steps=nst.value, n_msgs=nmsg)
+
     def dist_schedule(self, nranks: int, rank: int):
+        """This rank's messages in posting order: (comm step, peer, bytes, is_send)."""
         cnt = _check(lib().sc_dist_schedule(self.h, nranks, rank, None, None, None, None, 0), "dist_schedule")
         lev = np.zeros(max(cnt, 1), dtype=np.int32)
         peer = np.zeros(max(cnt, 1), dtype=np.int32)
@@ -488,14 +503,23 @@ class Numeric:
     """Device factorization handle (pools + level schedule on one HIP device)."""
 
     def __init__(self, symb: Symbolic, device: int = -1, rank: int = 0, nranks: int = 1,
-                 uid: Optional[bytes] = None, virtual: bool = False):
+                 uid: Optional[bytes] = None, virtual: bool = False, transport=None):
         """nranks > 1 with ``uid`` (from :func:`dist_unique_id` on rank 0): this process is
         ``rank`` of a subtree-partitioned multi-GPU factorization over RCCL.  ``virtual=True``
-        emulates all ``nranks`` ranks' partitioned schedule in this one process."""
+        emulates all ``nranks`` ranks' partitioned schedule in this one process.
+        ``transport`` (e.g. :class:`GlooHostTransport`): the same multi-process protocol with
+        every transfer staged through host memory instead of RCCL (tests; ranks may share a GPU)."""
         self.symb = symb
         self.rank, self.nranks = rank, nranks
+        self.transport = transport
         h = C.c_void_p()
-        if nranks > 1 or virtual:
+        if transport == "dry":
+            _check(lib().sc_numeric_create_dist_dry(symb.h, device, rank, nranks, C.byref(h)),
+                   "numeric_create_dist_dry")
+        elif transport is not None:
+            _check(lib().sc_numeric_create_dist_host(symb.h, device, rank, nranks, C.cast(transport.fn, C.c_void_p),
+                                                     None, C.byref(h)), "numeric_create_dist_host")
+        elif nranks > 1 or virtual:
             idbuf = None
             if not virtual:
                 assert uid is not None and len(uid) == 128
@@ -568,6 +592,44 @@ class Numeric:
         if h and _lib is not None:
             _lib.sc_free_numeric(h)
             self.h = None
+
+
+_XPORT_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int64)
+
+
+class GlooHostTransport:
+    """Host-staged transport for :class:`Numeric` over ``torch.distributed`` (gloo):
+    every comm step's buffers go device -> host -> gloo isend/irecv -> host -> device.
+    For tests and debugging of the multi-process protocol without RCCL (several
+    processes may then share one GPU); not a performance path."""
+
+    def __init__(self, group=None):
+        import torch.distributed as tdist
+
+        self._dist = tdist
+        self._group = group
+        self._pending = []
+        self.error = None
+        self.fn = _XPORT_FN(self._callback)  # kept alive with the transport
+
+    def _callback(self, ctx, op, peer, buf, nbytes):
+        try:
+            if op == 2:
+                for w in self._pending:
+                    w.wait()
+                self._pending = []
+                return 0
+            import torch
+
+            t = torch.frombuffer((C.c_char * nbytes).from_address(buf), dtype=torch.uint8)
+            if op == 0:
+                self._pending.append(self._dist.isend(t, int(peer), group=self._group))
+            else:
+                self._pending.append(self._dist.irecv(t, int(peer), group=self._group))
+            return 0
+        except Exception as e:  # reported through the library's status
+            self.error = repr(e)
+            return 1
 
 
 def dist_unique_id() -> bytes:

@@ -1,6 +1,7 @@
 // extern "C" boundary (include/sparsecholesky.h).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <new>
 #include <string>
@@ -22,7 +23,8 @@ i64 dist_owner_map(const Symbolic& S, int nranks, i32* owner, double* work);
 i64 dist_schedule(const Symbolic& S, int nranks, int rank, i32* level, i32* peer, i64* bytes, i32* is_send,
                   i64 cap);
 i64 numeric_create_dist(const Symbolic& S, int device, int rank, int nranks, const void* id128,
-                        Numeric*& out, std::string& err);
+                        int32_t (*xport)(void*, int32_t, int32_t, void*, int64_t), void* xport_ctx, Numeric*& out,
+                        std::string& err);
 i64 dist_unique_id(void* id128);
 }  // namespace sc
 
@@ -78,6 +80,8 @@ void sc_default_options(sc_options* opt) {
     opt->inner_order = 1;
     opt->asm_tile_min_m = 0;
     opt->fuse_potrf = 0;
+    opt->dist_split = 1;
+    opt->dist_cbb = 1024;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,
@@ -339,7 +343,7 @@ int64_t sc_numeric_create_dist(const sc_symbolic* sym, int32_t device, int32_t r
     sc_numeric* h = new (std::nothrow) sc_numeric();
     if (!h) return SC_ERR_NOMEM;
     std::string err;
-    int64_t rc = sc::numeric_create_dist(sym->S, device, rank, nranks, id128, h->N, err);
+    int64_t rc = sc::numeric_create_dist(sym->S, device, rank, nranks, id128, nullptr, nullptr, h->N, err);
     if (rc != SC_OK) {
         g_last_error = err;
         delete h;
@@ -348,6 +352,64 @@ int64_t sc_numeric_create_dist(const sc_symbolic* sym, int32_t device, int32_t r
     h->sym = sym;
     *out = h;
     return SC_OK;
+}
+
+int64_t sc_numeric_create_dist_host(const sc_symbolic* sym, int32_t device, int32_t rank, int32_t nranks,
+                                    sc_transport_fn fn, void* ctx, sc_numeric** out) {
+    if (!sym || !out || !fn || nranks <= 0 || rank < 0 || rank >= nranks) return SC_ERR_ARG;
+    *out = nullptr;
+    sc_numeric* h = new (std::nothrow) sc_numeric();
+    if (!h) return SC_ERR_NOMEM;
+    std::string err;
+    int64_t rc = sc::numeric_create_dist(sym->S, device, rank, nranks, nullptr, fn, ctx, h->N, err);
+    if (rc != SC_OK) {
+        g_last_error = err;
+        delete h;
+        return rc;
+    }
+    h->sym = sym;
+    *out = h;
+    return SC_OK;
+}
+
+int64_t sc_numeric_create_dist_dry(const sc_symbolic* sym, int32_t device, int32_t rank, int32_t nranks,
+                                   sc_numeric** out) {
+    if (!sym || !out || nranks <= 0 || rank < 0 || rank >= nranks) return SC_ERR_ARG;
+    *out = nullptr;
+    sc_numeric* h = new (std::nothrow) sc_numeric();
+    if (!h) return SC_ERR_NOMEM;
+    std::string err;
+    int64_t rc = sc::numeric_create_dist(sym->S, device, rank, nranks, nullptr, DIST_DRY, nullptr, h->N, err);
+    if (rc != SC_OK) {
+        g_last_error = err;
+        delete h;
+        return rc;
+    }
+    h->sym = sym;
+    *out = h;
+    return SC_OK;
+}
+
+int64_t sc_dist_plan_info(const sc_symbolic* sym, int32_t nranks, int32_t* gsize, int32_t* split_cb_ranks,
+                          int64_t* n_steps) {
+    if (!sym || nranks <= 0) return SC_ERR_ARG;
+    sc::DistPlan D;
+    int64_t rc = sc::dist_plan(sym->S, nranks, D);
+    if (rc != SC_OK) return rc;
+    for (int32_t s = 0; s < sym->S.ns; ++s) {
+        if (gsize) gsize[s] = D.gsize[s];
+        if (split_cb_ranks) {
+            int32_t v = 0;
+            if (D.split[s] >= 0) {
+                std::vector<int32_t> r = D.cb_rank[D.split[s]];
+                std::sort(r.begin(), r.end());
+                v = (int32_t)(std::unique(r.begin(), r.end()) - r.begin());
+            }
+            split_cb_ranks[s] = v;
+        }
+    }
+    if (n_steps) *n_steps = (int64_t)D.steps.size();
+    return (int64_t)D.msgs.size();
 }
 
 // ---- debug hooks ----

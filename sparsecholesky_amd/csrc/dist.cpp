@@ -1,7 +1,26 @@
-// Multi-GPU plan: proportional subtree-to-GPU mapping of the assembly tree
-// (SURVEY.md 8e).  Every supernode gets one owner rank; a contribution block
-// crosses GPUs only where a child and its parent have different owners (the
-// subtree-merge fronts).
+// Multi-GPU plan: proportional subtree-to-GPU mapping of the
+// assembly tree, split top fronts, and the comm steps between ranks.
+//
+// Mapping.  The ranks form a continuous interval [0, P) of processor mass split
+// among the children of every front in proportion to subtree work; rounded to
+// whole ranks, a child whose interval holds at most one rank gets its whole
+// subtree there (no communication inside).  Fronts whose interval holds more
+// ranks are the subtree-merge ("shared") fronts; their rank groups nest and two
+// fronts of the same level have disjoint groups.
+//
+// Split fronts.  A shared front with a contribution block is split over its
+// group: its least-loaded rank (the owner) assembles it and factors its panel;
+// the other ranks own column blocks of its contribution block.  The owner sends
+// the assembled CB blocks once (STEP_INIT) and then rows [w, m) of every panel
+// slab as soon as the slab is final (STEP_SLAB); each CB rank applies
+// CB -= L21_k L21_k^T to its blocks per slab, so the CB update (the bulk of the
+// front's flops) runs on the group in parallel and overlaps the owner's panel
+// chain.  Shared fronts without a CB (the root) run on their owner.
+//
+// Transfers.  After each level, every CB column block whose producer is not the
+// executing rank of the parent goes there (STEP_DELIVER), packed (only rows
+// >= the block's first column: the lower part), so several links feed one parent
+// at once when its child was split.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -15,144 +34,228 @@
 
 namespace sc {
 
-static void subtree_work(const Symbolic& S, std::vector<double>& work) {
-    work.assign((size_t)S.ns, 0.0);
-    for (i32 s = 0; s < S.ns; ++s) {  // children precede parents (postorder)
-        const double m = S.sn_m[s], w = S.w(s);
-        double f = 0.0;
-        // sum_{t<w} (m-t)^2, closed form
-        f = w * m * m - m * w * (w - 1) + (w - 1) * w * (2 * w - 1) / 6.0;
-        work[s] += f;
-        if (S.sn_parent[s] >= 0) work[S.sn_parent[s]] += work[s];
-    }
+// sum_{t<w} (m-t)^2, closed form: the front's dense partial-Cholesky work
+static double front_work(const Symbolic& S, i32 s) {
+    const double m = S.sn_m[s], w = S.w(s);
+    return w * m * m - m * w * (w - 1) + (w - 1) * w * (2 * w - 1) / 6.0;
 }
 
-// Recursive proportional mapping: the ranks [r0, r1) are a continuous interval of
-// processor mass split among the children in proportion to subtree work; a child
-// whose share rounds to one rank owns its whole subtree there.
-i64 dist_owner_map(const Symbolic& S, int nranks, i32* owner, double* work_per_rank) {
-    std::vector<double> work;
-    subtree_work(S, work);
-    std::vector<i32> own((size_t)S.ns, 0);
+// CB-update share of front_work: mb (mb + 1) w
+static double cb_work(const Symbolic& S, i32 s) {
+    const double mb = S.mb(s), w = S.w(s);
+    return mb * (mb + 1.0) * w;
+}
+
+int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
+    if (nranks <= 0) return SC_ERR_ARG;
+    D = DistPlan();
+    D.nranks = nranks;
+    D.cbb = std::max(64, S.opt.dist_cbb > 0 ? S.opt.dist_cbb : 1024);
+    D.nbo = std::max(PNB, (S.opt.panel_nb_outer / PNB) * PNB);
+    const i32 ns = S.ns;
+    D.owner.assign((size_t)ns, 0);
+    D.gsize.assign((size_t)ns, 1);
+    D.split.assign((size_t)ns, -1);
+    D.work.assign((size_t)nranks, 0.0);
+    std::vector<double> sub((size_t)ns, 0.0);
+    for (i32 s = 0; s < ns; ++s) {  // children precede parents (postorder)
+        sub[s] += front_work(S, s);
+        if (S.sn_parent[s] >= 0) sub[S.sn_parent[s]] += sub[s];
+    }
     struct Item {
         i32 s;
-        double a, b;  // processor interval
+        double a, b;   // processor interval
+        i32 plo, phi;  // parent's rank group (single owners are clamped into it)
     };
     std::vector<Item> stack;
-    // roots share the whole machine
-    std::vector<i32> roots;
-    double W = 0.0;
-    for (i32 s = 0; s < S.ns; ++s)
-        if (S.sn_parent[s] < 0) {
-            roots.push_back(s);
-            W += work[s];
-        }
     {
-        double cum = 0.0;
-        for (i32 r : roots) {
-            const double a = nranks * (W > 0 ? cum / W : 0.0);
-            cum += work[r];
-            const double b = nranks * (W > 0 ? cum / W : 1.0);
-            stack.push_back({r, a, b});
-        }
+        double W = 0.0, cum = 0.0;
+        for (i32 s = 0; s < ns; ++s)
+            if (S.sn_parent[s] < 0) W += sub[s];
+        for (i32 s = 0; s < ns; ++s)
+            if (S.sn_parent[s] < 0) {
+                const double a = nranks * (W > 0 ? cum / W : 0.0);
+                cum += sub[s];
+                const double b = nranks * (W > 0 ? cum / W : 1.0);
+                stack.push_back({s, a, b, 0, nranks});
+            }
     }
-    auto whole_subtree = [&](i32 s, i32 rank) {
-        // subtree of s = contiguous supernode range ending at s (postorder)
-        std::vector<i32> st {s};
-        while (!st.empty()) {
-            i32 v = st.back();
-            st.pop_back();
-            own[v] = rank;
-            for (i32 q = S.child_ptr[v]; q < S.child_ptr[v + 1]; ++q) st.push_back(S.child_list[q]);
-        }
-    };
-    const double eps = 1e-9;
-    // multi-rank (merge) fronts, placed after the subtrees: least-loaded rank of
-    // their interval, children before parents
-    std::vector<std::pair<i32, std::pair<i32, i32>>> shared;
+    std::vector<i32> glo((size_t)ns, 0);
+    std::vector<char> shared((size_t)ns, 0);
+    auto rnd = [&](double x) { return std::min(nranks, std::max(0, (int)std::floor(x + 0.5))); };
     while (!stack.empty()) {
-        Item it = stack.back();
+        const Item it = stack.back();
         stack.pop_back();
-        i32 lo = (i32)std::floor(it.a + eps);
-        i32 hi = std::max(lo + 1, (i32)std::ceil(it.b - eps));
-        lo = std::min(lo, nranks - 1);
-        hi = std::min(hi, nranks);
+        const int lo = rnd(it.a), hi = rnd(it.b);
         if (hi - lo <= 1) {
-            whole_subtree(it.s, lo);
+            int r = std::min(lo, nranks - 1);
+            r = std::max(it.plo, std::min(it.phi - 1, r));
+            std::vector<i32> st {it.s};  // whole subtree on r
+            while (!st.empty()) {
+                const i32 v = st.back();
+                st.pop_back();
+                D.owner[v] = r;
+                for (i32 q = S.child_ptr[v]; q < S.child_ptr[v + 1]; ++q) st.push_back(S.child_list[q]);
+            }
             continue;
         }
-        own[it.s] = lo;
-        shared.push_back({it.s, {lo, hi}});
-        double Wc = 0.0;
-        for (i32 q = S.child_ptr[it.s]; q < S.child_ptr[it.s + 1]; ++q) Wc += work[S.child_list[q]];
-        double cum = 0.0;
+        shared[it.s] = 1;
+        glo[it.s] = lo;
+        D.gsize[it.s] = hi - lo;
+        double Wc = 0.0, cum = 0.0;
+        for (i32 q = S.child_ptr[it.s]; q < S.child_ptr[it.s + 1]; ++q) Wc += sub[S.child_list[q]];
         for (i32 q = S.child_ptr[it.s]; q < S.child_ptr[it.s + 1]; ++q) {
-            i32 c = S.child_list[q];
+            const i32 c = S.child_list[q];
             const double a = it.a + (it.b - it.a) * (Wc > 0 ? cum / Wc : 0.0);
-            cum += work[c];
+            cum += sub[c];
             const double b = it.a + (it.b - it.a) * (Wc > 0 ? cum / Wc : 1.0);
-            stack.push_back({c, a, b});
+            stack.push_back({c, a, b, lo, hi});
         }
     }
-    {
-        std::vector<double> load((size_t)nranks, 0.0);
-        std::vector<char> is_shared((size_t)S.ns, 0);
-        for (auto& sh : shared) is_shared[sh.first] = 1;
-        for (i32 s = 0; s < S.ns; ++s) {
-            if (is_shared[s]) continue;
-            const double m = S.sn_m[s], w = S.w(s);
-            load[own[s]] += w * m * m - m * w * (w - 1) + (w - 1) * w * (2 * w - 1) / 6.0;
+    for (i32 s = 0; s < ns; ++s)
+        if (!shared[s]) D.work[D.owner[s]] += front_work(S, s);
+    // shared fronts, children first: owner = least-loaded rank of the group; split
+    // fronts deal their CB column blocks to the other ranks, largest block first
+    for (i32 s = 0; s < ns; ++s) {
+        if (!shared[s]) continue;
+        const int lo = glo[s], hi = lo + D.gsize[s];
+        int own = lo;
+        for (int r = lo + 1; r < hi; ++r)
+            if (D.work[r] < D.work[own]) own = r;
+        D.owner[s] = own;
+        const int mb = S.mb(s), w = S.w(s);
+        const bool split = S.opt.dist_split != 0 && S.fclass[s] == FRONT_LARGE && mb > 0;
+        if (!split) {
+            D.work[own] += front_work(S, s);
+            continue;
         }
-        std::sort(shared.begin(), shared.end());  // postorder: children first
-        for (auto& sh : shared) {
-            const i32 s = sh.first, lo = sh.second.first, hi = sh.second.second;
-            i32 best = lo;
-            for (i32 r = lo + 1; r < hi; ++r)
-                if (load[r] < load[best]) best = r;
-            own[s] = best;
-            const double m = S.sn_m[s], w = S.w(s);
-            load[best] += w * m * m - m * w * (w - 1) + (w - 1) * w * (2 * w - 1) / 6.0;
+        D.work[own] += front_work(S, s) - cb_work(S, s);
+        const int nblk = (mb + D.cbb - 1) / D.cbb;
+        std::vector<int> ord((size_t)nblk);
+        for (int b = 0; b < nblk; ++b) ord[b] = b;  // block b has mb - b*cbb rows: descending work
+        std::vector<i32> cbr((size_t)nblk, -1);
+        for (int b : ord) {
+            const double rows = mb - (double)b * D.cbb, cols = std::min<double>(D.cbb, rows);
+            int best = -1;
+            for (int r = lo; r < hi; ++r)
+                if (r != own && (best < 0 || D.work[r] < D.work[best])) best = r;
+            cbr[b] = best;
+            D.work[best] += w * (2.0 * rows * cols - cols * cols + cols);
         }
+        D.split[s] = (i32)D.split_s.size();
+        D.split_s.push_back(s);
+        D.cb_rank.push_back(std::move(cbr));
     }
-    if (owner) std::memcpy(owner, own.data(), sizeof(i32) * (size_t)S.ns);
-    if (work_per_rank) {
-        std::fill(work_per_rank, work_per_rank + nranks, 0.0);
-        for (i32 s = 0; s < S.ns; ++s) {
-            const double m = S.sn_m[s], w = S.w(s);
-            work_per_rank[own[s]] += w * m * m - m * w * (w - 1) + (w - 1) * w * (2 * w - 1) / 6.0;
+
+    // comm steps in the global order: per level, the split fronts' INIT and SLAB
+    // steps (ascending supernode), then the level's DELIVER step
+    std::vector<std::vector<i32>> by_level((size_t)S.nlevels);
+    for (i32 s = 0; s < ns; ++s) by_level[S.level[s]].push_back(s);
+    auto cb_block = [&](DistMsg& g, i32 c, int jb) {
+        const int mbc = S.mb(c);
+        g.pool = 1;
+        g.off = S.cb_off[c] + (i64)jb * D.cbb * mbc + (i64)jb * D.cbb;
+        g.ld = mbc;
+        g.rows = mbc - jb * D.cbb;
+        g.cols = std::min(D.cbb, g.rows);
+        g.s = c;
+    };
+    auto open_step = [&](int kind, int lev, int s, int k) {
+        D.steps.push_back({kind, lev, s, k});
+        return (int32_t)D.steps.size() - 1;
+    };
+    auto close_step = [&](int32_t id) {  // drop a step without messages
+        if (D.msgs.empty() || D.msgs.back().step != id) D.steps.pop_back();
+    };
+    for (i32 lev = 0; lev < S.nlevels; ++lev) {
+        for (i32 s : by_level[lev]) {
+            if (D.split[s] < 0) continue;
+            const std::vector<i32>& cbr = D.cb_rank[D.split[s]];
+            const int own = D.owner[s], m = S.sn_m[s], w = S.w(s), mb = m - w;
+            int32_t id = open_step(STEP_INIT, lev, s, 0);
+            for (int jb = 0; jb < (int)cbr.size(); ++jb) {
+                DistMsg g {};
+                g.step = id;
+                g.src = own;
+                g.dst = cbr[jb];
+                cb_block(g, s, jb);
+                D.msgs.push_back(g);
+            }
+            close_step(id);
+            std::vector<i32> dsts(cbr);
+            std::sort(dsts.begin(), dsts.end());
+            dsts.erase(std::unique(dsts.begin(), dsts.end()), dsts.end());
+            for (int k0 = 0, k = 0; k0 < w; k0 += D.nbo, ++k) {
+                const int k1 = std::min(w, k0 + D.nbo);
+                id = open_step(STEP_SLAB, lev, s, k);
+                for (i32 r : dsts) {
+                    DistMsg g {};
+                    g.step = id;
+                    g.src = own;
+                    g.dst = r;
+                    g.pool = 0;
+                    g.off = S.panel_off[s] + (i64)k0 * m + w;
+                    g.ld = m;
+                    g.rows = mb;
+                    g.cols = k1 - k0;
+                    g.s = s;
+                    D.msgs.push_back(g);
+                }
+                close_step(id);
+            }
         }
+        int32_t id = open_step(STEP_DELIVER, lev, -1, 0);
+        for (i32 c : by_level[lev]) {
+            const i32 p = S.sn_parent[c];
+            const int mbc = S.mb(c);
+            if (p < 0 || mbc <= 0) continue;
+            const int dst = D.owner[p];
+            for (int jb = 0; jb * D.cbb < mbc; ++jb) {
+                const int src = D.split[c] >= 0 ? D.cb_rank[D.split[c]][jb] : D.owner[c];
+                if (src == dst) continue;
+                DistMsg g {};
+                g.step = id;
+                g.src = src;
+                g.dst = dst;
+                cb_block(g, c, jb);
+                D.msgs.push_back(g);
+            }
+        }
+        close_step(id);
     }
     return SC_OK;
 }
 
-// Messages of `rank` in global order (level of the sending child, then child id):
-// a child's CB goes from owner(child) to owner(parent) after the child's level.
-i64 dist_schedule(const Symbolic& S, int nranks, int rank, i32* level, i32* peer, i64* bytes, i32* is_send,
+i64 dist_owner_map(const Symbolic& S, int nranks, i32* owner, double* work_per_rank) {
+    DistPlan D;
+    i64 rc = dist_plan(S, nranks, D);
+    if (rc != SC_OK) return rc;
+    if (owner) std::memcpy(owner, D.owner.data(), sizeof(i32) * (size_t)S.ns);
+    if (work_per_rank) std::memcpy(work_per_rank, D.work.data(), sizeof(double) * (size_t)nranks);
+    return SC_OK;
+}
+
+// Messages of `rank` in posting order: (comm step, peer, bytes, is_send).
+i64 dist_schedule(const Symbolic& S, int nranks, int rank, i32* step, i32* peer, i64* bytes, i32* is_send,
                   i64 cap) {
-    std::vector<i32> own((size_t)S.ns);
-    dist_owner_map(S, nranks, own.data(), nullptr);
-    std::vector<i32> order((size_t)S.ns);
-    for (i32 s = 0; s < S.ns; ++s) order[s] = s;
-    std::stable_sort(order.begin(), order.end(), [&](i32 a, i32 b) { return S.level[a] < S.level[b]; });
+    DistPlan D;
+    i64 rc = dist_plan(S, nranks, D);
+    if (rc != SC_OK) return rc;
     i64 cnt = 0;
-    for (i32 c : order) {
-        const i32 p = S.sn_parent[c];
-        if (p < 0 || own[c] == own[p]) continue;
-        const bool snd = own[c] == rank, rcv = own[p] == rank;
-        if (!snd && !rcv) continue;
-        if (level && cnt < cap) {
-            level[cnt] = S.level[c];
-            peer[cnt] = snd ? own[p] : own[c];
-            const i64 mb = S.mb(c);
-            bytes[cnt] = mb * mb * (i64)sizeof(double);
-            is_send[cnt] = snd ? 1 : 0;
+    for (const DistMsg& g : D.msgs) {
+        if (g.src != rank && g.dst != rank) continue;
+        if (step && cnt < cap) {
+            step[cnt] = g.step;
+            peer[cnt] = g.src == rank ? g.dst : g.src;
+            bytes[cnt] = (i64)g.rows * g.cols * (i64)sizeof(double);
+            is_send[cnt] = g.src == rank ? 1 : 0;
         }
         ++cnt;
     }
     return cnt;
 }
 
-// ---------------- RCCL transport ----------------
+// ---------------- transport ----------------
 static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
 
 i64 dist_unique_id(void* id128) {
@@ -163,28 +266,63 @@ i64 dist_unique_id(void* id128) {
     return SC_OK;
 }
 
-// All CB transfers of one level as one RCCL group on the library stream: both
-// sides post them in the same global order (level, then child id), so the
-// point-to-point matching per peer pair is consistent.
+// One comm step of this rank on the comm stream: pack the sends into their
+// staging slots, one RCCL group with every send / receive of the step (both
+// sides post a step's messages in the same plan order, so the per-peer matching
+// is consistent), unpack the receives.  With a host transport (tests) the group
+// goes through host memory instead, synchronously.
 hipError_t comm_launch(Numeric& N, const Launch& L) {
-    if (!N.comm) return hipErrorInvalidValue;
-    ncclComm_t comm = (ncclComm_t)N.comm;
-    if (ncclGroupStart() != ncclSuccess) return hipErrorUnknown;
-    for (int64_t q = L.off; q < L.off + L.count; ++q) {
-        const Msg& g = N.msgs[q];
-        ncclResult_t r = g.is_send ? ncclSend(g.buf, (size_t)g.count, ncclDouble, g.peer, comm, N.stream)
-                                   : ncclRecv(g.buf, (size_t)g.count, ncclDouble, g.peer, comm, N.stream);
+    hipStream_t st = N.stream3;
+    hipError_t e = hipSuccess;
+    if (L.pcount > 0 && (e = launch_copy2d(N.d_copy, N.d_ctiles + L.poff, L.pcount, false, st)) != hipSuccess)
+        return e;
+    if (N.dry_comm) {
+        // timing projection of one rank alone: packing and unpacking, no transfer
+    } else if (N.xport) {
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+        std::vector<std::vector<char>> host((size_t)L.count);
+        for (int64_t q = 0; q < L.count; ++q) {
+            const Msg& g = N.msgs[L.off + q];
+            const size_t nb = (size_t)g.count * sizeof(double);
+            host[q].resize(std::max<size_t>(nb, 1));
+            if (g.is_send && (e = hipMemcpy(host[q].data(), g.buf, nb, hipMemcpyDeviceToHost)) != hipSuccess) return e;
+            if (N.xport(N.xport_ctx, g.is_send ? 0 : 1, g.peer, host[q].data(), (int64_t)nb) != 0) {
+                N.err = "host transport: post failed";
+                return hipErrorUnknown;
+            }
+        }
+        if (N.xport(N.xport_ctx, 2, -1, nullptr, 0) != 0) {
+            N.err = "host transport: completion failed";
+            return hipErrorUnknown;
+        }
+        for (int64_t q = 0; q < L.count; ++q) {
+            const Msg& g = N.msgs[L.off + q];
+            if (!g.is_send &&
+                (e = hipMemcpy(g.buf, host[q].data(), (size_t)g.count * sizeof(double), hipMemcpyHostToDevice)) !=
+                    hipSuccess)
+                return e;
+        }
+    } else {
+        if (!N.comm) return hipErrorInvalidValue;
+        ncclComm_t comm = (ncclComm_t)N.comm;
+        if (ncclGroupStart() != ncclSuccess) return hipErrorUnknown;
+        for (int64_t q = L.off; q < L.off + L.count; ++q) {
+            const Msg& g = N.msgs[q];
+            ncclResult_t r = g.is_send ? ncclSend(g.buf, (size_t)g.count, ncclDouble, g.peer, comm, st)
+                                       : ncclRecv(g.buf, (size_t)g.count, ncclDouble, g.peer, comm, st);
+            if (r != ncclSuccess) {
+                N.err = std::string("rccl p2p: ") + ncclGetErrorString(r);
+                (void)ncclGroupEnd();
+                return hipErrorUnknown;
+            }
+        }
+        ncclResult_t r = ncclGroupEnd();
         if (r != ncclSuccess) {
-            N.err = std::string("rccl p2p: ") + ncclGetErrorString(r);
-            (void)ncclGroupEnd();
+            N.err = std::string("rccl group: ") + ncclGetErrorString(r);
             return hipErrorUnknown;
         }
     }
-    ncclResult_t r = ncclGroupEnd();
-    if (r != ncclSuccess) {
-        N.err = std::string("rccl group: ") + ncclGetErrorString(r);
-        return hipErrorUnknown;
-    }
+    if (L.ucount > 0) return launch_copy2d(N.d_copy, N.d_ctiles + L.uoff, L.ucount, true, st);
     return hipSuccess;
 }
 
@@ -195,10 +333,12 @@ void comm_destroy(Numeric& N) {
     }
 }
 
-// Real multi-GPU handle: this process is `rank` of `nranks` (one GPU each).
-// Every rank allocates the full pools (288 GB HBM per GPU holds them) but only
-// computes the supernodes the proportional mapping gives it.
-i64 numeric_create_dist(const Symbolic& S, int device, int rank, int nranks, const void* id128, Numeric*& out,
+// Multi-GPU handle: this process is `rank` of `nranks` (one GPU each).  Every rank
+// allocates the full pools (288 GB HBM per GPU holds them) but computes only its
+// part of the plan.  id128 != NULL: RCCL transport; xport != NULL: host-staged
+// transport (tests); neither: in-process emulation of all ranks (shared pools).
+i64 numeric_create_dist(const Symbolic& S, int device, int rank, int nranks, const void* id128,
+                        int32_t (*xport)(void*, int32_t, int32_t, void*, int64_t), void* xport_ctx, Numeric*& out,
                         std::string& err) {
     out = nullptr;
     Numeric* Np = new (std::nothrow) Numeric();
@@ -206,11 +346,19 @@ i64 numeric_create_dist(const Symbolic& S, int device, int rank, int nranks, con
     Numeric& N = *Np;
     N.rank = rank;
     N.nranks = nranks;
-    N.owner.resize((size_t)S.ns);
-    dist_owner_map(S, nranks, N.owner.data(), nullptr);
-    if (!id128) {
-        // in-process emulation of all ranks (shared pools, no transfers)
-        N.virt_ranks = nranks;
+    i64 rc = dist_plan(S, nranks, N.D);
+    if (rc != SC_OK) {
+        delete Np;
+        return rc;
+    }
+    N.owner = N.D.owner;
+    if (xport == DIST_DRY) {
+        N.dry_comm = true;
+    } else if (xport) {
+        N.xport = xport;
+        N.xport_ctx = xport_ctx;
+    } else if (!id128) {
+        N.virt_ranks = nranks;  // shared pools, no transfers
     } else if (nranks > 1) {
         int dev = device;
         if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
@@ -230,7 +378,7 @@ i64 numeric_create_dist(const Symbolic& S, int device, int rank, int nranks, con
         }
         N.comm = comm;
     }
-    i64 rc = numeric_init(N, S, device);
+    rc = numeric_init(N, S, device);
     if (rc != SC_OK) {
         err = N.err;
         numeric_free(Np);

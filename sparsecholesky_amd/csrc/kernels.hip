@@ -829,6 +829,32 @@ hipError_t launch_stamp(uint64_t* slot, hipStream_t st) {
     return hipGetLastError();
 }
 
+// Multi-GPU staging: strided <-> packed copy of contribution-block / panel column
+// blocks around the RCCL transfers.  One workgroup per COPY_COLS columns of one
+// block, one wave per column, 64 consecutive doubles per wave access (HBM-bound).
+__global__ __launch_bounds__(256) void copy2d_kernel(const Copy2D* __restrict__ descs, const int2* __restrict__ tiles,
+                                                     int unpack) {
+    const int2 t = tiles[blockIdx.x];
+    const Copy2D d = descs[t.x];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int j1 = min(d.cols, t.y + COPY_COLS);
+    for (int j = t.y + wid; j < j1; j += 4) {
+        double* a = d.a + (int64_t)j * d.lda;
+        double* b = d.b + (int64_t)j * d.rows;
+        if (unpack) {
+            for (int r = lane; r < d.rows; r += 64) a[r] = b[r];
+        } else {
+            for (int r = lane; r < d.rows; r += 64) b[r] = a[r];
+        }
+    }
+}
+
+hipError_t launch_copy2d(const Copy2D* descs, const int2* tiles, int count, bool unpack, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(copy2d_kernel, dim3(count), dim3(256), 0, st, descs, tiles, unpack ? 1 : 0);
+    return hipGetLastError();
+}
+
 // Peak probe: independent fp64 MFMA chains, operands in registers.
 template <int NACC>
 __global__ __launch_bounds__(256) void mfma_peak_kernel(double* out, int iters) {

@@ -56,6 +56,18 @@ struct GemmTask {
                         // value = internal column of the block + 1 (for non-PD reporting)
 };
 
+// Strided <-> packed copy of a rows x cols block (pack: a -> b; unpack: b -> a).
+struct Copy2D {
+    double* a;  // strided, leading dimension lda
+    double* b;  // packed, leading dimension rows
+    int64_t lda;
+    int32_t rows, cols;
+};
+
+constexpr int COPY_COLS = 16;  // columns per copy workgroup
+// tiles: (descriptor, first column) per workgroup
+hipError_t launch_copy2d(const Copy2D* descs, const int2* tiles, int count, bool unpack, hipStream_t st);
+
 hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count, int maxm, const double* Ax,
                               hipStream_t st);
 // tiled: tasks are (front, (row tile << 16) | 16-column block) for the write-once

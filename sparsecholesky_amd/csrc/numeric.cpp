@@ -123,9 +123,19 @@ void xcd_order_tasks(int2* tiles, int64_t n, const GemmTask* tasks, int ntasks) 
     for (int64_t b = 0; b < n; ++b) tiles[b] = per[b % 8][b / 8];
 }
 
+// Staging slots of this rank's messages (patched to device addresses once the
+// staging pool is allocated): slot < 0 = the message moves in place.
+struct CommBuild {
+    std::vector<Copy2D> copies;
+    std::vector<int64_t> copy_slot;
+    std::vector<int2> ctiles;
+    std::vector<int64_t> msg_slot;
+    int64_t stage_total = 0;
+};
+
 static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vector<int2>& asmv,
                               std::vector<int2>& potrf, std::vector<int4>& trsm,
-                              std::vector<GemmTask>& gemm, std::vector<int2>& tiles) {
+                              std::vector<GemmTask>& gemm, std::vector<int2>& tiles, CommBuild& cbld) {
     const Symbolic& S = *N.S;
     const int NBO = std::max(PNB, (S.opt.panel_nb_outer / PNB) * PNB);
     std::vector<std::vector<int32_t>> by_level((size_t)S.nlevels);
@@ -133,6 +143,25 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
     double* panel_pool = N.P.panel_pool;
     double* cb_pool = N.P.cb_pool;
     std::vector<int32_t> fused_at((size_t)S.ns, -1);
+    // multi-GPU plan lookups
+    const DistPlan& D = N.D;
+    const bool real_comm = !N.owner.empty() && N.virt_ranks <= 1;
+    auto is_split = [&](int32_t s) { return !D.split.empty() && D.split[s] >= 0; };
+    std::vector<int32_t> init_step, slab_step0, deliver_step((size_t)S.nlevels, -1);
+    std::vector<int64_t> step_beg;
+    if (!N.owner.empty()) {
+        init_step.assign((size_t)S.ns, -1);
+        slab_step0.assign((size_t)S.ns, -1);
+        for (int32_t id = 0; id < (int32_t)D.steps.size(); ++id) {
+            const DistStep& t = D.steps[id];
+            if (t.kind == STEP_INIT) init_step[t.s] = id;
+            if (t.kind == STEP_SLAB && t.k == 0) slab_step0[t.s] = id;
+            if (t.kind == STEP_DELIVER) deliver_step[t.level] = id;
+        }
+        step_beg.assign(D.steps.size() + 1, 0);
+        for (const DistMsg& g : D.msgs) step_beg[g.step + 1]++;
+        for (size_t i = 0; i < D.steps.size(); ++i) step_beg[i + 1] += step_beg[i];
+    }
     auto push_gemm_launch = [&](int kind, int level, const std::vector<GemmTask>& tasks, int big,
                                 double flops, int strm = 0) {
         if (tasks.empty()) return;
@@ -179,6 +208,94 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         L.count = ev;
         N.sched.push_back(L);
     };
+    // this rank's part of comm step `id` on the comm stream (strm 2): it waits for
+    // the main stream's work so far (the data it sends), and the main stream waits
+    // for it when it receives.  Messages keep the plan order, so every peer pair
+    // posts its matching sends and receives in the same order.
+    auto emit_step = [&](int32_t id) {
+        if (!real_comm || id < 0) return;
+        Launch L {};
+        L.kind = L_COMM;
+        L.level = D.steps[id].level;
+        L.strm = 2;
+        L.step = id;
+        L.off = (int64_t)N.msgs.size();
+        int nrecv = 0;
+        std::vector<int32_t> pack_d, unpack_d;  // copy descriptors of the sends / receives
+        for (int64_t q = step_beg[id]; q < step_beg[id + 1]; ++q) {
+            const DistMsg& g = D.msgs[q];
+            const bool snd = g.src == N.rank, rcv = g.dst == N.rank;
+            if (!snd && !rcv) continue;
+            double* base = (g.pool == 0 ? panel_pool : cb_pool) + g.off;
+            const int64_t cnt = (int64_t)g.rows * g.cols;
+            Msg m {};
+            m.count = cnt;
+            m.peer = snd ? g.dst : g.src;
+            m.is_send = snd ? 1 : 0;
+            m.child = g.s;
+            nrecv += rcv ? 1 : 0;
+            if (g.ld == g.rows || g.cols == 1) {  // contiguous: moves in place
+                m.buf = base;
+                N.msgs.push_back(m);
+                cbld.msg_slot.push_back(-1);
+                continue;
+            }
+            N.msgs.push_back(m);
+            cbld.msg_slot.push_back(cbld.stage_total);
+            Copy2D c {};
+            c.a = base;
+            c.lda = g.ld;
+            c.rows = g.rows;
+            c.cols = g.cols;
+            (snd ? pack_d : unpack_d).push_back((int32_t)cbld.copies.size());
+            cbld.copies.push_back(c);
+            cbld.copy_slot.push_back(cbld.stage_total);
+            cbld.stage_total += cnt;
+        }
+        L.count = (int32_t)((int64_t)N.msgs.size() - L.off);
+        if (L.count == 0) return;
+        auto add_tiles = [&](const std::vector<int32_t>& ds) {
+            for (int32_t d : ds)
+                for (int j = 0; j < cbld.copies[d].cols; j += COPY_COLS) cbld.ctiles.push_back(make_int2(d, j));
+        };
+        L.poff = (int64_t)cbld.ctiles.size();
+        add_tiles(pack_d);
+        L.pcount = (int32_t)((int64_t)cbld.ctiles.size() - L.poff);
+        L.uoff = (int64_t)cbld.ctiles.size();
+        add_tiles(unpack_d);
+        L.ucount = (int32_t)((int64_t)cbld.ctiles.size() - L.uoff);
+        push_wait(2, push_record(0));
+        N.sched.push_back(L);
+        if (nrecv > 0) push_wait(0, push_record(2));
+    };
+    // CB rank `who` of split front s: per final panel slab, CB -= L21_k L21_k^T on
+    // the column blocks it owns (K = slab width)
+    auto emit_cb_rank = [&](int32_t lev, int32_t s, int who) {
+        const std::vector<int32_t>& cbr = D.cb_rank[D.split[s]];
+        const int w = S.w(s), m = S.sn_m[s], mb = m - w;
+        emit_step(init_step[s]);
+        for (int k0 = 0, k = 0; k0 < w; k0 += D.nbo, ++k) {
+            const int k1 = std::min(w, k0 + D.nbo);
+            emit_step(slab_step0[s] < 0 ? -1 : slab_step0[s] + k);
+            std::vector<GemmTask> cbt;
+            double fl = 0.0;
+            for (int jb = 0; jb < (int)cbr.size(); ++jb) {
+                if (cbr[jb] != who) continue;
+                const int r0 = jb * D.cbb;
+                GemmTask t {};
+                t.C = cb_pool + S.cb_off[s] + (int64_t)r0 * mb + r0;
+                t.A = panel_pool + S.panel_off[s] + (int64_t)k0 * m + w + r0;
+                t.ldc = mb;
+                t.lda = m;
+                t.M = mb - r0;
+                t.N = std::min(D.cbb, mb - r0);
+                t.K = k1 - k0;
+                cbt.push_back(t);
+                fl += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
+            }
+            push_gemm_launch(L_CB, lev, cbt, w >= 256 ? 1 : 0, fl);
+        }
+    };
     // one level's fronts (already filtered to the ranks this process runs)
     auto emit_level = [&](int32_t lev, const std::vector<int32_t>& nodes) {
         // small fronts by LDS bucket
@@ -222,6 +339,8 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             L.count = (int32_t)((int64_t)asmv.size() - L.off);
             if (L.count > 0) N.sched.push_back(L);
         }
+        for (int32_t s : large)
+            if (is_split(s)) emit_step(init_step[s]);
         int maxw = 0;
         for (int32_t s : large) maxw = std::max(maxw, S.w(s));
         // Lookahead: at a slab end the outer rank-NBO update is split into the next
@@ -304,6 +423,13 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
                 trsm.insert(trsm.end(), trsm_part.begin(), trsm_part.end());
                 N.sched.push_back(Lq);
             }
+            // split fronts: a slab is final after the TRSM of its last block
+            for (int32_t s : large) {
+                const int w = S.w(s);
+                if (!is_split(s) || w <= k0 || slab_step0[s] < 0) continue;
+                const int k1 = std::min(w, k0 + PNB);
+                if (k1 == w || k1 % D.nbo == 0) emit_step(slab_step0[s] + k0 / D.nbo);
+            }
             push_gemm_launch(L_PANEL, lev, upd, 0, uflops);
             int e_trsm = -1;
             if (!outer_b.empty()) e_trsm = push_record(0);
@@ -327,7 +453,7 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             double fl = 0.0;
             for (int32_t s : large) {
                 const int w = S.w(s), m = S.sn_m[s], mb = m - w;
-                if (mb <= 0 || (w >= 256) != (big == 1)) continue;
+                if (mb <= 0 || (w >= 256) != (big == 1) || is_split(s)) continue;
                 GemmTask t {};
                 t.C = cb_pool + S.cb_off[s];
                 t.A = panel_pool + S.panel_off[s] + w;
@@ -355,33 +481,21 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
                 if (N.owner[s] == who) mine.push_back(s);
             if (!mine.empty()) emit_level(lev, mine);
         }
-        if (N.virt_ranks > 1) continue;  // shared pools: nothing moves
-        // contribution blocks that leave / enter this rank after this level
-        Launch L {};
-        L.kind = L_COMM;
-        L.level = lev;
-        L.off = (int64_t)N.msgs.size();
-        for (int32_t c : by_level[lev]) {
-            const int32_t p = S.sn_parent[c];
-            if (p < 0 || N.owner[c] == N.owner[p]) continue;
-            const int64_t mb = S.mb(c);
-            Msg g {};
-            g.buf = cb_pool + S.cb_off[c];
-            g.count = mb * mb;
-            g.child = c;
-            if (N.owner[c] == N.rank) {
-                g.peer = N.owner[p];
-                g.is_send = 1;
-                N.msgs.push_back(g);
-            } else if (N.owner[p] == N.rank) {
-                g.peer = N.owner[c];
-                g.is_send = 0;
-                N.msgs.push_back(g);
+        // contribution-block ranks of this level's split fronts (in the emulation
+        // after the owners' panels: shared pools, nothing moves)
+        for (int32_t s : by_level[lev]) {
+            if (!is_split(s)) continue;
+            const std::vector<int32_t>& cbr = D.cb_rank[D.split[s]];
+            for (int r = 0; r < nr; ++r) {
+                const int who = N.virt_ranks > 1 ? r : N.rank;
+                if (who != D.owner[s] && std::find(cbr.begin(), cbr.end(), who) != cbr.end())
+                    emit_cb_rank(lev, s, who);
             }
         }
-        L.count = (int32_t)((int64_t)N.msgs.size() - L.off);
-        if (L.count > 0) N.sched.push_back(L);
+        // contribution blocks that leave / enter this rank after this level
+        emit_step(deliver_step[lev]);
     }
+    if (real_comm) push_wait(0, push_record(2));  // join the comm stream (its last sends)
     return SC_OK;
 }
 
@@ -436,6 +550,10 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     } else if (ok) {
         ok = hipStreamCreateWithPriority(&N.stream2, hipStreamNonBlocking, prio_lo) == hipSuccess;
     }
+    // multi-GPU comm stream (only then: an extra stream changes the hardware-queue
+    // mapping of the other two, measured 569 -> 649 ms single-GPU at 128^3)
+    if (ok && !N.owner.empty() && N.virt_ranks <= 1)
+        ok = hipStreamCreateWithPriority(&N.stream3, hipStreamNonBlocking, prio_hi) == hipSuccess;
     if (!ok) {
         N.err = "hipStreamCreate failed";
         return fail(SC_ERR_HIP);
@@ -489,7 +607,16 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     std::vector<int4> trsm;
     std::vector<GemmTask> gemm;
     std::vector<int2> tiles;
-    if ((rc = build_schedule(N, small, asmv, potrf, trsm, gemm, tiles))) return fail(rc);
+    CommBuild cbld;
+    if ((rc = build_schedule(N, small, asmv, potrf, trsm, gemm, tiles, cbld))) return fail(rc);
+    if (cbld.stage_total > 0) {  // multi-GPU: packed staging slots of this rank's messages
+        if ((rc = dalloc(N, (size_t)cbld.stage_total * sizeof(double), p))) return fail(rc);
+        N.staging = (double*)p;
+        for (size_t q = 0; q < N.msgs.size(); ++q)
+            if (cbld.msg_slot[q] >= 0) N.msgs[q].buf = N.staging + cbld.msg_slot[q];
+        for (size_t q = 0; q < cbld.copies.size(); ++q) cbld.copies[q].b = N.staging + cbld.copy_slot[q];
+    }
+    if ((rc = upload(N, cbld.copies, N.d_copy)) || (rc = upload(N, cbld.ctiles, N.d_ctiles))) return fail(rc);
     N.stamp_of.assign(N.sched.size(), -1);
     int nstamp = 0;
     for (size_t i = 0; i < N.sched.size(); ++i)
@@ -511,8 +638,12 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
 
 hipError_t comm_launch(Numeric& N, const Launch& L);  // dist.cpp
 
+static hipStream_t stream_of(const Numeric& N, int strm) {
+    return strm == 2 ? N.stream3 : strm == 1 ? N.stream2 : N.stream;
+}
+
 static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
-    hipStream_t st = L.strm ? N.stream2 : N.stream;
+    hipStream_t st = stream_of(N, L.strm);
     switch (L.kind) {
         case L_RECORD:
             return hipEventRecord(N.sync_ev[L.count], st);
@@ -542,7 +673,7 @@ static int64_t enqueue_all(Numeric& N, const double* d_Ax, int prof) {
         const Launch& L = N.sched[i];
         const bool timed = prof == 1 && L.kind < L_RECORD;
         const bool stamped = prof == 2 && N.stamp_of[i] >= 0;
-        hipStream_t st = L.strm ? N.stream2 : N.stream;
+        hipStream_t st = stream_of(N, L.strm);
         if (timed) HIP_TRY(hipEventRecord(N.ev[2 * i], st));
         if (stamped) HIP_TRY(launch_stamp(N.d_stamps + 2 * N.stamp_of[i], st));
         HIP_TRY(launch_one(N, L, d_Ax));
@@ -624,6 +755,8 @@ int64_t numeric_status(Numeric& N) {
     if (N.status_valid) return N.status;
     HIP_TRY(hipSetDevice(N.device));
     HIP_TRY(hipStreamSynchronize(N.stream));
+    HIP_TRY(hipStreamSynchronize(N.stream2));
+    if (N.stream3) HIP_TRY(hipStreamSynchronize(N.stream3));
     int32_t info = 0;
     HIP_TRY(hipMemcpy(&info, N.P.info, sizeof(info), hipMemcpyDeviceToHost));
     if (info == 0x7f7f7f7f || info <= 0)
@@ -772,6 +905,7 @@ void numeric_free(Numeric* Np) {
     if (N.d_Ax_owned) (void)hipFree(N.d_Ax_owned);
     if (N.stream) (void)hipStreamDestroy(N.stream);
     if (N.stream2) (void)hipStreamDestroy(N.stream2);
+    if (N.stream3) (void)hipStreamDestroy(N.stream3);
     delete Np;
 }
 

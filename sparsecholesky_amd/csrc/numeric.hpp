@@ -24,13 +24,54 @@ enum LaunchKind : int32_t {
     L_KINDS = 9
 };
 
-// One point-to-point contribution-block transfer (multi-GPU).
+// ---------------- multi-GPU plan (dist.cpp) ----------------
+// Comm steps, in one global order every rank follows (each rank posts exactly its
+// part of every step it takes part in, as one RCCL group, on its comm stream):
+//   STEP_INIT(s)    split front s: the owner sends the assembled CB column blocks to
+//                   the ranks that compute them
+//   STEP_SLAB(s,k)  split front s: the owner sends rows [w, m) of panel slab k (final)
+//                   to every CB rank
+//   STEP_DELIVER(l) after level l: every contribution block (column block) whose
+//                   producer is not the executing rank of the parent goes there
+enum StepKind : int32_t { STEP_INIT = 0, STEP_SLAB = 1, STEP_DELIVER = 2 };
+struct DistStep {
+    int32_t kind, level, s, k;
+};
+// One 2D block transfer: rows x cols doubles at pool + off, leading dimension ld,
+// moved packed (rows-contiguous) through a staging slot.
+struct DistMsg {
+    int32_t step;
+    int32_t src, dst;
+    int32_t pool;  // 0 = panel pool, 1 = CB pool
+    int64_t off;
+    int64_t ld;
+    int32_t rows, cols;
+    int32_t s;     // supernode the block belongs to
+};
+struct DistPlan {
+    int nranks = 1;
+    int cbb = 1024;  // CB column-block width
+    int nbo = 1024;  // panel slab width (panel_nb_outer)
+    std::vector<int32_t> owner;    // rank executing each supernode's assembly + panel
+    std::vector<int32_t> gsize;    // rank-group size of each supernode (1 = inside a subtree)
+    std::vector<int32_t> split;    // index into split_s / cb_rank, or -1
+    std::vector<int32_t> split_s;
+    std::vector<std::vector<int32_t>> cb_rank;  // per split front: rank of CB column block jb
+    std::vector<DistStep> steps;
+    std::vector<DistMsg> msgs;     // ascending step
+    std::vector<double> work;      // estimated flops per rank
+};
+int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D);
+// transport argument of numeric_create_dist selecting the dry mode
+#define DIST_DRY ((int32_t(*)(void*, int32_t, int32_t, void*, int64_t))1)
+
+// One point-to-point block transfer of this rank (device addresses resolved).
 struct Msg {
-    double* buf;
-    int64_t count;  // doubles
+    double* buf;      // staging slot (packed rows x cols)
+    int64_t count;    // doubles
     int32_t peer;
     int32_t is_send;
-    int32_t child;  // supernode whose CB moves
+    int32_t child;    // supernode whose data moves
 };
 
 struct Launch {
@@ -46,6 +87,11 @@ struct Launch {
     int32_t strm;     // 0 = main stream, 1 = lookahead stream
     int32_t fuse;     // panel launch whose tasks may factor the next diagonal block (potrf_col)
     double flops;     // algorithmic SYRK flops (CB launches: mb*(mb+1)*w)
+    // L_COMM: copy tiles [poff, poff + pcount) pack the sends, [uoff, uoff + ucount)
+    // unpack the receives (Numeric::d_ctiles)
+    int64_t poff, uoff;
+    int32_t pcount, ucount;
+    int32_t step;
 };
 
 struct Numeric {
@@ -54,6 +100,7 @@ struct Numeric {
     int panel_variant = PANEL_VARIANT;  // large-front POTRF/TRSM kernels (kernels.hpp)
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;  // trailing panel updates overlapped with the next slab
+    hipStream_t stream3 = nullptr;  // multi-GPU: comm stream (pack, RCCL group, unpack), strm == 2
     std::vector<hipEvent_t> sync_ev;
     int32_t n_sync_events = 0;
     DevPlan P {};
@@ -90,8 +137,17 @@ struct Numeric {
     // pools, no transfers) to validate the partition on one device.
     int rank = 0, nranks = 1, virt_ranks = 0;
     std::vector<int32_t> owner;
+    DistPlan D;
     std::vector<Msg> msgs;
+    Copy2D* d_copy = nullptr;     // pack / unpack descriptors
+    int2* d_ctiles = nullptr;     // (descriptor, first column) per copy workgroup
+    double* staging = nullptr;    // one packed slot per message of this rank
     void* comm = nullptr;  // ncclComm_t
+    // host-staged transport (tests: several processes on one GPU, no RCCL):
+    // op 0 post send, 1 post recv, 2 complete everything posted
+    int32_t (*xport)(void* ctx, int32_t op, int32_t peer, void* buf, int64_t bytes) = nullptr;
+    void* xport_ctx = nullptr;
+    bool dry_comm = false;  // comm steps pack / unpack but move nothing (one-rank timing projection)
     double comm_ms = 0.0;
 
     std::string err;

@@ -32,12 +32,12 @@ def test_single_rank_has_no_messages():
     assert np.all(own == 0)
 
 
-def _worker(rank, world, port, k, out):
+def _worker(rank, world, port, k, opts, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        s = sc.Symbolic(sc.laplacian3d(k))
+        s = sc.Symbolic(sc.laplacian3d(k), **opts)
         lev, peer, nb, snd = s.dist_schedule(world, rank)
         mine = [(int(a), int(b), int(c), int(d)) for a, b, c, d in zip(lev, peer, nb, snd)]
         allv = [None] * world
@@ -51,7 +51,8 @@ def _worker(rank, world, port, k, out):
                 recvs = [(l, n) for (l, p, n, sd) in allv[b] if sd == 0 and p == a]
                 if sends != recvs:
                     ok = False
-        # levels are non-decreasing in each rank's posting order (deadlock-free grouping)
+        # comm steps are non-decreasing in each rank's posting order (one global step
+        # order: deadlock-free)
         for msgs in allv:
             levels = [m[0] for m in msgs]
             if levels != sorted(levels):
@@ -62,14 +63,37 @@ def _worker(rank, world, port, k, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,k", [(2, 16), (4, 20)])
-def test_message_schedule_matches_across_ranks(world, k):
+@pytest.mark.parametrize("world,k,opts", [(2, 16, {}), (4, 20, {}),
+                                          (4, 20, dict(panel_nb_outer=128, dist_cbb=64, small_front_max=32)),
+                                          (3, 24, dict(dist_cbb=128)), (4, 20, dict(dist_split=0))])
+def test_message_schedule_matches_across_ranks(world, k, opts):
     import random
 
     port = 29500 + random.randint(0, 2000)
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, port, k, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, port, k, opts, out), nprocs=world, join=True)
     res = [out[r] for r in range(world)]
     assert all(ok for ok, _ in res), res
     assert res[0][1] > 0  # some contribution blocks do cross ranks
+
+
+@pytest.mark.parametrize("k,nranks", [(20, 4), (24, 8), (24, 3)])
+def test_split_front_plan(k, nranks):
+    # shared fronts: rank groups nest; a split front (shared, large, with a CB) keeps
+    # its panel on the owner and deals every CB column block to other group members
+    s = sc.Symbolic(sc.laplacian3d(k), panel_nb_outer=128, dist_cbb=64, small_front_max=32)
+    info = s.dist_plan_info(nranks)
+    sn = s.supernodes()
+    g, cbr = info["gsize"], info["split_cb_ranks"]
+    assert (cbr > 0).any()
+    for v in np.nonzero(cbr)[0]:
+        assert g[v] > 1
+        assert 1 <= cbr[v] <= g[v] - 1
+        assert sn["m"][v] > sn["w"][v]  # has a contribution block
+    par = sn["parent"]
+    for v in range(len(g)):  # groups only shrink going down the tree
+        if par[v] >= 0:
+            assert g[v] <= g[par[v]]
+    s0 = sc.Symbolic(sc.laplacian3d(k), panel_nb_outer=128, dist_cbb=64, small_front_max=32, dist_split=0)
+    assert (s0.dist_plan_info(nranks)["split_cb_ranks"] == 0).all()

@@ -195,10 +195,10 @@ def test_device_resident_factor(gpu):
 
 @pytest.mark.parametrize("nranks", [2, 3, 8])
 def test_partitioned_schedule_bitwise_equal(gpu, nranks):
-    # the multi-GPU partition (every front computed once by its owner, per-level
-    # ordering) emulated in one process must reproduce the single-GPU factor
+    # the multi-GPU partition with every front on one rank (dist_split=0), emulated in
+    # one process, must reproduce the single-GPU factor bitwise
     A = sc.laplacian3d(20)
-    s = sc.Symbolic(A)
+    s = sc.Symbolic(A, dist_split=0)
     ref = sc.Numeric(s)
     assert ref.factor(A.x) == 0
     _, L0 = ref.export()
@@ -207,6 +207,22 @@ def test_partitioned_schedule_bitwise_equal(gpu, nranks):
     _, L1 = v.export()
     assert np.array_equal(L0.x, L1.x)
     st, Lp, Li, Lx = oracle.chol(A)
+    assert rel_fro(L1.x, Lx) < TOL
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 4, 8])
+def test_partitioned_split_fronts_emulated(gpu, nranks):
+    # split top fronts (panel on the owner, CB column blocks updated per slab by the
+    # other ranks of the group), emulated in one process: the same factor to 1e-12
+    A = sc.laplacian3d(20)
+    s = sc.Symbolic(A, panel_nb_outer=128, dist_cbb=64, small_front_max=32)
+    info = s.dist_plan_info(nranks)
+    assert nranks == 2 or (info["split_cb_ranks"] > 0).any()
+    v = sc.Numeric(s, nranks=nranks, virtual=True)
+    assert v.factor(A.x) == 0
+    _, L1 = v.export()
+    st, Lp, Li, Lx = oracle.chol(A)
+    assert np.array_equal(L1.p, Lp) and np.array_equal(L1.i, Li)
     assert rel_fro(L1.x, Lx) < TOL
 
 
