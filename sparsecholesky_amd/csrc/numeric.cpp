@@ -550,8 +550,9 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     } else if (ok) {
         ok = hipStreamCreateWithPriority(&N.stream2, hipStreamNonBlocking, prio_lo) == hipSuccess;
     }
-    // multi-GPU comm stream (only then: an extra stream changes the hardware-queue
-    // mapping of the other two, measured 569 -> 649 ms single-GPU at 128^3)
+    // multi-GPU comm stream.  Only there: one more stream on the device costs 13.5%
+    // under hipGraph replay (569 -> 649 ms at 128^3, any priority, any
+    // GPU_MAX_HW_QUEUES) though nothing runs on it; eager runs (multi-GPU) see 0.5%.
     if (ok && !N.owner.empty() && N.virt_ranks <= 1)
         ok = hipStreamCreateWithPriority(&N.stream3, hipStreamNonBlocking, prio_hi) == hipSuccess;
     if (!ok) {
