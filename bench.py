@@ -89,6 +89,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--k", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-solve", action="store_true")
     ap.add_argument("--cpu-k", type=int, default=32)
     ap.add_argument("--graph", type=int, default=1)
     ap.add_argument("--relax-wmax", type=int, default=None)
@@ -218,6 +219,24 @@ def main():
                               "panel_update_ms": round(pms, 2), "panel_update_flops": pfl,
                               "cb_all_tflops": round(cfl / (cms * 1e-3) / 1e12, 2)}
 
+    solve = None
+    if world == 1 and not args.no_solve:
+        # triangular solves with the factor: forward + backward sweep, each
+        # reads L once (8 * panel entries bytes, relaxed zeros included)
+        d_b = torch.ones(st["n"], dtype=torch.float64, device=f"cuda:{dev}")
+        d_x = torch.empty_like(d_b)
+        num.solve_device(d_b.data_ptr(), d_x.data_ptr())
+        reps = 3
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            num.solve_device(d_b.data_ptr(), d_x.data_ptr())
+        torch.cuda.synchronize()
+        sms = (time.perf_counter() - t0) * 1e3 / reps
+        lbytes = 2.0 * 8.0 * st["panel_entries"]
+        solve = {"ms": round(sms, 3), "L_read_GBs": round(lbytes / (sms * 1e-3) / 1e9, 1),
+                 "note": "x = A^-1 b, device vectors, forward + backward sweep; GB/s = 2 x 8 B x panel entries / time"}
+
     out = {
         "metric": "numeric-factorization fp64 GFLOP/s (F=sum colcount^2)",
         "value": round(gflops, 2),
@@ -247,6 +266,7 @@ def main():
         "roofline": roof,
         "timing_s": {"generate": round(t_gen, 3), "analyze": round(t_an, 3), "numeric_create": round(t_alloc, 3)},
         "phase_ms": phases,
+        "solve": solve,
     }
     if not args.no_cpu_baseline and rank == 0 and world == 1:
         out["cpu_baseline"] = cpu_baseline(args.cpu_k)

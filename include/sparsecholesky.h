@@ -168,9 +168,13 @@ int64_t sc_numeric_syrk_stats(sc_numeric* num, int32_t wmin, double* flops, doub
                               int64_t* launches);
 void sc_free_numeric(sc_numeric* num);
 
-/* Solve A x = b with the factor (forward/back substitution on the host,
- * natural order).  Not in the reference; used for residual checks. */
+/* Solve A x = b with the factor on the GPU (not in the reference):
+ * level-scheduled supernodal forward (L y = P b) and backward (L^T z = y) sweeps,
+ * x = P^T z.  sc_solve_host: host vectors b, x (length n; copies over PCIe);
+ * sc_solve_device: device vectors (may alias), synchronous.  Returns the factor's
+ * status (> 0: not positive definite, nothing solved); single-device handles only. */
 int64_t sc_solve_host(sc_numeric* num, const double* b, double* x);
+int64_t sc_solve_device(sc_numeric* num, const double* d_b, double* d_x);
 
 /* ---------------- reference-API helpers (host) ----------------
  * Each mirrors one reference function, with int64 column pointers. */

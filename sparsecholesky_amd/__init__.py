@@ -118,6 +118,7 @@ _SIGS = [
     ("sc_numeric_syrk_stats", _I64, [_P, _I32, C.POINTER(_D), C.POINTER(_D), C.POINTER(_I64)]),
     ("sc_free_numeric", None, [_P]),
     ("sc_solve_host", _I64, [_P, _P, _P]),
+    ("sc_solve_device", _I64, [_P, _P, _P]),
     ("sc_etree", _I64, [_I64, _P, _P, _P]),
     ("sc_post_order", _I64, [_I64, _P, _P]),
     ("sc_col_count", _I64, [_I64, _P, _P, _P, _P, _P]),
@@ -582,10 +583,20 @@ class Numeric:
         return st, csc_matrix(n, n, Lp, Li[:nz], Lx[:nz], sym.none)
 
     def solve(self, b: np.ndarray) -> np.ndarray:
+        """x = A^{-1} b on the GPU (host vectors in / out)."""
         b = np.ascontiguousarray(b, dtype=np.float64)
         x = np.zeros_like(b)
-        _check(lib().sc_solve_host(self.h, _ptr(b), _ptr(x)), "solve")
+        st = _check(lib().sc_solve_host(self.h, _ptr(b), _ptr(x)), "solve")
+        if st > 0:
+            raise LibraryError(f"solve: A is not positive definite (column {st})")
         return x
+
+    def solve_device(self, d_b_ptr: int, d_x_ptr: int) -> int:
+        """x = A^{-1} b with device vectors (may alias)."""
+        st = _check(lib().sc_solve_device(self.h, C.c_void_p(d_b_ptr), C.c_void_p(d_x_ptr)), "solve_device")
+        if st > 0:
+            raise LibraryError(f"solve_device: A is not positive definite (column {st})")
+        return st
 
     def __del__(self):
         h = getattr(self, "h", None)

@@ -244,23 +244,16 @@ void sc_free_numeric(sc_numeric* num) {
 
 int64_t sc_solve_host(sc_numeric* num, const double* b, double* x) {
     if (!num || !num->N || !b || !x) return SC_ERR_ARG;
-    const auto& S = num->sym->S;
-    const int64_t n = S.n;
-    std::vector<int64_t> Lp((size_t)n + 1);
-    std::vector<int32_t> Li((size_t)std::max<int64_t>(S.nnzL, 1));
-    std::vector<double> Lx((size_t)std::max<int64_t>(S.nnzL, 1));
-    int64_t st = sc::numeric_export(*num->N, Lp.data(), Li.data(), Lx.data());
-    if (st != SC_OK) return st;
-    std::memmove(x, b, sizeof(double) * (size_t)n);
-    for (int64_t j = 0; j < n; ++j) {  // L y = b
-        x[j] /= Lx[Lp[j]];
-        for (int64_t p = Lp[j] + 1; p < Lp[j + 1]; ++p) x[Li[p]] -= Lx[p] * x[j];
-    }
-    for (int64_t j = n - 1; j >= 0; --j) {  // L^T x = y
-        for (int64_t p = Lp[j] + 1; p < Lp[j + 1]; ++p) x[j] -= Lx[p] * x[Li[p]];
-        x[j] /= Lx[Lp[j]];
-    }
-    return SC_OK;
+    int64_t rc = sc::numeric_solve_host(*num->N, b, x);
+    if (rc < 0) g_last_error = num->N->err;
+    return rc;
+}
+
+int64_t sc_solve_device(sc_numeric* num, const double* d_b, double* d_x) {
+    if (!num || !num->N || !d_b || !d_x) return SC_ERR_ARG;
+    int64_t rc = sc::numeric_solve_device(*num->N, d_b, d_x);
+    if (rc < 0) g_last_error = num->N->err;
+    return rc;
 }
 
 // ---- reference-API helpers ----

@@ -882,4 +882,146 @@ hipError_t launch_mfma_peak(double* out, int blocks, int iters, int nacc, hipStr
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Triangular solves with the supernodal factor (the
+// reference has no solve).  Level-scheduled like the factorization; per 64-column
+// block of every supernode of a level: a one-wave diagonal solve (block staged in
+// LDS, pivot broadcast by readlane) and a multi-workgroup GEMV over the rows
+// below it.  HBM-bound: L is read once per sweep.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void solve_diag_kernel(SolvePlan P, const int2* __restrict__ tasks, int backward) {
+    __shared__ double Lb[PNB * (PNB + 1)];  // Lb[j * (PNB + 1) + i] = L(k0 + i, k0 + j)
+    __shared__ double dinv[PNB];
+    const int2 t = tasks[blockIdx.x];
+    const int s = t.x, k0 = t.y;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int c0 = P.sn_start[s];
+    const int w = P.sn_start[s + 1] - c0;
+    const int m = P.sn_m[s];
+    const int nb = min(PNB, w - k0);
+    const double* __restrict__ pan = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m + k0;
+    // stage the block: 16 independent loads per thread, one column per wave access
+#pragma unroll
+    for (int q = 0; q < PNB * PNB / 256; ++q) {
+        const int e = tid + 256 * q, j = e >> 6, i = e & 63;
+        Lb[j * (PNB + 1) + i] = (i < nb && j < nb) ? pan[(int64_t)j * m + i] : 0.0;
+    }
+    if (tid < PNB) dinv[tid] = 0.0;
+    __syncthreads();
+    if (tid < nb) dinv[tid] = 1.0 / Lb[tid * (PNB + 1) + tid];
+    __syncthreads();
+    if (tid >= 64) return;
+    // lane i keeps its row (forward: L(i, j)) or column (backward: L(j, i)) of the
+    // block in registers; all 64 steps run (zero padding past nb is inert), fully
+    // unrolled so the pivot and its reciprocal come from readlane, not LDS
+    double r[PNB];
+#pragma unroll
+    for (int j = 0; j < PNB; ++j) r[j] = backward ? Lb[lane * (PNB + 1) + j] : Lb[j * (PNB + 1) + lane];
+    const double d = dinv[lane];
+    double v = lane < nb ? P.c[c0 + k0 + lane] : 0.0;
+    if (!backward) {
+#pragma unroll
+        for (int j = 0; j < PNB; ++j) {  // y_j = v_j / L_jj; v_i -= L_ij y_j (i > j)
+            const double yj = readlane_f64(v, j) * readlane_f64(d, j);
+            v = lane == j ? yj : (lane > j ? v - r[j] * yj : v);
+        }
+    } else {
+#pragma unroll
+        for (int j = PNB - 1; j >= 0; --j) {  // x_j = v_j / L_jj; v_i -= L_ji x_j (i < j)
+            const double xj = readlane_f64(v, j) * readlane_f64(d, j);
+            v = lane == j ? xj : (lane < j ? v - r[j] * xj : v);
+        }
+    }
+    if (lane < nb) P.c[c0 + k0 + lane] = v;
+}
+
+__global__ __launch_bounds__(SOLVE_ROWS) void solve_gemv_kernel(SolvePlan P, const int4* __restrict__ tasks,
+                                                                int backward) {
+    __shared__ double vb[SOLVE_ROWS];             // forward: y_blk; backward: x of the rows
+    __shared__ double T[PNB * (PNB + 1)];         // backward: 64-row chunk, T[j * (PNB + 1) + i]
+    __shared__ double part[SOLVE_ROWS / 64][PNB];
+    const int4 t = tasks[blockIdx.x];
+    const int s = t.x, k0 = t.y, r0 = t.z;
+    const int tid = threadIdx.x;
+    const int c0 = P.sn_start[s];
+    const int w = P.sn_start[s + 1] - c0;
+    const int m = P.sn_m[s];
+    const int nb = min(PNB, w - k0);
+    const double* __restrict__ pan = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m;
+    const int32_t* __restrict__ rows = P.rows + P.rows_ptr[s];
+    const int r = r0 + tid;
+    const bool live = r < m;
+    if (!backward) {
+        // one thread per row; 16 independent loads in flight per chunk
+        if (tid < PNB) vb[tid] = tid < nb ? P.c[c0 + k0 + tid] : 0.0;
+        __syncthreads();
+        double acc = 0.0;
+#pragma unroll
+        for (int jc = 0; jc < PNB; jc += 16) {
+            double v[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = (live && jc + q < nb) ? pan[(int64_t)(jc + q) * m + r] : 0.0;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc += v[q] * vb[jc + q];
+        }
+        if (live) unsafeAtomicAdd(P.c + rows[r], -acc);
+        return;
+    }
+    // backward: c[blk] -= L[rows, blk]^T x[rows].  Per 64-row chunk: coalesced
+    // column loads into LDS, then thread (column j, quarter g) sums 16 rows of column j.
+    vb[tid] = live ? P.c[rows[r]] : 0.0;
+    const int j = tid & 63, g = tid >> 6;
+    double acc = 0.0;
+    for (int ch = 0; ch < SOLVE_ROWS && r0 + ch < m; ch += 64) {
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PNB * 64 / SOLVE_ROWS; ++q) {
+            const int e = tid + SOLVE_ROWS * q, jj = e >> 6, ii = e & 63;
+            const int rr = r0 + ch + ii;
+            T[jj * (PNB + 1) + ii] = (rr < m && jj < nb) ? pan[(int64_t)jj * m + rr] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc += T[j * (PNB + 1) + g * 16 + q] * vb[ch + g * 16 + q];
+    }
+    part[g][j] = acc;
+    __syncthreads();
+    if (tid < nb) {
+        double a = 0.0;
+#pragma unroll
+        for (int q = 0; q < SOLVE_ROWS / 64; ++q) a += part[q][tid];
+        unsafeAtomicAdd(P.c + c0 + k0 + tid, -a);
+    }
+}
+
+__global__ void permute_kernel(double* __restrict__ dst, const double* __restrict__ src,
+                               const int32_t* __restrict__ perm, int64_t n, int scatter) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (scatter)
+        dst[perm[i]] = src[i];
+    else
+        dst[i] = src[perm[i]];
+}
+
+hipError_t launch_solve_diag(const SolvePlan& P, const int2* tasks, int count, bool backward, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(solve_diag_kernel, dim3(count), dim3(256), 0, st, P, tasks, backward ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_solve_gemv(const SolvePlan& P, const int4* tasks, int count, bool backward, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(solve_gemv_kernel, dim3(count), dim3(SOLVE_ROWS), 0, st, P, tasks, backward ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_permute(double* dst, const double* src, const int32_t* perm, int64_t n, bool scatter,
+                          hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(permute_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, dst, src, perm, n,
+                       scatter ? 1 : 0);
+    return hipGetLastError();
+}
+
 }  // namespace sc

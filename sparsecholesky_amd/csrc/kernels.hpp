@@ -68,6 +68,28 @@ constexpr int COPY_COLS = 16;  // columns per copy workgroup
 // tiles: (descriptor, first column) per workgroup
 hipError_t launch_copy2d(const Copy2D* descs, const int2* tiles, int count, bool unpack, hipStream_t st);
 
+// ---- triangular solves with the supernodal factor ----
+struct SolvePlan {
+    const int32_t* sn_start;
+    const int32_t* sn_m;
+    const int64_t* panel_off;
+    const int64_t* rows_ptr;  // ns+1
+    const int32_t* rows;      // front rows (internal numbering), first w = the pivots
+    const double* panel_pool;
+    double* c;                // right-hand side / solution, internal numbering
+};
+constexpr int SOLVE_ROWS = 256;  // front rows per GEMV workgroup
+// tasks (s, k0): the 64-column diagonal block of supernode s at column k0;
+// forward L11 y = c, backward L11^T x = c, in place in c
+hipError_t launch_solve_diag(const SolvePlan& P, const int2* tasks, int count, bool backward, hipStream_t st);
+// tasks (s, k0, r0): front rows [r0, r0 + SOLVE_ROWS) below the block.  Forward:
+// c[rows[r]] -= L[r, blk] y_blk (fp64 atomics: fronts of a level share ancestors);
+// backward: c[blk] -= L[r, blk]^T x[rows[r]]
+hipError_t launch_solve_gemv(const SolvePlan& P, const int4* tasks, int count, bool backward, hipStream_t st);
+// c[i] = b[perm[i]] (gather) or x[perm[i]] = c[i] (scatter)
+hipError_t launch_permute(double* dst, const double* src, const int32_t* perm, int64_t n, bool scatter,
+                          hipStream_t st);
+
 hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count, int maxm, const double* Ax,
                               hipStream_t st);
 // tiled: tasks are (front, (row tile << 16) | 16-column block) for the write-once

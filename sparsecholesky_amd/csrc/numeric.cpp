@@ -888,6 +888,115 @@ int64_t numeric_export(Numeric& N, int64_t* Lp, int32_t* Li, double* Lx) {
     return st;
 }
 
+// ---------------- triangular solves ----------------
+// A = P^T L L^T P (P = etree postorder): c = P b; L y = c (levels up); L^T x = y
+// (levels down); x = P^T c.  Per level and 64-column step: diagonal solves of every
+// supernode with w > k0 (one wave each), GEMVs over the rows below (SOLVE_ROWS per
+// workgroup).  Forward runs the steps in order, backward in reverse (GEMV first).
+static int64_t solve_build(Numeric& N) {
+    const Symbolic& S = *N.S;
+    std::vector<std::vector<int32_t>> by_level((size_t)S.nlevels);
+    for (int32_t s = 0; s < S.ns; ++s) by_level[S.level[s]].push_back(s);
+    std::vector<int2> diag;
+    std::vector<int4> gemv;
+    for (int32_t lev = 0; lev < S.nlevels; ++lev) {
+        int maxw = 0;
+        for (int32_t s : by_level[lev]) maxw = std::max(maxw, S.w(s));
+        for (int k0 = 0; k0 < maxw; k0 += PNB) {
+            Numeric::SolveStep st {};
+            st.doff = (int64_t)diag.size();
+            st.goff = (int64_t)gemv.size();
+            for (int32_t s : by_level[lev]) {
+                const int w = S.w(s), m = S.sn_m[s];
+                if (w <= k0) continue;
+                diag.push_back(make_int2(s, k0));
+                for (int r0 = std::min(w, k0 + PNB); r0 < m; r0 += SOLVE_ROWS) gemv.push_back(make_int4(s, k0, r0, 0));
+            }
+            st.dcount = (int32_t)((int64_t)diag.size() - st.doff);
+            st.gcount = (int32_t)((int64_t)gemv.size() - st.goff);
+            N.solve_steps.push_back(st);
+        }
+    }
+    int64_t rc;
+    int32_t* d_rows = nullptr;
+    int64_t* d_rows_ptr = nullptr;
+    if ((rc = upload(N, diag, N.d_sdiag)) || (rc = upload(N, gemv, N.d_sgemv)) || (rc = upload(N, S.rows, d_rows)) ||
+        (rc = upload(N, S.rows_ptr, d_rows_ptr)) || (rc = upload(N, S.post, N.d_post)))
+        return rc;
+    void* p = nullptr;
+    if ((rc = dalloc(N, (size_t)std::max<int64_t>(S.n, 1) * 2 * sizeof(double), p))) return rc;
+    N.d_sbuf = (double*)p;
+    N.SP.sn_start = N.P.sn_start;
+    N.SP.sn_m = N.P.sn_m;
+    N.SP.panel_off = N.P.panel_off;
+    N.SP.rows_ptr = d_rows_ptr;
+    N.SP.rows = d_rows;
+    N.SP.panel_pool = N.P.panel_pool;
+    N.SP.c = N.d_sbuf + S.n;  // internal-order work vector
+    N.solve_ready = true;
+    return SC_OK;
+}
+
+int64_t numeric_solve_device(Numeric& N, const double* d_b, double* d_x) {
+    if (!N.factored) return SC_ERR_STATE;
+    if (!N.owner.empty() && N.virt_ranks <= 1) {
+        N.err = "solve needs the whole factor on one device (multi-rank handles hold only their part)";
+        return SC_ERR_NOTIMPL;
+    }
+    const int64_t st = numeric_status(N);
+    if (st != SC_OK) return st;
+    HIP_TRY(hipSetDevice(N.device));
+    if (!N.solve_ready) TRY(solve_build(N));
+    const int64_t n = N.S->n;
+    if (n == 0) return SC_OK;
+    hipStream_t s0 = N.stream;
+    if (!N.solve_gexec || N.solve_b != d_b || N.solve_x != d_x) {
+        // ~700 dependent steps per sweep at 128^3: replayed as one hipGraph
+        if (N.solve_gexec) (void)hipGraphExecDestroy(N.solve_gexec);
+        if (N.solve_graph) (void)hipGraphDestroy(N.solve_graph);
+        N.solve_gexec = nullptr;
+        N.solve_graph = nullptr;
+        HIP_TRY(hipStreamBeginCapture(s0, hipStreamCaptureModeThreadLocal));
+        hipError_t e = launch_permute(N.SP.c, d_b, N.d_post, n, false, s0);
+        for (size_t i = 0; e == hipSuccess && i < N.solve_steps.size(); ++i) {
+            const Numeric::SolveStep& t = N.solve_steps[i];
+            e = launch_solve_diag(N.SP, N.d_sdiag + t.doff, t.dcount, false, s0);
+            if (e == hipSuccess) e = launch_solve_gemv(N.SP, N.d_sgemv + t.goff, t.gcount, false, s0);
+        }
+        for (size_t i = N.solve_steps.size(); e == hipSuccess && i-- > 0;) {
+            const Numeric::SolveStep& t = N.solve_steps[i];
+            e = launch_solve_gemv(N.SP, N.d_sgemv + t.goff, t.gcount, true, s0);
+            if (e == hipSuccess) e = launch_solve_diag(N.SP, N.d_sdiag + t.doff, t.dcount, true, s0);
+        }
+        if (e == hipSuccess) e = launch_permute(d_x, N.SP.c, N.d_post, n, true, s0);
+        hipGraph_t g = nullptr;
+        hipError_t e2 = hipStreamEndCapture(s0, &g);
+        HIP_TRY(e);
+        HIP_TRY(e2);
+        N.solve_graph = g;
+        HIP_TRY(hipGraphInstantiate(&N.solve_gexec, g, nullptr, nullptr, 0));
+        N.solve_b = d_b;
+        N.solve_x = d_x;
+    }
+    HIP_TRY(hipGraphLaunch(N.solve_gexec, s0));
+    HIP_TRY(hipStreamSynchronize(s0));
+    return SC_OK;
+}
+
+int64_t numeric_solve_host(Numeric& N, const double* b, double* x) {
+    if (!N.factored) return SC_ERR_STATE;
+    const int64_t st = numeric_status(N);
+    if (st != SC_OK) return st;
+    HIP_TRY(hipSetDevice(N.device));
+    if (!N.solve_ready) TRY(solve_build(N));
+    const size_t nb = (size_t)N.S->n * sizeof(double);
+    if (nb == 0) return SC_OK;
+    HIP_TRY(hipMemcpy(N.d_sbuf, b, nb, hipMemcpyHostToDevice));
+    TRY(numeric_solve_device(N, N.d_sbuf, N.d_sbuf));
+    HIP_TRY(hipMemcpy(x, N.d_sbuf, nb, hipMemcpyDeviceToHost));
+    return SC_OK;
+}
+
 void comm_destroy(Numeric& N);  // dist.cpp
 
 void numeric_free(Numeric* Np) {
@@ -896,6 +1005,8 @@ void numeric_free(Numeric* Np) {
     (void)hipSetDevice(N.device);
     if (N.stream) (void)hipStreamSynchronize(N.stream);
     comm_destroy(N);
+    if (N.solve_gexec) (void)hipGraphExecDestroy(N.solve_gexec);
+    if (N.solve_graph) (void)hipGraphDestroy(N.solve_graph);
     if (N.gexec) (void)hipGraphExecDestroy(N.gexec);
     if (N.graph) (void)hipGraphDestroy(N.graph);
     for (auto e : N.ev)

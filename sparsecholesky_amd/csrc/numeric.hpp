@@ -150,6 +150,23 @@ struct Numeric {
     bool dry_comm = false;  // comm steps pack / unpack but move nothing (one-rank timing projection)
     double comm_ms = 0.0;
 
+    // triangular solves (built at the first solve)
+    struct SolveStep {
+        int64_t doff, goff;
+        int32_t dcount, gcount;
+    };
+    std::vector<SolveStep> solve_steps;  // forward order (levels up, k0 up)
+    bool solve_ready = false;
+    SolvePlan SP {};
+    int2* d_sdiag = nullptr;
+    int4* d_sgemv = nullptr;
+    int32_t* d_post = nullptr;
+    double* d_sbuf = nullptr;  // host-interface staging (b in, x out)
+    hipGraph_t solve_graph = nullptr;  // both sweeps captured once per (b, x) pair
+    hipGraphExec_t solve_gexec = nullptr;
+    const double* solve_b = nullptr;
+    double* solve_x = nullptr;
+
     std::string err;
 };
 
@@ -166,6 +183,10 @@ int64_t numeric_launch_trace(Numeric& N, int32_t* kind, int32_t* level, int32_t*
                              int64_t cap);
 int64_t numeric_syrk_stats(Numeric& N, int wmin, double* flops, double* ms, int64_t* launches);
 void numeric_free(Numeric* N);
+// x = A^{-1} b with the factor: device vectors of length n (may alias), on the
+// library stream, synchronous.  Single-device factors only.
+int64_t numeric_solve_device(Numeric& N, const double* d_b, double* d_x);
+int64_t numeric_solve_host(Numeric& N, const double* b, double* x);
 int64_t debug_syrk(double* dC, int ldc, const double* dA, int lda, int M, int N, int K);
 int64_t debug_bench(int which, int M, int K, int reps, int arg, double* tflops);
 

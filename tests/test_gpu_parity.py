@@ -150,17 +150,86 @@ def test_refactor_new_values(gpu):
         assert rel_fro(L.x, Lx) < TOL
 
 
-def test_solve_residual(gpu):
-    A = sc.laplacian3d(20)
+def _sym_full(A):
+    import scipy.sparse as sp
+
+    U = sp.csc_matrix((A.x, A.i, A.p), shape=(A.size(), A.size()))
+    U = sp.triu(U)
+    return (U + sp.triu(U, 1).T).tocsr()
+
+
+def _backward_error(A, x, b):
+    """normwise backward error |Ax - b|_inf / (|A|_inf |x|_inf + |b|_inf)"""
+    from scipy.sparse.linalg import norm as spnorm
+
+    Af = _sym_full(A)
+    r = Af @ x - b
+    return np.abs(r).max() / (spnorm(Af, np.inf) * np.abs(x).max() + np.abs(b).max())
+
+
+def _oracle_solve(A, b):
+    import scipy.sparse as sp
+    from scipy.sparse.linalg import spsolve_triangular
+
+    st, Lp, Li, Lx = oracle.chol(A)
+    L = sp.csc_matrix((Lx, Li, Lp), shape=(A.size(), A.size())).tocsr()
+    y = spsolve_triangular(L, b, lower=True)
+    return spsolve_triangular(L.T.tocsr(), y, lower=False)
+
+
+@pytest.mark.parametrize("case", ["lap20", "bcsstk01", "1138_bus", "random", "lap12_allfronts", "lap16_nbo128"])
+def test_solve_vs_oracle(gpu, mtx, case):
+    # GPU supernodal forward/backward solve vs triangular solves with the oracle's L
+    kw = {}
+    if case == "lap20":
+        A = sc.laplacian3d(20)
+    elif case == "random":
+        A = random_spd(500, 0.02, 5)
+    elif case == "lap12_allfronts":
+        A, kw = sc.laplacian3d(12), dict(small_front_max=0)
+    elif case == "lap16_nbo128":
+        A, kw = sc.laplacian3d(16), dict(small_front_max=0, panel_nb_outer=128)
+    else:
+        A = mtx(case)
+    s = sc.Symbolic(A, **kw)
+    num = sc.Numeric(s)
+    assert num.factor(A.x) == 0
+    rng = np.random.default_rng(1)
+    b = rng.standard_normal(A.size())
+    x = num.solve(b)
+    xo = _oracle_solve(A, b)
+    assert np.linalg.norm(x - xo) / np.linalg.norm(xo) < 1e-10
+    assert _backward_error(A, x, b) < 1e-14
+
+
+def test_solve_device_and_residual_lap32(gpu):
+    # size-independent property at a larger size: backward-stable solve residual
+    torch = pytest.importorskip("torch")
+    A = sc.laplacian3d(32)
     s = sc.Symbolic(A)
     num = sc.Numeric(s)
     assert num.factor(A.x) == 0
-    rng = np.random.default_rng(0)
+    rng = np.random.default_rng(2)
     xt = rng.standard_normal(A.size())
-    D = sc.csc_to_dense(A)
-    b = D @ xt
-    x = num.solve(b)
+    b = _sym_full(A) @ xt
+    d = torch.from_numpy(b.copy()).to("cuda:0")
+    torch.cuda.synchronize()
+    num.solve_device(d.data_ptr(), d.data_ptr())  # in place
+    x = d.cpu().numpy()
+    assert _backward_error(A, x, b) < 1e-14
     assert np.linalg.norm(x - xt) / np.linalg.norm(xt) < 1e-10
+    x2 = num.solve(b)
+    assert np.linalg.norm(x2 - x) / np.linalg.norm(x) < 1e-13
+
+
+def test_solve_after_failed_factor(gpu):
+    A = sc.laplacian3d(6)
+    A.x[A.p[5]:A.p[6]][-1] = -10.0  # diagonal of column 5 (last entry of an upper column)
+    num = sc.Numeric(sc.Symbolic(A))
+    st = num.factor(A.x)
+    assert st > 0
+    with pytest.raises(Exception):
+        num.solve(np.ones(A.size()))
 
 
 @pytest.mark.parametrize("M,N,K", [(64, 64, 16), (130, 70, 33), (300, 300, 256), (17, 5, 3)])
