@@ -73,8 +73,13 @@ typedef struct sc_options {
                                 has its contribution block computed by the other ranks of its group, slab-streamed
                                 (1, default); 0: every front on one rank */
     int32_t dist_cbb;        /* multi-GPU: column-block width of contribution-block ownership and transfers (1024) */
-    int32_t reserved[2];
+    int32_t ordering;        /* SC_ORDER_NATURAL (default: the given order, as the reference) or SC_ORDER_ND:
+                                factor P A P^T with a nested-dissection P (sc_symbolic_perm); L, the pattern
+                                and the statistics are then those of P A P^T, solves take and return A's order */
+    int32_t reserved[1];
 } sc_options;
+
+enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };
 
 /* Symbolic statistics (host analysis). */
 typedef struct sc_symbolic_stats {
@@ -123,6 +128,9 @@ int64_t sc_symbolic_etree(const sc_symbolic* sym, int32_t* parent, int32_t* post
  * sn_parent[ns] assembly-tree parent (-1 = root), level[ns] height.  Any may be NULL. */
 int64_t sc_symbolic_supernodes(const sc_symbolic* sym, int32_t* sn_start, int32_t* sn_m, int32_t* sn_parent,
                                int32_t* level);
+/* The ordering used: perm[new] = old (identity for SC_ORDER_NATURAL); returns 1
+ * when a fill-reducing permutation is in effect, else 0. */
+int64_t sc_symbolic_perm(const sc_symbolic* sym, int32_t* perm);
 void sc_free_symbolic(sc_symbolic* sym);
 
 /* ---------------- device numeric factorization ----------------

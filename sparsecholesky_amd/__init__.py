@@ -69,7 +69,7 @@ class Options(C.Structure):
         ("use_graph", C.c_int32), ("relax_wmax", C.c_int32), ("syrk_tile", C.c_int32),
         ("lookahead", C.c_int32), ("panel_variant", C.c_int32), ("inner_order", C.c_int32),
         ("asm_tile_min_m", C.c_int32), ("fuse_potrf", C.c_int32), ("dist_split", C.c_int32), ("dist_cbb", C.c_int32),
-        ("reserved", C.c_int32 * 2),
+        ("ordering", C.c_int32), ("reserved", C.c_int32 * 1),
     ]
 
 
@@ -104,6 +104,7 @@ _SIGS = [
     ("sc_symbolic_pattern", _I64, [_P, _P, _P]),
     ("sc_symbolic_etree", _I64, [_P, _P, _P]),
     ("sc_symbolic_supernodes", _I64, [_P, _P, _P, _P, _P]),
+    ("sc_symbolic_perm", _I64, [_P, _P]),
     ("sc_free_symbolic", None, [_P]),
     ("sc_numeric_create", _I64, [_P, _I32, C.POINTER(_P)]),
     ("sc_factor", _I64, [_P, _P]),
@@ -394,6 +395,19 @@ def atree(S: "SChol", sn_id, supernodes) -> np.ndarray:
     return sp
 
 
+def permute_symmetric(A: csc_matrix, perm: np.ndarray) -> csc_matrix:
+    """P A P^T as upper CSC (perm[new] = old); entries below the diagonal of A are
+    ignored as the reference does, duplicates are summed."""
+    n = A.size()
+    ip = np.empty(n, dtype=np.int64)
+    ip[np.asarray(perm, dtype=np.int64)] = np.arange(n)
+    col = np.repeat(np.arange(n, dtype=np.int64), np.diff(A.p))
+    keep = A.i <= col
+    a, b = ip[A.i[keep]], ip[col[keep]]
+    return triplet_to_csc_matrix(np.minimum(a, b).astype(np.int32), np.maximum(a, b).astype(np.int32),
+                                 A.x[keep], n)
+
+
 def csc_to_dense(A: csc_matrix) -> np.ndarray:
     """chol.hpp:1448-1479 (returns a 2-D array; the reference returns column-major flat)."""
     D = np.zeros((A.rows(), A.cols()))
@@ -448,6 +462,12 @@ class Symbolic:
         Li = np.zeros(max(self.nnz_L, 1), dtype=np.int32)
         _check(lib().sc_symbolic_pattern(self.h, _ptr(Lp), _ptr(Li)), "pattern")
         return Lp, Li[: self.nnz_L]
+
+    def perm(self) -> np.ndarray:
+        """Ordering in effect, perm[new] = old (identity unless ordering=SC_ORDER_ND)."""
+        p = np.zeros(max(self.n, 1), dtype=np.int32)
+        _check(lib().sc_symbolic_perm(self.h, _ptr(p)), "perm")
+        return p[: self.n]
 
     def etree(self):
         parent = np.zeros(self.n, dtype=np.int32)

@@ -100,7 +100,32 @@ int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_opt
     std::string err;
     int64_t rc;
     try {
-        rc = sc::analyze(n, Ap, Ai, o, h->S, err);
+        if (o.ordering == SC_ORDER_ND && n > 0 && Ap && (Ai || Ap[n] == 0)) {
+            // factor B = P A P^T; numeric values still come from A's arrays (a_src remapped)
+            std::vector<int32_t> perm((size_t)n);
+            std::vector<int64_t> Bp, src;
+            std::vector<int32_t> Bi;
+            // the CSC checks analyze() makes, before the ordering walks the arrays
+            rc = Ap[0] == 0 ? SC_OK : SC_ERR_ARG;
+            for (int64_t j = 0; rc == SC_OK && j < n; ++j)
+                if (Ap[j + 1] < Ap[j]) rc = SC_ERR_ARG;
+            for (int64_t p = 0; rc == SC_OK && p < Ap[n]; ++p)
+                if (Ai[p] < 0 || Ai[p] >= n) rc = SC_ERR_ARG;
+            if (rc != SC_OK) err = "malformed CSC";
+            if (rc == SC_OK) {
+                sc::nd_order(n, Ap, Ai, perm.data());
+                sc::permute_upper(n, Ap, Ai, perm.data(), Bp, Bi, src);
+                rc = sc::analyze(n, Bp.data(), Bi.data(), o, h->S, err);
+            }
+            if (rc == SC_OK) {
+                auto& S = h->S;
+                for (int64_t q = 0; q < S.nnzA_used; ++q) S.a_src[q] = src[S.a_src[q]];
+                S.nnzA_in = Ap[n];
+                S.perm = std::move(perm);
+            }
+        } else {
+            rc = sc::analyze(n, Ap, Ai, o, h->S, err);
+        }
     } catch (const std::bad_alloc&) {
         rc = SC_ERR_NOMEM;
         err = "out of host memory";
@@ -147,6 +172,18 @@ int64_t sc_symbolic_supernodes(const sc_symbolic* sym, int32_t* sn_start, int32_
     if (sn_parent && ns) std::memcpy(sn_parent, S.sn_parent.data(), sizeof(int32_t) * ns);
     if (level && ns) std::memcpy(level, S.level.data(), sizeof(int32_t) * ns);
     return S.ns;
+}
+
+int64_t sc_symbolic_perm(const sc_symbolic* sym, int32_t* perm) {
+    if (!sym) return SC_ERR_ARG;
+    const auto& S = sym->S;
+    if (perm) {
+        if (S.perm.empty())
+            for (int64_t i = 0; i < S.n; ++i) perm[i] = (int32_t)i;
+        else
+            std::memcpy(perm, S.perm.data(), sizeof(int32_t) * (size_t)S.n);
+    }
+    return S.perm.empty() ? 0 : 1;
 }
 
 void sc_free_symbolic(sc_symbolic* sym) { delete sym; }

@@ -899,6 +899,11 @@ static int64_t solve_build(Numeric& N) {
     for (int32_t s = 0; s < S.ns; ++s) by_level[S.level[s]].push_back(s);
     std::vector<int2> diag;
     std::vector<int4> gemv;
+    // internal index -> index in the caller's order (postorder, then the fill-reducing
+    // permutation when one is in effect)
+    std::vector<int32_t> solve_perm(S.post);
+    if (!S.perm.empty())
+        for (auto& v : solve_perm) v = S.perm[v];
     for (int32_t lev = 0; lev < S.nlevels; ++lev) {
         int maxw = 0;
         for (int32_t s : by_level[lev]) maxw = std::max(maxw, S.w(s));
@@ -921,7 +926,7 @@ static int64_t solve_build(Numeric& N) {
     int32_t* d_rows = nullptr;
     int64_t* d_rows_ptr = nullptr;
     if ((rc = upload(N, diag, N.d_sdiag)) || (rc = upload(N, gemv, N.d_sgemv)) || (rc = upload(N, S.rows, d_rows)) ||
-        (rc = upload(N, S.rows_ptr, d_rows_ptr)) || (rc = upload(N, S.post, N.d_post)))
+        (rc = upload(N, S.rows_ptr, d_rows_ptr)) || (rc = upload(N, solve_perm, N.d_post)))
         return rc;
     void* p = nullptr;
     if ((rc = dalloc(N, (size_t)std::max<int64_t>(S.n, 1) * 2 * sizeof(double), p))) return rc;

@@ -49,6 +49,7 @@ struct Symbolic {
     std::vector<i32> Ai;
 
     // natural-order symbolic (reference semantics)
+    std::vector<i32> perm;      // fill-reducing ordering, new -> old (empty: the given order)
     std::vector<i32> parent;    // etree
     std::vector<i32> post;      // internal -> natural
     std::vector<i32> ipost;     // natural -> internal
@@ -95,6 +96,12 @@ struct Symbolic {
 // `err` holds a message.
 i64 analyze(i64 n, const i64* Ap, const i32* Ai, const sc_options& opt, Symbolic& S,
             std::string& err);
+
+// Fill-reducing ordering (ordering.cpp): nested dissection by level structures,
+// perm[new] = old; and B = P A P^T as upper CSC with src[q] = A-index of entry q.
+i64 nd_order(i64 n, const i64* Ap, const i32* Ai, i32* perm);
+void permute_upper(i64 n, const i64* Ap, const i32* Ai, const i32* perm, std::vector<i64>& Bp,
+                   std::vector<i32>& Bi, std::vector<i64>& src);
 
 // Reference-layout pattern of L (schol().p()/i()), natural numbering.
 void pattern_L(const Symbolic& S, i64* Lp, i32* Li);

@@ -145,3 +145,31 @@ def test_empty_and_single():
     A1 = sc.triplet_to_csc_matrix([0], [0], [9.0], 1)
     s = sc.Symbolic(A1).stats()
     assert s["nnz_L"] == 1 and s["n_supernodes"] == 1
+
+
+@pytest.mark.parametrize("name", ["1138_bus", "lap20nat", "random"])
+def test_nd_ordering_pattern_and_fill(mtx, name):
+    # the factor of P A P^T (nested dissection) has the oracle's pattern of
+    # P A P^T and less fill than the given order
+    if name == "1138_bus":
+        A = mtx(name)
+    elif name == "lap20nat":
+        A = sc.laplacian3d(20, nd=False)
+    else:
+        rng = np.random.default_rng(3)
+        n = 400
+        i = rng.integers(0, n, 2000)
+        j = rng.integers(0, n, 2000)
+        A = sc.triplet_to_csc_matrix(np.concatenate([np.minimum(i, j), np.arange(n)]).astype(np.int32),
+                                     np.concatenate([np.maximum(i, j), np.arange(n)]).astype(np.int32),
+                                     np.concatenate([-np.ones(2000), np.full(n, 50.0)]), n)
+    s = sc.Symbolic(A, ordering=1)
+    p = s.perm()
+    assert np.array_equal(np.sort(p), np.arange(A.size()))
+    B = sc.permute_symmetric(A, p)
+    Lp, Li = s.pattern()
+    Op, Oi, _ = oracle.schol(B)
+    assert np.array_equal(Lp, Op) and np.array_equal(Li, Oi)
+    s0 = sc.Symbolic(A)
+    assert s.nnz_L < s0.nnz_L and s.flops < s0.flops
+    assert np.array_equal(s0.perm(), np.arange(A.size()))  # default: the given order
