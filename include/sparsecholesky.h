@@ -76,7 +76,8 @@ typedef struct sc_options {
     int32_t ordering;        /* SC_ORDER_NATURAL (default: the given order, as the reference) or SC_ORDER_ND:
                                 factor P A P^T with a nested-dissection P (sc_symbolic_perm); L, the pattern
                                 and the statistics are then those of P A P^T, solves take and return A's order */
-    int32_t reserved[1];
+    int32_t cb_slab;         /* 1: fronts with several slabs apply their CB update slab by slab on the lookahead
+                                stream (overlapping the panel chain); 0 (default): one K = w SYRK after the panel */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

@@ -1,0 +1,10 @@
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -k "panel_schedule or nonpd or not_pd" -x -q --timeout 240 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_pv3.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_pv3.log
+[ $rc -eq 0 ] || exit $rc
+for o in "" "--panel-variant 3" "" "--panel-variant 3"; do
+  timeout -k 10 300 python bench.py --no-cpu-baseline --no-solve $o > gpurun_out/pv3.log 2>&1 || exit $?
+  echo "opts [$o]"; grep '^{' gpurun_out/pv3.log | python3 scripts/summarize.py
+done

@@ -525,6 +525,70 @@ __global__ __launch_bounds__(256) void trsm_panel_g_kernel(DevPlan P, const int4
     for (int c = 0; c < PNB; ++c) buf_st(r[c], rs, voff, c * m * 8);
 }
 
+// Variant 3: POTRF fused into the panel TRSM (one launch and one dependent-launch
+// gap fewer per 64-column block on the chain).  Every workgroup of the block
+// factors the 64 x 64 diagonal block itself (wave 0, registers) into the packed
+// LDS operand stream; the workgroups' A11 loads all precede their ticket on the
+// front's counter, so the last one to take a ticket stores L11 over A11 (and
+// resets the counter for the next block / factorization).  No waiting anywhere.
+__global__ __launch_bounds__(256) void trsm_fused_g_kernel(DevPlan P, const int4* __restrict__ tasks) {
+    __shared__ double2 S[TRSM64_STREAM / 2 + PNB / 2];  // + one dummy slot per lane
+    __shared__ double C[2 * PNB];
+    __shared__ double Ld[PNB];   // diag(L11)
+    __shared__ int last;
+    const int4 t = tasks[blockIdx.x];
+    const int s = t.x, k0 = t.y, r0 = t.z;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int c0 = P.sn_start[s];
+    const int w = P.sn_start[s + 1] - c0;
+    const int m = P.sn_m[s];
+    const int nb = min(PNB, w - k0);
+    double* pan = P.panel_pool + P.panel_off[s];
+    if (nb < PNB) return;  // partial blocks: potrf + trsm_partial_kernel
+    double* Sd = reinterpret_cast<double*>(S);
+    const __amdgpu_buffer_rsrc_t rb = buf_rsrc(pan + (int64_t)k0 * m + k0);
+    if (tid < 64) {
+        double r[PNB];
+#pragma unroll
+        for (int c = 0; c < PNB; ++c) r[c] = buf_ld(rb, lane * 8, c * m * 8);
+        const int bad = potrf64_full(r, C, lane);
+        if (bad >= 0 && lane == 0) report_fail(P.info, c0 + k0 + bad);
+        double diag = 0.0;
+#pragma unroll
+        for (int c = 0; c < PNB; ++c) {
+            Sd[c < lane ? PNB * c - c * (c - 1) / 2 + (lane - c) : TRSM64_STREAM + lane] = r[c];
+            diag = (c == lane) ? r[c] : diag;
+        }
+        Sd[PNB * lane - lane * (lane - 1) / 2] = 1.0 / diag;
+        Ld[lane] = diag;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const int nwg = (m - (k0 + PNB) + TRSM_ROWS - 1) / TRSM_ROWS;
+        __threadfence();  // this workgroup's A11 reads precede its ticket
+        last = atomicAdd(P.blk_cnt + s, 1) == nwg - 1;
+        if (last) atomicExch(P.blk_cnt + s, 0);
+    }
+    __syncthreads();
+    if (last) {  // every workgroup has read A11: store L11 (lower, column-major, ld = m)
+        double* blk = pan + (int64_t)k0 * m + k0;
+        for (int e = tid; e < PNB * PNB; e += 256) {
+            const int j = e / PNB, q = e % PNB;
+            if (q > j) blk[(int64_t)j * m + q] = Sd[PNB * j - j * (j - 1) / 2 + (q - j)];
+            if (q == j) blk[(int64_t)j * m + q] = Ld[j];
+        }
+    }
+    const int row = r0 + tid;
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pan + (int64_t)k0 * m, (uint32_t)m * PNB * 8u);
+    const int voff = row < m ? row * 8 : BUF_DEAD;
+    double r[PNB];
+#pragma unroll
+    for (int c = 0; c < PNB; ++c) r[c] = buf_ld(rs, voff, c * m * 8);
+    trsm64_full(r, S);
+#pragma unroll
+    for (int c = 0; c < PNB; ++c) buf_st(r[c], rs, voff, c * m * 8);
+}
+
 // Variant 2 (default) panel TRSM: X := X W with W = inv(L11)^T from
 // potrf_inv_kernel, on fp64 MFMA (v_mfma_f64_16x16x4_f64).  Rows [r0, r0 + 64):
 // wave v owns rows r0 + 16v .. + 16 (A fragments = its 16 x 64 block of X in
@@ -588,12 +652,13 @@ __global__ __launch_bounds__(256) void trsm_panel_mfma_kernel(DevPlan P, const i
 // top-left of its C (the next panel block, complete after this update): tile
 // (0, 0) keeps that quadrant in LDS instead of storing it, and one wave factors it
 // in registers (potrf64_full) and stores L11, so the block needs no POTRF launch.
-template <int BT, int WM, int WN, int TAG, bool FUSE = false>
+template <int BT, int WM, int WN, int TAG, bool FUSE = false, int BK = 16>
 __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
                                                                   const int2* __restrict__ tiles,
                                                                   int32_t* __restrict__ info) {
     constexpr int NT = 64 * WM * WN;
-    constexpr int BK = 16;
+    // BK = 8 halves the LDS (36.9 KB at BT = 128) so that the panel chain's kernels
+    // still fit next to two resident lookahead workgroups on a CU
     constexpr int LDT = BT + 16;  // +128 B row pad: the two k-rows read by a half-wave hit disjoint banks
     constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
     __shared__ double smem[2 * 2 * BK * LDT];  // A and B stages; after the K loop: the fused POTRF block
@@ -747,7 +812,7 @@ hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hip
     if (count <= 0) return hipSuccess;
     if (variant == 0)
         hipLaunchKernelGGL(potrf_diag_kernel, dim3(count), dim3(64), 0, st, P, tasks);
-    else if (variant == 1)
+    else if (variant == 1 || variant == 3)  // 3: partial blocks / blocks with no rows below
         hipLaunchKernelGGL(potrf_diag_g_kernel, dim3(count), dim3(64), 0, st, P, tasks);
     else
         hipLaunchKernelGGL(potrf_inv_kernel, dim3(count), dim3(64), 0, st, P, tasks);
@@ -763,6 +828,8 @@ hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hip
         hipLaunchKernelGGL(trsm_panel_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks);
     else if (variant == 1)
         hipLaunchKernelGGL(trsm_panel_g_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks);
+    else if (variant == 3)
+        hipLaunchKernelGGL(trsm_fused_g_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks);
     else
         hipLaunchKernelGGL(trsm_panel_mfma_kernel, dim3(count), dim3(256), 0, st, P, tasks);
     return hipGetLastError();
@@ -774,9 +841,19 @@ hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hip
 // launch sits on a CU (the overlapped lookahead GEMMs leave room for the panel
 // chain's kernels instead of filling every CU twice).
 template <int TAG, bool FUSE>
-static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int bt, bool one_per_cu, int32_t* info,
+static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int bt, int lds_mode, int32_t* info,
                           hipStream_t st) {
     constexpr size_t kHalfLds = 80 * 1024;
+    const bool one_per_cu = lds_mode == 1;
+    if (lds_mode == 2 && !FUSE) {  // BK = 8: half the LDS per workgroup
+        if (bt == 128)
+            hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, false, 8>), dim3(n), dim3(512), 0, st, tasks, tiles,
+                               info);
+        else
+            hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG, false, 8>), dim3(n), dim3(256), 0, st, tasks, tiles,
+                               info);
+        return;
+    }
     if (bt == SYRK_BT_LARGE_W4) {  // 128 x 128 on 4 waves of 64 x 64 (experimental)
         hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 2, TAG, FUSE>), dim3(n), dim3(256), 0, st, tasks, tiles, info);
     } else if (bt == 128) {
@@ -793,14 +870,14 @@ static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int b
 }
 
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
-                       bool one_per_cu, int32_t* fuse_info) {
+                       int lds_mode, int32_t* fuse_info) {
     if (total_tiles <= 0) return hipSuccess;
     if (tag)
-        launch_syrk_t<1, false>(tasks, tiles, total_tiles, bt, one_per_cu, nullptr, st);
+        launch_syrk_t<1, false>(tasks, tiles, total_tiles, bt, lds_mode, nullptr, st);
     else if (fuse_info)
-        launch_syrk_t<0, true>(tasks, tiles, total_tiles, bt, one_per_cu, fuse_info, st);
+        launch_syrk_t<0, true>(tasks, tiles, total_tiles, bt, lds_mode, fuse_info, st);
     else
-        launch_syrk_t<0, false>(tasks, tiles, total_tiles, bt, one_per_cu, nullptr, st);
+        launch_syrk_t<0, false>(tasks, tiles, total_tiles, bt, lds_mode, nullptr, st);
     return hipGetLastError();
 }
 

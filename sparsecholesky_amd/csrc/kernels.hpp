@@ -43,6 +43,7 @@ struct DevPlan {
     double* panel_pool;
     double* cb_pool;
     int32_t* info;              // min failing internal column + 1
+    int32_t* blk_cnt;           // ns: arrival tickets of the fused POTRF+TRSM (panel variant 3)
 };
 
 // One lower-trapezoid SYRK update: C[i,j] -= sum_k A[i,k] A[j,k], j < N, j <= i < M.
@@ -102,7 +103,7 @@ hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count,
 // for A/B microbenchmarks (sc_debug_bench).
 constexpr int PANEL_VARIANT = 1;
 constexpr int TRSM_MFMA_ROWS = 64;
-inline int trsm_task_rows(int variant) { return variant >= 2 ? TRSM_MFMA_ROWS : TRSM_ROWS; }
+inline int trsm_task_rows(int variant) { return variant == 2 ? TRSM_MFMA_ROWS : TRSM_ROWS; }
 hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hipStream_t st,
                              int variant = PANEL_VARIANT);
 // partial: every task is a partial last block (nb < 64); variants 1/2 need those
@@ -110,8 +111,9 @@ hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hip
 hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st,
                              int variant = PANEL_VARIANT, bool partial = false);
 // fuse_info != nullptr: panel-update launch whose tasks may carry a fused POTRF
+// lds_mode: 0 default; 1 at most one workgroup per CU; 2 BK = 8 (half the LDS)
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
-                       bool one_per_cu = false, int32_t* fuse_info = nullptr);
+                       int lds_mode = 0, int32_t* fuse_info = nullptr);
 hipError_t launch_stamp(uint64_t* slot, hipStream_t st);
 hipError_t launch_fill_random(double* p, int64_t n, hipStream_t st);
 hipError_t launch_mfma_peak(double* out, int blocks, int iters, int nacc, hipStream_t st);

@@ -348,6 +348,13 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         // (stream 1), which overlaps the next slab's factorization.  A later outer
         // update of overlapping columns waits for the stream-1 work first.
         int b_pending = -1;
+        // cb_slab: fronts with several slabs (and a CB, not split) take their CB update
+        // slab by slab on stream 1 (K = NBO) as the slabs become final, instead of one
+        // K = w SYRK after the panel; the last slab stays in the level's CB launch
+        int cb_pending = -1;
+        auto cb_by_slab = [&](int32_t s) {
+            return S.opt.cb_slab != 0 && !is_split(s) && S.w(s) > NBO && S.mb(s) > 0;
+        };
         // fused POTRF: the update that completes block [c_lo, c_lo + 64) of front s
         // (its last update before its POTRF) factors that diagonal block in its tile
         // (0, 0); the block then gets no POTRF task.  fused_at[s] = that block's start.
@@ -356,7 +363,7 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             if (c_hi <= c_lo || kb <= ka) return;
             GemmTask t {};
             // (not with panel variant 2: its TRSM needs the inverse only potrf_inv_kernel forms)
-            if (s >= 0 && S.opt.fuse_potrf && N.panel_variant != 2 && S.w(s) - c_lo >= PNB && c_hi - c_lo >= PNB) {
+            if (s >= 0 && S.opt.fuse_potrf && N.panel_variant != 2 && N.panel_variant != 3 && S.w(s) - c_lo >= PNB && c_hi - c_lo >= PNB) {
                 t.potrf_col = S.sn_start[s] + c_lo + 1;
                 fused_at[s] = c_lo;
             }
@@ -379,7 +386,8 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             Lt.kind = L_TRSM;
             Lt.level = lev;
             Lt.off = (int64_t)trsm.size();
-            std::vector<GemmTask> upd, outer_a, outer_b;
+            std::vector<GemmTask> upd, outer_a, outer_b, cbs;
+            double cfl = 0.0;
             std::vector<int4> trsm_part;  // partial last blocks: own launch (big = 1)
             double uflops = 0.0, afl = 0.0, bfl = 0.0;
             for (int32_t s : large) {
@@ -387,7 +395,9 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
                 if (w <= k0) continue;
                 const int nb = std::min(PNB, w - k0);
                 const int k1 = k0 + nb;
-                if (fused_at[s] != k0) potrf.push_back(make_int2(s, k0));
+                // variant 3: full blocks with rows below are factored inside their TRSM
+                const bool in_trsm = N.panel_variant == 3 && nb == PNB && k1 < m;
+                if (fused_at[s] != k0 && !in_trsm) potrf.push_back(make_int2(s, k0));
                 for (int r0 = k1; r0 < m; r0 += trsm_task_rows(N.panel_variant))
                     (nb < PNB ? trsm_part : trsm).push_back(make_int4(s, k0, r0, 0));
                 double* pan = panel_pool + S.panel_off[s];
@@ -409,6 +419,19 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
                     const int nxt = S.opt.lookahead ? std::min(w, slab1 + NBO) : w;
                     add_update(outer_a, afl, pan, m, slab1, nxt, slab0, slab1, s);
                     add_update(outer_b, bfl, pan, m, nxt, w, slab0, slab1);
+                    if (cb_by_slab(s)) {
+                        const int mb = m - w;
+                        GemmTask t {};
+                        t.C = cb_pool + S.cb_off[s];
+                        t.A = pan + (int64_t)slab0 * m + w;
+                        t.ldc = mb;
+                        t.lda = m;
+                        t.M = mb;
+                        t.N = mb;
+                        t.K = slab1 - slab0;
+                        cbs.push_back(t);
+                        cfl += (double)mb * (mb + 1.0) * t.K;
+                    }
                 }
             }
             Lp.count = (int32_t)((int64_t)potrf.size() - Lp.off);
@@ -432,7 +455,7 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             }
             push_gemm_launch(L_PANEL, lev, upd, 0, uflops);
             int e_trsm = -1;
-            if (!outer_b.empty()) e_trsm = push_record(0);
+            if (!outer_b.empty() || !cbs.empty()) e_trsm = push_record(0);
             if (!outer_a.empty()) {
                 if (b_pending >= 0) {
                     push_wait(0, b_pending);
@@ -445,8 +468,14 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
                 push_gemm_launch(L_PANEL, lev, outer_b, 0, bfl, 1);
                 b_pending = push_record(1);
             }
+            if (!cbs.empty()) {  // after b_pending: the chain never waits for these
+                if (outer_b.empty()) push_wait(1, e_trsm);
+                push_gemm_launch(L_CB, lev, cbs, 1, cfl, 1);
+                cb_pending = push_record(1);
+            }
         }
         if (b_pending >= 0) push_wait(0, b_pending);
+        if (cb_pending >= 0) push_wait(0, cb_pending);
         // contribution-block SYRK, K = w; fronts with w >= 256 in their own launch
         for (int big = 1; big >= 0; --big) {
             std::vector<GemmTask> cbt;
@@ -455,15 +484,16 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
                 const int w = S.w(s), m = S.sn_m[s], mb = m - w;
                 if (mb <= 0 || (w >= 256) != (big == 1) || is_split(s)) continue;
                 GemmTask t {};
+                const int kfrom = cb_by_slab(s) ? ((w - 1) / NBO) * NBO : 0;  // last slab only
                 t.C = cb_pool + S.cb_off[s];
-                t.A = panel_pool + S.panel_off[s] + w;
+                t.A = panel_pool + S.panel_off[s] + (int64_t)kfrom * m + w;
                 t.ldc = mb;
                 t.lda = m;
                 t.M = mb;
                 t.N = mb;
-                t.K = w;
+                t.K = w - kfrom;
                 cbt.push_back(t);
-                fl += (double)mb * (mb + 1.0) * w;
+                fl += (double)mb * (mb + 1.0) * t.K;
             }
             push_gemm_launch(L_CB, lev, cbt, big, fl);
         }
@@ -560,7 +590,7 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
         return fail(SC_ERR_HIP);
     }
     N.use_graph = S.opt.use_graph != 0;
-    N.panel_variant = (S.opt.panel_variant == 1 || S.opt.panel_variant == 2) ? S.opt.panel_variant : PANEL_VARIANT;
+    N.panel_variant = (S.opt.panel_variant >= 1 && S.opt.panel_variant <= 3) ? S.opt.panel_variant : PANEL_VARIANT;
     const int32_t ns = S.ns;
     int64_t rc;
     DevPlan& P = N.P;
@@ -602,6 +632,12 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     P.cb_pool = (double*)p;
     if ((rc = dalloc(N, 64, p))) return fail(rc);
     P.info = (int32_t*)p;
+    if ((rc = dalloc(N, (size_t)std::max(ns, 1) * sizeof(int32_t), p))) return fail(rc);
+    if (hipMemset(p, 0, (size_t)std::max(ns, 1) * sizeof(int32_t)) != hipSuccess) {
+        N.err = "hipMemset failed";
+        return fail(SC_ERR_HIP);
+    }
+    P.blk_cnt = (int32_t*)p;
 
     std::vector<int32_t> small;
     std::vector<int2> asmv, potrf;
@@ -660,8 +696,16 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
             return launch_trsm_panel(N.P, N.d_trsm + L.off, L.count, N.stream, N.panel_variant, L.big != 0);
         case L_PANEL:
         case L_CB:
+        {
+            // lookahead 2: stream-1 updates at most one workgroup per CU; 4: stream-1
+            // updates with BK = 8; 5: every panel update with BK = 8
+            const int la = N.S->opt.lookahead;
+            int lds_mode = 0;
+            if (L.strm == 1 && la == 2) lds_mode = 1;
+            if ((L.strm == 1 && la == 4) || (L.kind == L_PANEL && la == 5)) lds_mode = 2;
             return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st,
-                               L.strm == 1 && N.S->opt.lookahead == 2, L.fuse ? N.P.info : nullptr);
+                               lds_mode, L.fuse ? N.P.info : nullptr);
+        }
         case L_COMM:
             return comm_launch(N, L);
     }

@@ -394,7 +394,10 @@ def test_dense_matrix_large_front(gpu):
 # TRSM), inner slab update order (0 right-looking, 1 recursive), lookahead modes
 PANEL_OPTS = [dict(panel_variant=2), dict(inner_order=0), dict(panel_variant=2, inner_order=0, lookahead=0),
               dict(lookahead=2), dict(panel_variant=2, lookahead=3), dict(lookahead=0), dict(asm_tile_min_m=1),
-              dict(asm_tile_min_m=300), dict(fuse_potrf=1), dict(fuse_potrf=1, inner_order=0, lookahead=0)]
+              dict(asm_tile_min_m=300), dict(fuse_potrf=1), dict(fuse_potrf=1, inner_order=0, lookahead=0),
+              dict(cb_slab=1), dict(cb_slab=1, panel_nb_outer=128), dict(cb_slab=1, panel_nb_outer=64, lookahead=0),
+              dict(panel_variant=3), dict(panel_variant=3, panel_nb_outer=128, lookahead=0),
+              dict(panel_variant=3, fuse_potrf=1)]
 
 
 @pytest.mark.parametrize("opts", PANEL_OPTS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
