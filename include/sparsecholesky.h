@@ -78,6 +78,9 @@ typedef struct sc_options {
                                 and the statistics are then those of P A P^T, solves take and return A's order */
     int32_t cb_slab;         /* 1: fronts with several slabs apply their CB update slab by slab on the lookahead
                                 stream (overlapping the panel chain); 0 (default): one K = w SYRK after the panel */
+    int32_t dist_early;      /* multi-GPU: a large child whose parent runs on another rank computes its CB in
+                                4-block column groups and sends each group as soon as it is done (1, default) */
+    int32_t reserved[1];
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

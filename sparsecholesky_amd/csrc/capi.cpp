@@ -82,6 +82,7 @@ void sc_default_options(sc_options* opt) {
     opt->fuse_potrf = 0;
     opt->dist_split = 1;
     opt->dist_cbb = 1024;
+    opt->dist_early = 1;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,

@@ -147,8 +147,15 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
         D.cb_rank.push_back(std::move(cbr));
     }
 
+    D.early_gw = 4 * D.cbb;
+    D.early.assign((size_t)ns, 0);
+    for (i32 c = 0; c < ns; ++c) {
+        const i32 p = S.sn_parent[c];
+        D.early[c] = S.opt.dist_early != 0 && p >= 0 && D.split[c] < 0 && D.owner[c] != D.owner[p] &&
+                     S.fclass[c] == FRONT_LARGE && S.mb(c) >= 2 * D.cbb;
+    }
     // comm steps in the global order: per level, the split fronts' INIT and SLAB
-    // steps (ascending supernode), then the level's DELIVER step
+    // steps (ascending supernode), then the level's DELIVER sub-steps
     std::vector<std::vector<i32>> by_level((size_t)S.nlevels);
     for (i32 s = 0; s < ns; ++s) by_level[S.level[s]].push_back(s);
     auto cb_block = [&](DistMsg& g, i32 c, int jb) {
@@ -204,11 +211,27 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
                 close_step(id);
             }
         }
+        for (i32 c : by_level[lev]) {  // early children: one sub-step per column group
+            if (!D.early[c]) continue;
+            const int mbc = S.mb(c), per = D.early_gw / D.cbb;
+            for (int g = 0; g * D.early_gw < mbc; ++g) {
+                const int32_t id = open_step(STEP_DELIVER, lev, c, g);
+                for (int jb = g * per; jb < (g + 1) * per && jb * D.cbb < mbc; ++jb) {
+                    DistMsg m {};
+                    m.step = id;
+                    m.src = D.owner[c];
+                    m.dst = D.owner[S.sn_parent[c]];
+                    cb_block(m, c, jb);
+                    D.msgs.push_back(m);
+                }
+                close_step(id);
+            }
+        }
         int32_t id = open_step(STEP_DELIVER, lev, -1, 0);
         for (i32 c : by_level[lev]) {
             const i32 p = S.sn_parent[c];
             const int mbc = S.mb(c);
-            if (p < 0 || mbc <= 0) continue;
+            if (p < 0 || mbc <= 0 || D.early[c]) continue;
             const int dst = D.owner[p];
             for (int jb = 0; jb * D.cbb < mbc; ++jb) {
                 const int src = D.split[c] >= 0 ? D.cb_rank[D.split[c]][jb] : D.owner[c];

@@ -147,16 +147,19 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
     const DistPlan& D = N.D;
     const bool real_comm = !N.owner.empty() && N.virt_ranks <= 1;
     auto is_split = [&](int32_t s) { return !D.split.empty() && D.split[s] >= 0; };
-    std::vector<int32_t> init_step, slab_step0, deliver_step((size_t)S.nlevels, -1);
+    std::vector<int32_t> init_step, slab_step0, early_step0, deliver_step((size_t)S.nlevels, -1);
+    std::vector<std::vector<int>> early_ev((size_t)S.ns);  // sender: event after each CB column group
     std::vector<int64_t> step_beg;
     if (!N.owner.empty()) {
         init_step.assign((size_t)S.ns, -1);
         slab_step0.assign((size_t)S.ns, -1);
+        early_step0.assign((size_t)S.ns, -1);
         for (int32_t id = 0; id < (int32_t)D.steps.size(); ++id) {
             const DistStep& t = D.steps[id];
             if (t.kind == STEP_INIT) init_step[t.s] = id;
             if (t.kind == STEP_SLAB && t.k == 0) slab_step0[t.s] = id;
-            if (t.kind == STEP_DELIVER) deliver_step[t.level] = id;
+            if (t.kind == STEP_DELIVER && t.s < 0) deliver_step[t.level] = id;
+            if (t.kind == STEP_DELIVER && t.s >= 0 && t.k == 0) early_step0[t.s] = id;
         }
         step_beg.assign(D.steps.size() + 1, 0);
         for (const DistMsg& g : D.msgs) step_beg[g.step + 1]++;
@@ -212,7 +215,7 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
     // the main stream's work so far (the data it sends), and the main stream waits
     // for it when it receives.  Messages keep the plan order, so every peer pair
     // posts its matching sends and receives in the same order.
-    auto emit_step = [&](int32_t id) {
+    auto emit_step = [&](int32_t id, int send_ev = -1) {
         if (!real_comm || id < 0) return;
         Launch L {};
         L.kind = L_COMM;
@@ -264,9 +267,16 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         L.uoff = (int64_t)cbld.ctiles.size();
         add_tiles(unpack_d);
         L.ucount = (int32_t)((int64_t)cbld.ctiles.size() - L.uoff);
-        push_wait(2, push_record(0));
+        // sends wait for the data (default: everything the main stream has so far);
+        // receive-only steps post right away (their targets are never touched by this
+        // rank's compute before the step, and the comm stream joins the main stream at
+        // the start and end of every factorization)
+        if (nrecv < L.count) push_wait(2, send_ev >= 0 ? send_ev : push_record(0));
         N.sched.push_back(L);
         if (nrecv > 0) push_wait(0, push_record(2));
+    };
+    auto is_early_sender = [&](int32_t s) {
+        return real_comm && !D.early.empty() && D.early[s] && D.owner[s] == N.rank;
     };
     // CB rank `who` of split front s: per final panel slab, CB -= L21_k L21_k^T on
     // the column blocks it owns (K = slab width)
@@ -476,13 +486,32 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         }
         if (b_pending >= 0) push_wait(0, b_pending);
         if (cb_pending >= 0) push_wait(0, cb_pending);
+        // early-delivery children: the CB SYRK in column groups, an event after each
+        // (the group's comm sub-step waits for exactly that event)
+        for (int32_t s : large) {
+            if (!is_early_sender(s)) continue;
+            const int w = S.w(s), m = S.sn_m[s], mb = m - w;
+            for (int j0 = 0; j0 < mb; j0 += D.early_gw) {
+                GemmTask t {};
+                t.C = cb_pool + S.cb_off[s] + (int64_t)j0 * mb + j0;
+                t.A = panel_pool + S.panel_off[s] + w + j0;
+                t.ldc = mb;
+                t.lda = m;
+                t.M = mb - j0;
+                t.N = std::min(D.early_gw, mb - j0);
+                t.K = w;
+                const double fl = 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
+                push_gemm_launch(L_CB, lev, std::vector<GemmTask> {t}, w >= 256 ? 1 : 0, fl);
+                early_ev[s].push_back(push_record(0));
+            }
+        }
         // contribution-block SYRK, K = w; fronts with w >= 256 in their own launch
         for (int big = 1; big >= 0; --big) {
             std::vector<GemmTask> cbt;
             double fl = 0.0;
             for (int32_t s : large) {
                 const int w = S.w(s), m = S.sn_m[s], mb = m - w;
-                if (mb <= 0 || (w >= 256) != (big == 1) || is_split(s)) continue;
+                if (mb <= 0 || (w >= 256) != (big == 1) || is_split(s) || is_early_sender(s)) continue;
                 GemmTask t {};
                 const int kfrom = cb_by_slab(s) ? ((w - 1) / NBO) * NBO : 0;  // last slab only
                 t.C = cb_pool + S.cb_off[s];
@@ -498,6 +527,7 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             push_gemm_launch(L_CB, lev, cbt, big, fl);
         }
         };
+    if (real_comm) push_wait(2, push_record(0));  // previous factorization's reads are done
     for (int32_t lev = 0; lev < S.nlevels; ++lev) {
         if (N.owner.empty()) {
             emit_level(lev, by_level[lev]);
@@ -522,7 +552,14 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
                     emit_cb_rank(lev, s, who);
             }
         }
-        // contribution blocks that leave / enter this rank after this level
+        // contribution blocks that leave / enter this rank after this level: early
+        // children's column groups first, then the rest
+        for (int32_t c : by_level[lev]) {
+            if (D.early.empty() || !D.early[c] || early_step0[c] < 0) continue;
+            const int ng = (S.mb(c) + D.early_gw - 1) / D.early_gw;
+            for (int g = 0; g < ng; ++g)
+                emit_step(early_step0[c] + g, is_early_sender(c) ? early_ev[c][g] : -1);
+        }
         emit_step(deliver_step[lev]);
     }
     if (real_comm) push_wait(0, push_record(2));  // join the comm stream (its last sends)

@@ -32,7 +32,9 @@ enum LaunchKind : int32_t {
 //   STEP_SLAB(s,k)  split front s: the owner sends rows [w, m) of panel slab k (final)
 //                   to every CB rank
 //   STEP_DELIVER(l) after level l: every contribution block (column block) whose
-//                   producer is not the executing rank of the parent goes there
+//                   producer is not the executing rank of the parent goes there; one
+//                   sub-step (s = child, k = group) per column group of an early child
+//                   first, then one (s = -1) with the rest
 enum StepKind : int32_t { STEP_INIT = 0, STEP_SLAB = 1, STEP_DELIVER = 2 };
 struct DistStep {
     int32_t kind, level, s, k;
@@ -57,6 +59,10 @@ struct DistPlan {
     std::vector<int32_t> split;    // index into split_s / cb_rank, or -1
     std::vector<int32_t> split_s;
     std::vector<std::vector<int32_t>> cb_rank;  // per split front: rank of CB column block jb
+    // early delivery: a large, unsplit child whose parent runs on another rank has its
+    // CB SYRK in column groups of early_gw, each group sent as soon as it is computed
+    int early_gw = 4096;
+    std::vector<char> early;
     std::vector<DistStep> steps;
     std::vector<DistMsg> msgs;     // ascending step
     std::vector<double> work;      // estimated flops per rank

@@ -61,6 +61,8 @@ def _rank_main(rank, world, port, k, opts, out):
 
 @pytest.mark.parametrize("world,k,opts", [
     (2, 16, {}),
+    (2, 20, dict(dist_cbb=64, small_front_max=32)),
+    (3, 20, dict(dist_cbb=64, dist_early=0)),
     (4, 20, dict(panel_nb_outer=128, dist_cbb=64, small_front_max=32)),
     (3, 20, dict(panel_nb_outer=128, dist_cbb=128)),
     (4, 20, dict(panel_nb_outer=128, dist_cbb=64, dist_split=0)),
