@@ -80,7 +80,9 @@ typedef struct sc_options {
                                 stream (overlapping the panel chain); 0 (default): one K = w SYRK after the panel */
     int32_t dist_early;      /* multi-GPU: a large child whose parent runs on another rank computes its CB in
                                 4-block column groups and sends each group as soon as it is done (1, default) */
-    int32_t reserved[1];
+    int32_t chain_small;     /* 1: runs of >= 2 thin levels (<= 512 fronts, all small) go in one ticket-ordered
+                                launch instead of one launch per level (single device).  Default 0: measured
+                                slower on 1138_bus (3.06 vs 2.09 ms) */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

@@ -70,7 +70,7 @@ class Options(C.Structure):
         ("lookahead", C.c_int32), ("panel_variant", C.c_int32), ("inner_order", C.c_int32),
         ("asm_tile_min_m", C.c_int32), ("fuse_potrf", C.c_int32), ("dist_split", C.c_int32), ("dist_cbb", C.c_int32),
         ("ordering", C.c_int32), ("cb_slab", C.c_int32),
-        ("dist_early", C.c_int32), ("reserved", C.c_int32 * 1),
+        ("dist_early", C.c_int32), ("chain_small", C.c_int32),
     ]
 
 

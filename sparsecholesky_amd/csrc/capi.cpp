@@ -83,6 +83,7 @@ void sc_default_options(sc_options* opt) {
     opt->dist_split = 1;
     opt->dist_cbb = 1024;
     opt->dist_early = 1;
+    opt->chain_small = 0;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,

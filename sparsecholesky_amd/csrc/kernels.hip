@@ -29,11 +29,8 @@ __device__ __forceinline__ void report_fail(int32_t* info, int32_t col_internal)
 // deterministic, no atomics), right-looking partial Cholesky of the w pivots
 // (the CB is updated in place = the SYRK), write L panel and CB.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void front_small_kernel(DevPlan P, const int32_t* __restrict__ nodes,
-                                                           const double* __restrict__ Ax) {
-    extern __shared__ double F[];
-    __shared__ double s_piv;
-    const int s = nodes[blockIdx.x];
+__device__ __forceinline__ void small_front(const DevPlan& P, const int s, const double* __restrict__ Ax,
+                                            double* F, double& s_piv) {
     const int tid = threadIdx.x;
     const int c0 = P.sn_start[s];
     const int w = P.sn_start[s + 1] - c0;
@@ -94,6 +91,50 @@ __global__ __launch_bounds__(256) void front_small_kernel(DevPlan P, const int32
             if (ic >= jc) cb[idx] = F[(jc + w) * m + (ic + w)];
         }
     }
+}
+
+__global__ __launch_bounds__(256) void front_small_kernel(DevPlan P, const int32_t* __restrict__ nodes,
+                                                           const double* __restrict__ Ax) {
+    extern __shared__ double F[];
+    __shared__ double s_piv;
+    small_front(P, nodes[blockIdx.x], Ax, F, s_piv);
+}
+
+// Chains of thin levels of small fronts in ONE launch (1138_bus: 93 levels, about 22
+// us each as separate launches).  nodes[] is in level order, so children precede
+// parents.  A workgroup takes the next front by ticket (ticket order = the order
+// workgroups actually start) and waits only for its children in this launch; those
+// hold lower tickets, so they are running already and wait only on lower tickets
+// themselves: no deadlock whatever the dispatch order or residency.  The wait is
+// bounded (chain_err set, no hang) as a safety net.
+__global__ __launch_bounds__(256) void front_chain_kernel(DevPlan P, const int32_t* __restrict__ nodes,
+                                                           const double* __restrict__ Ax, int32_t* ticket,
+                                                           int chain_id) {
+    extern __shared__ double F[];
+    __shared__ double s_piv;
+    __shared__ int my;
+    if (threadIdx.x == 0) my = atomicAdd(ticket, 1);
+    __syncthreads();
+    const int s = nodes[my];
+    if (threadIdx.x == 0) {
+        for (int ci = P.child_ptr[s]; ci < P.child_ptr[s + 1]; ++ci) {
+            const int c = P.child_list[ci];
+            if (P.chain_of[c] != chain_id) continue;  // produced by an earlier launch
+            int spins = 0;
+            while (__hip_atomic_load(P.chain_done + c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > (1 << 24)) {
+                    atomicOr(P.chain_err, 1);
+                    break;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    small_front(P, s, Ax, F, s_piv);
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(P.chain_done + s, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------
@@ -795,6 +836,14 @@ hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count,
     if (count <= 0) return hipSuccess;
     size_t lds = (size_t)maxm * maxm * sizeof(double);
     hipLaunchKernelGGL(front_small_kernel, dim3(count), dim3(256), lds, st, P, nodes, Ax);
+    return hipGetLastError();
+}
+
+hipError_t launch_front_chain(const DevPlan& P, const int32_t* nodes, int count, int maxm, const double* Ax,
+                              int32_t* ticket, int chain_id, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    size_t lds = (size_t)maxm * maxm * sizeof(double);
+    hipLaunchKernelGGL(front_chain_kernel, dim3(count), dim3(256), lds, st, P, nodes, Ax, ticket, chain_id);
     return hipGetLastError();
 }
 

@@ -44,6 +44,9 @@ struct DevPlan {
     double* cb_pool;
     int32_t* info;              // min failing internal column + 1
     int32_t* blk_cnt;           // ns: arrival tickets of the fused POTRF+TRSM (panel variant 3)
+    const int32_t* chain_of;    // ns: chain launch computing the front (-1: none)
+    int32_t* chain_done;        // ns: front finished in this factorization (chain launches)
+    int32_t* chain_err;         // a chain wait timed out (never expected)
 };
 
 // One lower-trapezoid SYRK update: C[i,j] -= sum_k A[i,k] A[j,k], j < N, j <= i < M.
@@ -93,6 +96,9 @@ hipError_t launch_permute(double* dst, const double* src, const int32_t* perm, i
 
 hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count, int maxm, const double* Ax,
                               hipStream_t st);
+// runs of thin small-front levels as one ticket-ordered launch; ticket: zeroed per factorization
+hipError_t launch_front_chain(const DevPlan& P, const int32_t* nodes, int count, int maxm, const double* Ax,
+                              int32_t* ticket, int chain_id, hipStream_t st);
 // tiled: tasks are (front, (row tile << 16) | 16-column block) for the write-once
 // tile kernel (fronts with m >= ASM_TILE_MIN_M), else (front, column block)
 hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count, const double* Ax,

@@ -528,7 +528,38 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         }
         };
     if (real_comm) push_wait(2, push_record(0));  // previous factorization's reads are done
+    // single device: runs of >= 2 thin levels of small fronts -> one ticket-ordered launch
+    std::vector<int32_t>& chain_of = N.chain_of;
+    chain_of.assign((size_t)S.ns, -1);
+    auto thin = [&](int32_t lev) {
+        if (by_level[lev].empty() || by_level[lev].size() > 512) return false;
+        for (int32_t s : by_level[lev])
+            if (S.fclass[s] != FRONT_SMALL) return false;
+        return true;
+    };
     for (int32_t lev = 0; lev < S.nlevels; ++lev) {
+        if (N.owner.empty() && S.opt.chain_small && lev + 1 < S.nlevels && thin(lev) && thin(lev + 1)) {
+            int32_t l2 = lev;
+            while (l2 + 1 < S.nlevels && thin(l2 + 1)) ++l2;
+            Launch L {};
+            L.kind = L_SMALL;
+            L.big = 1;
+            L.level = lev;
+            L.off = (int64_t)small.size();
+            int mx = 1;
+            for (int32_t l = lev; l <= l2; ++l)
+                for (int32_t s : by_level[l]) {
+                    small.push_back(s);
+                    chain_of[s] = N.n_chains;
+                    mx = std::max(mx, (int)S.sn_m[s]);
+                }
+            L.count = (int32_t)((int64_t)small.size() - L.off);
+            L.maxm = bucket_of(mx);
+            L.step = N.n_chains++;
+            N.sched.push_back(L);
+            lev = l2;
+            continue;
+        }
         if (N.owner.empty()) {
             emit_level(lev, by_level[lev]);
             continue;
@@ -691,6 +722,18 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
         for (size_t q = 0; q < cbld.copies.size(); ++q) cbld.copies[q].b = N.staging + cbld.copy_slot[q];
     }
     if ((rc = upload(N, cbld.copies, N.d_copy)) || (rc = upload(N, cbld.ctiles, N.d_ctiles))) return fail(rc);
+    {
+        const int32_t* d_chain_of = nullptr;
+        int32_t* tmp = nullptr;
+        if ((rc = upload(N, N.chain_of, tmp))) return fail(rc);
+        d_chain_of = tmp;
+        if ((rc = dalloc(N, sizeof(int32_t) * ((size_t)N.n_chains + ns + 1), p))) return fail(rc);
+        N.d_chain_state = (int32_t*)p;
+        P.chain_of = d_chain_of;
+        P.chain_done = N.d_chain_state + N.n_chains;
+        P.chain_err = N.d_chain_state + N.n_chains + ns;
+        HIP_TRY(hipMemset(p, 0, sizeof(int32_t) * ((size_t)N.n_chains + ns + 1)));
+    }
     N.stamp_of.assign(N.sched.size(), -1);
     int nstamp = 0;
     for (size_t i = 0; i < N.sched.size(); ++i)
@@ -724,6 +767,9 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
         case L_WAIT:
             return hipStreamWaitEvent(st, N.sync_ev[L.count], 0);
         case L_SMALL:
+            if (L.big)
+                return launch_front_chain(N.P, N.d_small + L.off, L.count, L.maxm, d_Ax, N.d_chain_state + L.step,
+                                          L.step, N.stream);
             return launch_front_small(N.P, N.d_small + L.off, L.count, L.maxm, d_Ax, N.stream);
         case L_ASM:
             return launch_assemble_large(N.P, N.d_asm + L.off, L.count, d_Ax, N.stream, L.big != 0);
@@ -751,6 +797,8 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
 
 static int64_t enqueue_all(Numeric& N, const double* d_Ax, int prof) {
     HIP_TRY(hipMemsetAsync(N.P.info, 0x7f, sizeof(int32_t), N.stream));
+    if (N.n_chains > 0)
+        HIP_TRY(hipMemsetAsync(N.d_chain_state, 0, sizeof(int32_t) * ((size_t)N.n_chains + N.S->ns + 1), N.stream));
     for (size_t i = 0; i < N.sched.size(); ++i) {
         const Launch& L = N.sched[i];
         const bool timed = prof == 1 && L.kind < L_RECORD;
@@ -841,6 +889,14 @@ int64_t numeric_status(Numeric& N) {
     if (N.stream3) HIP_TRY(hipStreamSynchronize(N.stream3));
     int32_t info = 0;
     HIP_TRY(hipMemcpy(&info, N.P.info, sizeof(info), hipMemcpyDeviceToHost));
+    if (N.n_chains > 0) {
+        int32_t cerr = 0;
+        HIP_TRY(hipMemcpy(&cerr, N.P.chain_err, sizeof(cerr), hipMemcpyDeviceToHost));
+        if (cerr) {
+            N.err = "small-front chain launch: a dependency wait timed out";
+            return SC_ERR_HIP;
+        }
+    }
     if (info == 0x7f7f7f7f || info <= 0)
         N.status = 0;
     else

@@ -118,6 +118,8 @@ struct Numeric {
     int4* d_trsm = nullptr;
     GemmTask* d_gemm = nullptr;
     int2* d_tiles = nullptr;
+    int32_t* d_chain_state = nullptr;  // tickets[n_chains], done[ns], err: zeroed per factorization
+    int32_t n_chains = 0;
     double* d_Ax_owned = nullptr;
     const double* last_Ax = nullptr;
     bool factored = false;
@@ -143,6 +145,7 @@ struct Numeric {
     // pools, no transfers) to validate the partition on one device.
     int rank = 0, nranks = 1, virt_ranks = 0;
     std::vector<int32_t> owner;
+    std::vector<int32_t> chain_of;  // supernode -> small-front chain launch, -1 = none
     DistPlan D;
     std::vector<Msg> msgs;
     Copy2D* d_copy = nullptr;     // pack / unpack descriptors

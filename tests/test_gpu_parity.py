@@ -229,6 +229,29 @@ def test_nd_ordering_factor_and_solve(gpu, mtx, case):
     assert _backward_error(A, x, b) < 1e-14
 
 
+@pytest.mark.parametrize("case", ["bcsstk01", "1138_bus", "random", "lap10nat"])
+def test_small_front_chain_launch(gpu, mtx, case):
+    # runs of thin small-front levels in one ticket-ordered launch: bitwise the same
+    # factor as one launch per level (same per-front arithmetic), and oracle parity
+    A = {"random": lambda: random_spd(700, 0.004, 13), "lap10nat": lambda: sc.laplacian3d(10, nd=False)}.get(
+        case, lambda: mtx(case))()
+    Ls = []
+    for chain in (1, 0):
+        r = sc.chol(A, chain_small=chain)
+        assert r.has_value(), r.error()
+        Ls.append(r.value())
+    assert np.array_equal(Ls[0].x, Ls[1].x)
+    st, Lp, Li, Lx = oracle.chol(A)
+    assert np.array_equal(Ls[0].p, Lp) and np.array_equal(Ls[0].i, Li)
+    assert rel_fro(Ls[0].x, Lx) < TOL
+    # refactor through the same handle (tickets and done flags reset per factorization)
+    num = sc.Numeric(sc.Symbolic(A))
+    for _ in range(3):
+        assert num.factor(A.x) == 0
+    _, L3 = num.export()
+    assert np.array_equal(L3.x, Ls[0].x)
+
+
 def test_solve_device_and_residual_lap32(gpu):
     # size-independent property at a larger size: backward-stable solve residual
     torch = pytest.importorskip("torch")
