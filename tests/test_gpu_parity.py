@@ -245,7 +245,7 @@ def test_small_front_chain_launch(gpu, mtx, case):
     assert np.array_equal(Ls[0].p, Lp) and np.array_equal(Ls[0].i, Li)
     assert rel_fro(Ls[0].x, Lx) < TOL
     # refactor through the same handle (tickets and done flags reset per factorization)
-    num = sc.Numeric(sc.Symbolic(A))
+    num = sc.Numeric(sc.Symbolic(A, chain_small=1))
     for _ in range(3):
         assert num.factor(A.x) == 0
     _, L3 = num.export()
