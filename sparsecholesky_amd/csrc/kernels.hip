@@ -894,6 +894,11 @@ static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int b
                           hipStream_t st) {
     constexpr size_t kHalfLds = 80 * 1024;
     const bool one_per_cu = lds_mode == 1;
+    if (lds_mode == 3 && !FUSE && bt == 128) {  // BK = 32: twice the LDS, half the barriers
+        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, false, 32>), dim3(n), dim3(512), 0, st, tasks, tiles,
+                           info);
+        return;
+    }
     if (lds_mode == 2 && !FUSE) {  // BK = 8: half the LDS per workgroup
         if (bt == 128)
             hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, false, 8>), dim3(n), dim3(512), 0, st, tasks, tiles,

@@ -1341,10 +1341,13 @@ int64_t debug_bench(int which, int M, int K, int reps, int arg, double* tflops) 
             (void)hipMalloc(&bl, tiles.size() * sizeof(int2));
             (void)hipMemcpy(bt, &t, sizeof(t), hipMemcpyHostToDevice);
             (void)hipMemcpy(bl, tiles.data(), tiles.size() * sizeof(int2), hipMemcpyHostToDevice);
-            (void)launch_syrk((GemmTask*)bt, (int2*)bl, (int)tiles.size(), tb, 1, nullptr);
+            // which 6 / 7: BK = 8 / 32 instances (lds_mode 2 / 3)
+            const int lm = which == 6 ? 2 : which == 7 ? 3 : 0;
+            (void)launch_syrk((GemmTask*)bt, (int2*)bl, (int)tiles.size(), tb, 1, nullptr, lm);
             (void)hipDeviceSynchronize();
             (void)hipEventRecord(e0, nullptr);
-            for (int r = 0; r < reps; ++r) (void)launch_syrk((GemmTask*)bt, (int2*)bl, (int)tiles.size(), tb, 1, nullptr);
+            for (int r = 0; r < reps; ++r)
+                (void)launch_syrk((GemmTask*)bt, (int2*)bl, (int)tiles.size(), tb, 1, nullptr, lm);
             (void)hipEventRecord(e1, nullptr);
             flops = (double)M * (M + 1.0) * K * reps;
         }
