@@ -156,6 +156,12 @@ int64_t sc_numeric_status(sc_numeric* num);
 /* Export L in the reference CSC layout (chol() output, chol.hpp:749-863):
  * Lp[n+1], Li[nnz_L], Lx[nnz_L]; any of the three may be NULL. */
 int64_t sc_export_L(sc_numeric* num, int64_t* Lp, int32_t* Li, double* Lx);
+/* Columns [j0, j1) of L straight from the supernodal panels (no pattern pass; for
+ * factors too large for sc_export_L): column j holds its front's rows from j down
+ * (row indices in the same numbering as Lp/Li, relaxed zeros included), values
+ * in rx.  cp[j1-j0+1] offsets; ri / rx may be NULL to query the count.  Returns
+ * the entry count (>= 0) or an error.  Single-device handles only. */
+int64_t sc_export_L_cols(sc_numeric* num, int64_t j0, int64_t j1, int64_t* cp, int32_t* ri, double* rx);
 /* Device pointer of the library stream (hipStream_t) for event timing. */
 void* sc_numeric_stream(sc_numeric* num);
 /* Per-phase timing of the last factorization, milliseconds (HIP events):

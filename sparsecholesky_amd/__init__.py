@@ -112,6 +112,7 @@ _SIGS = [
     ("sc_factor_device", _I64, [_P, _P, _I32]),
     ("sc_numeric_status", _I64, [_P]),
     ("sc_export_L", _I64, [_P, _P, _P, _P]),
+    ("sc_export_L_cols", _I64, [_P, _I64, _I64, _P, _P, _P]),
     ("sc_numeric_stream", _P, [_P]),
     ("sc_numeric_set_profile", _I64, [_P, _I32]),
     ("sc_numeric_timing", _I64, [_P, _P, _I32]),
@@ -602,6 +603,16 @@ class Numeric:
         Lx = np.zeros(max(nz, 1), dtype=np.float64)
         st = _check(lib().sc_export_L(self.h, _ptr(Lp), _ptr(Li), _ptr(Lx)), "export_L")
         return st, csc_matrix(n, n, Lp, Li[:nz], Lx[:nz], sym.none)
+
+    def export_cols(self, j0: int, j1: int) -> tuple:
+        """Columns [j0, j1) of L from the panels: (cp, ri, rx), column j's rows
+        ri[cp[j-j0]:cp[j-j0+1]] (its front's rows from j down, relaxed zeros included)."""
+        cp = np.zeros(j1 - j0 + 1, dtype=np.int64)
+        tot = _check(lib().sc_export_L_cols(self.h, j0, j1, _ptr(cp), None, None), "export_cols")
+        ri = np.zeros(max(tot, 1), dtype=np.int32)
+        rx = np.zeros(max(tot, 1), dtype=np.float64)
+        _check(lib().sc_export_L_cols(self.h, j0, j1, _ptr(cp), _ptr(ri), _ptr(rx)), "export_cols")
+        return cp, ri[:tot], rx[:tot]
 
     def solve(self, b: np.ndarray) -> np.ndarray:
         """x = A^{-1} b on the GPU (host vectors in / out)."""

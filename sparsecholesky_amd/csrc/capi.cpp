@@ -246,6 +246,17 @@ int64_t sc_export_L(sc_numeric* num, int64_t* Lp, int32_t* Li, double* Lx) {
     }
 }
 
+int64_t sc_export_L_cols(sc_numeric* num, int64_t j0, int64_t j1, int64_t* cp, int32_t* ri, double* rx) {
+    if (!num || !num->N || !cp) return SC_ERR_ARG;
+    try {
+        const int64_t rc = sc::numeric_export_cols(*num->N, j0, j1, cp, ri, rx);
+        if (rc < 0) g_last_error = num->N->err;
+        return rc;
+    } catch (const std::bad_alloc&) {
+        return SC_ERR_NOMEM;
+    }
+}
+
 void* sc_numeric_stream(sc_numeric* num) { return (num && num->N) ? (void*)num->N->stream : nullptr; }
 
 int64_t sc_numeric_set_profile(sc_numeric* num, int32_t on) {

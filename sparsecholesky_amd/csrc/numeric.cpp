@@ -1025,6 +1025,43 @@ int64_t numeric_export(Numeric& N, int64_t* Lp, int32_t* Li, double* Lx) {
     return st;
 }
 
+int64_t numeric_export_cols(Numeric& N, int64_t j0, int64_t j1, int64_t* cp, int32_t* ri, double* rx) {
+    if (!N.factored) return SC_ERR_STATE;
+    if (!N.owner.empty() && N.virt_ranks <= 1) {
+        N.err = "export_cols needs the whole factor on one device";
+        return SC_ERR_NOTIMPL;
+    }
+    const int64_t st = numeric_status(N);
+    if (st < 0) return st;
+    const Symbolic& S = *N.S;
+    if (j0 < 0 || j1 < j0 || j1 > S.n || !cp) return SC_ERR_ARG;
+    HIP_TRY(hipSetDevice(N.device));
+    std::vector<double> buf;  // panel of the last supernode touched
+    int32_t cached = -1;
+    int64_t tot = 0;
+    cp[0] = 0;
+    for (int64_t j = j0; j < j1; ++j) {
+        const int32_t c = S.ipost[j], s = S.sn_of[c];
+        const int64_t m = S.sn_m[s], off = c - S.sn_start[s];
+        if (ri) {
+            if (rx && s != cached) {
+                buf.resize((size_t)(m * S.w(s)));
+                HIP_TRY(hipMemcpy(buf.data(), N.P.panel_pool + S.panel_off[s], buf.size() * sizeof(double),
+                                  hipMemcpyDeviceToHost));
+                cached = s;
+            }
+            const int32_t* rows = S.rows.data() + S.rows_ptr[s];
+            for (int64_t t = off; t < m; ++t) {
+                ri[tot + t - off] = S.post[rows[t]];
+                if (rx) rx[tot + t - off] = buf[(size_t)(off * m + t)];
+            }
+        }
+        tot += m - off;
+        cp[j - j0 + 1] = tot;
+    }
+    return tot;
+}
+
 // ---------------- triangular solves ----------------
 // A = P^T L L^T P (P = etree postorder): c = P b; L y = c (levels up); L^T x = y
 // (levels down); x = P^T c.  Per level and 64-column step: diagonal solves of every

@@ -186,6 +186,10 @@ int64_t numeric_create(const Symbolic& S, int device, Numeric*& out, std::string
 int64_t numeric_factor(Numeric& N, const double* d_Ax, bool sync);
 int64_t numeric_status(Numeric& N);
 int64_t numeric_export(Numeric& N, int64_t* Lp, int32_t* Li, double* Lx);
+// Natural columns [j0, j1) in front-row form (count only when ri == NULL): column j
+// holds the rows of its supernode's front from its own position down (natural
+// numbering, front order; relaxed zeros included) with their values.  cp[j1-j0+1].
+int64_t numeric_export_cols(Numeric& N, int64_t j0, int64_t j1, int64_t* cp, int32_t* ri, double* rx);
 int64_t numeric_timing(Numeric& N, double* t, int nt);
 int64_t numeric_level_times(Numeric& N, double* ms, int nl);
 int64_t numeric_launch_trace(Numeric& N, int32_t* kind, int32_t* level, int32_t* strm, double* ms, double* flops,

@@ -272,6 +272,49 @@ def test_solve_device_and_residual_lap32(gpu):
     assert np.linalg.norm(x2 - x) / np.linalg.norm(x) < 1e-13
 
 
+def _closed_block_start(A, J, lo):
+    """Smallest a >= lo with no entry of A in a row < a in columns [a, a + J): no fill
+    path then reaches an earlier column, so L[a:a+J, a:a+J] = chol(A[a:a+J, a:a+J])."""
+    n = A.size()
+    rmin = A.i[A.p[:-1]]  # first (smallest) row of each upper column
+    for a in np.flatnonzero(rmin[lo:] == np.arange(lo, n)) + lo:
+        if a + J <= n and rmin[a:a + J].min() >= a:
+            return int(a)
+    pytest.fail("no closed block")
+
+
+def test_lap128_closed_blocks_parity_and_solve(gpu):
+    # C4 (SURVEY 8c): the whole 128^3 factor is beyond the oracle (~8 h of flops), so
+    # parity is checked on closed principal blocks (the leading one and one past n/2:
+    # J x J blocks of the GPU's factor of the full matrix vs the oracle's chol of the
+    # block, rel-Fro < 1e-12), then the normwise backward error of a GPU solve.
+    import scipy.sparse as sp
+    from scipy.sparse.linalg import norm as spnorm
+
+    A = sc.laplacian3d(128)
+    n = A.size()
+    num = sc.Numeric(sc.Symbolic(A))
+    assert num.factor(A.x) == 0
+    J = 32768
+    for a in (0, _closed_block_start(A, J, n // 2)):
+        b = a + J
+        cp, ri, rx = num.export_cols(a, b)
+        col = np.repeat(np.arange(J), np.diff(cp))
+        keep = (ri >= a) & (ri < b)
+        G = sp.csc_matrix((rx[keep], (ri[keep] - a, col[keep])), shape=(J, J))
+        q0, q1 = int(A.p[a]), int(A.p[b])
+        blk = sc.csc_matrix(J, J, A.p[a:b + 1] - q0, A.i[q0:q1] - a, A.x[q0:q1])
+        st, Lp, Li, Lx = oracle.chol(blk)
+        assert st == 0
+        O = sp.csc_matrix((Lx, Li, Lp), shape=(J, J))
+        err = spnorm(G - O) / spnorm(O)
+        assert err < TOL, (a, err)
+    rng = np.random.default_rng(3)
+    bvec = rng.standard_normal(n)
+    x = num.solve(bvec)
+    assert _backward_error(A, x, bvec) < 1e-14
+
+
 def test_solve_after_failed_factor(gpu):
     A = sc.laplacian3d(6)
     A.x[A.p[5]:A.p[6]][-1] = -10.0  # diagonal of column 5 (last entry of an upper column)
