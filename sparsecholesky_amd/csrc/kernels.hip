@@ -1125,6 +1125,65 @@ __global__ __launch_bounds__(SOLVE_ROWS) void solve_gemv_kernel(SolvePlan P, con
     }
 }
 
+// Fused forward step (one launch per 64-column step instead of two): every GEMV
+// workgroup of block (s, k0) solves L11 y = c_blk itself from the 64 x 64 block
+// (32 KB, L2-resident across the step's workgroups) and applies its rows.  The
+// block's writer (t.w = 1) stores y to P.y, not to c, which the step's other
+// workgroups still read.  r0 < 0: a block with no rows below (diagonal only).
+__global__ __launch_bounds__(SOLVE_ROWS) void solve_fwd_kernel(SolvePlan P, const int4* __restrict__ tasks) {
+    __shared__ double Lb[PNB * (PNB + 1)];  // Lb[j * (PNB + 1) + i] = L(k0 + i, k0 + j)
+    __shared__ double vb[PNB];
+    const int4 t = tasks[blockIdx.x];
+    const int s = t.x, k0 = t.y, r0 = t.z;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int c0 = P.sn_start[s];
+    const int w = P.sn_start[s + 1] - c0;
+    const int m = P.sn_m[s];
+    const int nb = min(PNB, w - k0);
+    const double* __restrict__ pan = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m;
+#pragma unroll
+    for (int q = 0; q < PNB * PNB / SOLVE_ROWS; ++q) {
+        const int e = tid + SOLVE_ROWS * q, j = e >> 6, i = e & 63;
+        Lb[j * (PNB + 1) + i] = (i < nb && j < nb) ? pan[(int64_t)j * m + k0 + i] : 0.0;
+    }
+    __syncthreads();
+    if (tid < 64) {
+        double r[PNB];
+#pragma unroll
+        for (int j = 0; j < PNB; ++j) r[j] = Lb[j * (PNB + 1) + lane];
+        const double d = lane < nb ? 1.0 / Lb[lane * (PNB + 1) + lane] : 0.0;
+        double v = lane < nb ? P.c[c0 + k0 + lane] : 0.0;
+#pragma unroll
+        for (int j = 0; j < PNB; ++j) {  // y_j = v_j / L_jj; v_i -= L_ij y_j (i > j)
+            const double yj = readlane_f64(v, j) * readlane_f64(d, j);
+            v = lane == j ? yj : (lane > j ? v - r[j] * yj : v);
+        }
+        vb[lane] = v;
+        if (t.w && lane < nb) P.y[c0 + k0 + lane] = v;
+    }
+    __syncthreads();
+    if (r0 < 0) return;
+    const int32_t* __restrict__ rows = P.rows + P.rows_ptr[s];
+    const int r = r0 + tid;
+    const bool live = r < m;
+    double acc = 0.0;
+#pragma unroll
+    for (int jc = 0; jc < PNB; jc += 16) {
+        double v[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = (live && jc + q < nb) ? pan[(int64_t)(jc + q) * m + r] : 0.0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc += v[q] * vb[jc + q];
+    }
+    if (live) unsafeAtomicAdd(P.c + rows[r], -acc);
+}
+
+hipError_t launch_solve_fwd(const SolvePlan& P, const int4* tasks, int count, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(solve_fwd_kernel, dim3(count), dim3(SOLVE_ROWS), 0, st, P, tasks);
+    return hipGetLastError();
+}
+
 __global__ void permute_kernel(double* __restrict__ dst, const double* __restrict__ src,
                                const int32_t* __restrict__ perm, int64_t n, int scatter) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

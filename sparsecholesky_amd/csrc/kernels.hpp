@@ -81,6 +81,7 @@ struct SolvePlan {
     const int32_t* rows;      // front rows (internal numbering), first w = the pivots
     const double* panel_pool;
     double* c;                // right-hand side / solution, internal numbering
+    double* y;                // forward result (fused steps write here; copied to c after the sweep)
 };
 constexpr int SOLVE_ROWS = 256;  // front rows per GEMV workgroup
 // tasks (s, k0): the 64-column diagonal block of supernode s at column k0;
@@ -90,6 +91,8 @@ hipError_t launch_solve_diag(const SolvePlan& P, const int2* tasks, int count, b
 // c[rows[r]] -= L[r, blk] y_blk (fp64 atomics: fronts of a level share ancestors);
 // backward: c[blk] -= L[r, blk]^T x[rows[r]]
 hipError_t launch_solve_gemv(const SolvePlan& P, const int4* tasks, int count, bool backward, hipStream_t st);
+// fused forward step: tasks (s, k0, r0, writer); r0 < 0 = diagonal block only
+hipError_t launch_solve_fwd(const SolvePlan& P, const int4* tasks, int count, hipStream_t st);
 // c[i] = b[perm[i]] (gather) or x[perm[i]] = c[i] (scatter)
 hipError_t launch_permute(double* dst, const double* src, const int32_t* perm, int64_t n, bool scatter,
                           hipStream_t st);

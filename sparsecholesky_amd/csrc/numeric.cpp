@@ -1072,7 +1072,7 @@ static int64_t solve_build(Numeric& N) {
     std::vector<std::vector<int32_t>> by_level((size_t)S.nlevels);
     for (int32_t s = 0; s < S.ns; ++s) by_level[S.level[s]].push_back(s);
     std::vector<int2> diag;
-    std::vector<int4> gemv;
+    std::vector<int4> gemv, fwd;
     // internal index -> index in the caller's order (postorder, then the fill-reducing
     // permutation when one is in effect)
     std::vector<int32_t> solve_perm(S.post);
@@ -1085,26 +1085,35 @@ static int64_t solve_build(Numeric& N) {
             Numeric::SolveStep st {};
             st.doff = (int64_t)diag.size();
             st.goff = (int64_t)gemv.size();
+            st.foff = (int64_t)fwd.size();
             for (int32_t s : by_level[lev]) {
                 const int w = S.w(s), m = S.sn_m[s];
                 if (w <= k0) continue;
                 diag.push_back(make_int2(s, k0));
-                for (int r0 = std::min(w, k0 + PNB); r0 < m; r0 += SOLVE_ROWS) gemv.push_back(make_int4(s, k0, r0, 0));
+                const int rb = std::min(w, k0 + PNB);
+                if (rb >= m) fwd.push_back(make_int4(s, k0, -1, 1));
+                for (int r0 = rb; r0 < m; r0 += SOLVE_ROWS) {
+                    gemv.push_back(make_int4(s, k0, r0, 0));
+                    fwd.push_back(make_int4(s, k0, r0, r0 == rb ? 1 : 0));
+                }
             }
             st.dcount = (int32_t)((int64_t)diag.size() - st.doff);
             st.gcount = (int32_t)((int64_t)gemv.size() - st.goff);
+            st.fcount = (int32_t)((int64_t)fwd.size() - st.foff);
             N.solve_steps.push_back(st);
         }
     }
     int64_t rc;
     int32_t* d_rows = nullptr;
     int64_t* d_rows_ptr = nullptr;
-    if ((rc = upload(N, diag, N.d_sdiag)) || (rc = upload(N, gemv, N.d_sgemv)) || (rc = upload(N, S.rows, d_rows)) ||
+    if ((rc = upload(N, diag, N.d_sdiag)) || (rc = upload(N, gemv, N.d_sgemv)) || (rc = upload(N, fwd, N.d_sfwd)) ||
+        (rc = upload(N, S.rows, d_rows)) ||
         (rc = upload(N, S.rows_ptr, d_rows_ptr)) || (rc = upload(N, solve_perm, N.d_post)))
         return rc;
     void* p = nullptr;
-    if ((rc = dalloc(N, (size_t)std::max<int64_t>(S.n, 1) * 2 * sizeof(double), p))) return rc;
+    if ((rc = dalloc(N, (size_t)std::max<int64_t>(S.n, 1) * 3 * sizeof(double), p))) return rc;
     N.d_sbuf = (double*)p;
+    N.SP.y = N.d_sbuf + 2 * S.n;  // forward result of the fused steps
     N.SP.sn_start = N.P.sn_start;
     N.SP.sn_m = N.P.sn_m;
     N.SP.panel_off = N.P.panel_off;
@@ -1137,11 +1146,13 @@ int64_t numeric_solve_device(Numeric& N, const double* d_b, double* d_x) {
         N.solve_graph = nullptr;
         HIP_TRY(hipStreamBeginCapture(s0, hipStreamCaptureModeThreadLocal));
         hipError_t e = launch_permute(N.SP.c, d_b, N.d_post, n, false, s0);
+        // forward: one fused launch per step (y to SP.y), then y -> c
         for (size_t i = 0; e == hipSuccess && i < N.solve_steps.size(); ++i) {
             const Numeric::SolveStep& t = N.solve_steps[i];
-            e = launch_solve_diag(N.SP, N.d_sdiag + t.doff, t.dcount, false, s0);
-            if (e == hipSuccess) e = launch_solve_gemv(N.SP, N.d_sgemv + t.goff, t.gcount, false, s0);
+            e = launch_solve_fwd(N.SP, N.d_sfwd + t.foff, t.fcount, s0);
         }
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(N.SP.c, N.SP.y, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s0);
         for (size_t i = N.solve_steps.size(); e == hipSuccess && i-- > 0;) {
             const Numeric::SolveStep& t = N.solve_steps[i];
             e = launch_solve_gemv(N.SP, N.d_sgemv + t.goff, t.gcount, true, s0);

@@ -161,14 +161,15 @@ struct Numeric {
 
     // triangular solves (built at the first solve)
     struct SolveStep {
-        int64_t doff, goff;
-        int32_t dcount, gcount;
+        int64_t doff, goff, foff;
+        int32_t dcount, gcount, fcount;
     };
     std::vector<SolveStep> solve_steps;  // forward order (levels up, k0 up)
     bool solve_ready = false;
     SolvePlan SP {};
     int2* d_sdiag = nullptr;
     int4* d_sgemv = nullptr;
+    int4* d_sfwd = nullptr;  // fused forward steps (s, k0, r0, writer)
     int32_t* d_post = nullptr;
     double* d_sbuf = nullptr;  // host-interface staging (b in, x out)
     hipGraph_t solve_graph = nullptr;  // both sweeps captured once per (b, x) pair
