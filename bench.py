@@ -95,7 +95,6 @@ def main():
     ap.add_argument("--relax-wmax", type=int, default=None)
     ap.add_argument("--nbo", type=int, default=None, help="panel outer block (rank-k update width)")
     ap.add_argument("--lookahead", type=int, default=None)
-    ap.add_argument("--panel-variant", type=int, default=None)
     ap.add_argument("--inner-order", type=int, default=None)
     ap.add_argument("--opt", action="append", default=[],
                     help="extra sc_options field, key=value (lists comma-separated), e.g. nrelax=4,16,48")
@@ -139,8 +138,6 @@ def main():
         kw["panel_nb_outer"] = args.nbo
     if args.lookahead is not None:
         kw["lookahead"] = args.lookahead
-    if args.panel_variant is not None:
-        kw["panel_variant"] = args.panel_variant
     if args.inner_order is not None:
         kw["inner_order"] = args.inner_order
     if args.tile is not None:
@@ -261,7 +258,7 @@ def main():
             "options": {"relax_wmax": symb.opt.relax_wmax, "panel_nb_outer": symb.opt.panel_nb_outer,
                         "small_front_max": symb.opt.small_front_max, "use_graph": symb.opt.use_graph,
                         "lookahead": symb.opt.lookahead, "syrk_tile": symb.opt.syrk_tile,
-                        "panel_variant": symb.opt.panel_variant, "inner_order": symb.opt.inner_order},
+                        "inner_order": symb.opt.inner_order},
         },
         "roofline": roof,
         "timing_s": {"generate": round(t_gen, 3), "analyze": round(t_an, 3), "numeric_create": round(t_alloc, 3)},

@@ -62,13 +62,10 @@ typedef struct sc_options {
     int32_t relax_wmax;      /* a child and its parent that are both wider than this are not amalgamated when
                                 the parent has other children (chains still merge; 0 = no limit; default 1) */
     int32_t syrk_tile;       /* 0 = auto (128x128/8 waves for wide, deep updates, else 64x64/4 waves); 64; 128 */
-    int32_t lookahead;       /* 0: none; 1: trailing panel updates on a 2nd stream; 2: same, at most one of their
-                                workgroups per CU; 3: same, 2nd stream CU-masked to 7/8 */
-    int32_t panel_variant;   /* large-front POTRF/TRSM kernels: 1 pipelined substitution, 2 inverse + MFMA (0 = default) */
+    int32_t lookahead;       /* 0: none; 1 (default): trailing panel updates on a 2nd stream, overlapping the
+                                next slab's POTRF/TRSM chain */
     int32_t inner_order;     /* updates inside a slab: 0 right-looking (K = 64), 1 recursive (K = 64..NBO/2) */
     int32_t asm_tile_min_m;  /* fronts with m >= this use the write-once tiled assembly (0 = default 8192) */
-    int32_t fuse_potrf;      /* 1: the update that completes a panel block also factors its diagonal block
-                                (default 0: measured slower, 625 vs 602 ms at 128^3) */
     int32_t dist_split;      /* multi-GPU: a shared front with a contribution block keeps its panel on one rank and
                                 has its contribution block computed by the other ranks of its group, slab-streamed
                                 (1, default); 0: every front on one rank */
@@ -76,13 +73,8 @@ typedef struct sc_options {
     int32_t ordering;        /* SC_ORDER_NATURAL (default: the given order, as the reference) or SC_ORDER_ND:
                                 factor P A P^T with a nested-dissection P (sc_symbolic_perm); L, the pattern
                                 and the statistics are then those of P A P^T, solves take and return A's order */
-    int32_t cb_slab;         /* 1: fronts with several slabs apply their CB update slab by slab on the lookahead
-                                stream (overlapping the panel chain); 0 (default): one K = w SYRK after the panel */
     int32_t dist_early;      /* multi-GPU: a large child whose parent runs on another rank computes its CB in
                                 4-block column groups and sends each group as soon as it is done (1, default) */
-    int32_t chain_small;     /* 1: runs of >= 2 thin levels (<= 512 fronts, all small) go in one ticket-ordered
-                                launch instead of one launch per level (single device).  Default 0: measured
-                                slower on 1138_bus (3.06 vs 2.09 ms) */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };
@@ -277,9 +269,8 @@ int64_t sc_debug_syrk(double* dC, int32_t ldc, const double* dA, int32_t lda, in
 /* Microbenchmarks: which=0 register-only fp64 MFMA probe (TFLOP/s; M blocks of
  * 4 waves, K iterations, arg accumulators); which=1/5 the SYRK kernel on an M x M
  * triangle with depth K, tile arg (64/128), with / without the XCD tile order
- * (TFLOP/s); which=2/3 the panel POTRF / TRSM kernel variant arg on an M x 64
- * front (microseconds per launch); which=4 max |variant 0 - variant 1| of the
- * POTRF + TRSM result on that front. */
+ * (TFLOP/s); which=2/3 the panel POTRF / TRSM kernel on an M x 64 front
+ * (microseconds per launch). */
 int64_t sc_debug_bench(int32_t which, int32_t M, int32_t K, int32_t reps, int32_t arg, double* tflops);
 int64_t sc_device_count(void);
 /* Message of the last failing call on this thread. */

@@ -76,14 +76,11 @@ void sc_default_options(sc_options* opt) {
     opt->relax_wmax = 1;
     opt->syrk_tile = 0;
     opt->lookahead = 1;
-    opt->panel_variant = 0;
     opt->inner_order = 1;
     opt->asm_tile_min_m = 0;
-    opt->fuse_potrf = 0;
     opt->dist_split = 1;
     opt->dist_cbb = 1024;
     opt->dist_early = 1;
-    opt->chain_small = 0;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,

@@ -100,43 +100,6 @@ __global__ __launch_bounds__(256) void front_small_kernel(DevPlan P, const int32
     small_front(P, nodes[blockIdx.x], Ax, F, s_piv);
 }
 
-// Chains of thin levels of small fronts in ONE launch (1138_bus: 93 levels, about 22
-// us each as separate launches).  nodes[] is in level order, so children precede
-// parents.  A workgroup takes the next front by ticket (ticket order = the order
-// workgroups actually start) and waits only for its children in this launch; those
-// hold lower tickets, so they are running already and wait only on lower tickets
-// themselves: no deadlock whatever the dispatch order or residency.  The wait is
-// bounded (chain_err set, no hang) as a safety net.
-__global__ __launch_bounds__(256) void front_chain_kernel(DevPlan P, const int32_t* __restrict__ nodes,
-                                                           const double* __restrict__ Ax, int32_t* ticket,
-                                                           int chain_id) {
-    extern __shared__ double F[];
-    __shared__ double s_piv;
-    __shared__ int my;
-    if (threadIdx.x == 0) my = atomicAdd(ticket, 1);
-    __syncthreads();
-    const int s = nodes[my];
-    if (threadIdx.x == 0) {
-        for (int ci = P.child_ptr[s]; ci < P.child_ptr[s + 1]; ++ci) {
-            const int c = P.child_list[ci];
-            if (P.chain_of[c] != chain_id) continue;  // produced by an earlier launch
-            int spins = 0;
-            while (__hip_atomic_load(P.chain_done + c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1 << 24)) {
-                    atomicOr(P.chain_err, 1);
-                    break;
-                }
-            }
-        }
-    }
-    __syncthreads();
-    small_front(P, s, Ax, F, s_piv);
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(P.chain_done + s, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // ---------------------------------------------------------------------------
 // Large fronts, assembly: one workgroup per (front, 64-column block).  Zeroes its
 // panel / CB columns, stores the A entries, then adds every child's CB entries
@@ -315,23 +278,6 @@ __device__ __forceinline__ void potrf_block_wave(double* blk, int64_t ld, int nb
     }
 }
 
-// ---------------------------------------------------------------------------
-// Large fronts, diagonal block POTRF (nb <= 64), one wave per front: lane i keeps
-// row i in registers; the pivot is broadcast with v_readlane, column j through
-// LDS; entries above the diagonal carry harmless garbage and are never stored.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void potrf_diag_kernel(DevPlan P, const int2* __restrict__ tasks) {
-    __shared__ double colj[PNB];
-    const int2 t = tasks[blockIdx.x];
-    const int s = t.x, k0 = t.y;
-    const int c0 = P.sn_start[s];
-    const int w = P.sn_start[s + 1] - c0;
-    const int m = P.sn_m[s];
-    const int nb = min(PNB, w - k0);
-    double* blk = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m + k0;
-    potrf_block_wave(blk, m, nb, threadIdx.x, colj, P.info, c0 + k0);
-}
-
 // Forward substitution steps of one row against L11 (column-major in LDS).
 template <int J>
 __device__ __forceinline__ void trsm_steps(double (&r)[PNB], const double* Lc, const double* invd, int nb) {
@@ -344,47 +290,6 @@ __device__ __forceinline__ void trsm_steps(double (&r)[PNB], const double* Lc, c
             for (int q = J + 1; q < PNB; ++q) r[q] = fma(-rj, Lc[J * LD + q], r[q]);
             trsm_steps<J + 1>(r, Lc, invd, nb);
         }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Large fronts, panel TRSM: X := X * L11^{-T} for rows below the diagonal block.
-// One lane per row (256 rows per workgroup), the row in registers; right-looking
-// substitution x_j *= 1/L(j,j), x_q -= x_j L(q,j) for q > j (independent FMAs).
-// L11 columns and the reciprocal diagonal are broadcast from LDS; no barriers
-// inside the solve.  tasks = (s, k0, r0): rows [r0, min(m, r0 + TRSM_ROWS)).
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void trsm_panel_kernel(DevPlan P, const int4* __restrict__ tasks) {
-    constexpr int LD = PNB + 2;
-    __shared__ double Lc[PNB * LD];  // Lc[j * LD + q] = L11(q, j), column-major
-    __shared__ double invd[PNB];
-    const int4 t = tasks[blockIdx.x];
-    const int s = t.x, k0 = t.y, r0 = t.z;
-    const int tid = threadIdx.x;
-    const int c0 = P.sn_start[s];
-    const int w = P.sn_start[s + 1] - c0;
-    const int m = P.sn_m[s];
-    const int nb = min(PNB, w - k0);
-    double* pan = P.panel_pool + P.panel_off[s];
-    const double* blk = pan + (int64_t)k0 * m + k0;
-    for (int idx = tid; idx < PNB * PNB; idx += 256) {
-        const int q = idx % PNB, j = idx / PNB;
-        const double v = (q < nb && j < nb && j <= q) ? blk[(int64_t)j * m + q] : 0.0;
-        Lc[j * LD + q] = v;
-        if (q == j) invd[j] = (j < nb) ? 1.0 / v : 0.0;
-    }
-    __syncthreads();
-    const int row = r0 + tid;
-    const bool live = row < m;
-    double* xs = pan + (int64_t)k0 * m + (live ? row : r0);
-    double r[PNB];
-#pragma unroll
-    for (int c = 0; c < PNB; ++c) r[c] = (live && c < nb) ? xs[(int64_t)c * m] : 0.0;
-    trsm_steps<0>(r, Lc, invd, nb);
-    if (live) {
-#pragma unroll
-        for (int c = 0; c < PNB; ++c)
-            if (c < nb) xs[(int64_t)c * m] = r[c];
     }
 }
 
@@ -443,50 +348,6 @@ __global__ __launch_bounds__(64) void potrf_diag_g_kernel(DevPlan P, const int2*
 #pragma unroll
     for (int c = 0; c < PNB; ++c)
         if (c <= lane) buf_st(r[c], rs, lane * 8, c * m * 8);
-}
-
-// Variant 2 (default), diagonal block: POTRF as above, then the same wave forms
-// W = inv(L11)^T by running the generated row solve on the identity rows (lane q
-// solves e_q L11^-T = column q of inv(L11)), and stores the strictly upper part of
-// W into the unused strictly upper triangle of the diagonal block:
-// blk[j*m + q] = inv(L11)(j, q), q < j.  diag(W) = 1 / diag(L11).
-__global__ __launch_bounds__(64) void potrf_inv_kernel(DevPlan P, const int2* __restrict__ tasks) {
-    __shared__ double C[2 * PNB];
-    __shared__ double2 S[TRSM64_STREAM / 2 + PNB / 2];  // + one dummy slot per lane
-    const int2 t = tasks[blockIdx.x];
-    const int s = t.x, k0 = t.y;
-    const int c0 = P.sn_start[s];
-    const int w = P.sn_start[s + 1] - c0;
-    const int m = P.sn_m[s];
-    const int nb = min(PNB, w - k0);
-    double* blk = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m + k0;
-    const int lane = threadIdx.x;
-    if (nb < PNB) {
-        potrf_block_wave(blk, m, nb, lane, C, P.info, c0 + k0);
-        return;
-    }
-    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(blk, (uint32_t)m * PNB * 8u);
-    double r[PNB];
-#pragma unroll
-    for (int c = 0; c < PNB; ++c) r[c] = buf_ld(rs, lane * 8, c * m * 8);
-    const int bad = potrf64_full(r, C, lane);
-    if (bad >= 0 && lane == 0) report_fail(P.info, c0 + k0 + bad);
-    // L11 operand stream (1/L(c,c), L(c+1..63, c)) for the inverse; lane q owns row q
-    // (branch-free: masked stores go out of buffer range / to a dummy LDS slot)
-    double* Sd = reinterpret_cast<double*>(S);
-    double diag = 0.0;
-#pragma unroll
-    for (int c = 0; c < PNB; ++c) {
-        buf_st(r[c], rs, c <= lane ? lane * 8 : BUF_DEAD, c * m * 8);
-        Sd[c < lane ? PNB * c - c * (c - 1) / 2 + (lane - c) : TRSM64_STREAM + lane] = r[c];
-        diag = (c == lane) ? r[c] : diag;
-    }
-    Sd[PNB * lane - lane * (lane - 1) / 2] = 1.0 / diag;
-#pragma unroll
-    for (int c = 0; c < PNB; ++c) r[c] = (c == lane) ? 1.0 : 0.0;
-    trsm64_full(r, S);  // r[i] = inv(L11)(i, lane), i >= lane
-#pragma unroll
-    for (int c = 0; c < PNB; ++c) buf_st(r[c], rs, c > lane ? lane * 8 : BUF_DEAD, c * m * 8);
 }
 
 // Partial last block (nb < 64) of the panel TRSM: template path, kept out of
@@ -566,144 +427,23 @@ __global__ __launch_bounds__(256) void trsm_panel_g_kernel(DevPlan P, const int4
     for (int c = 0; c < PNB; ++c) buf_st(r[c], rs, voff, c * m * 8);
 }
 
-// Variant 3: POTRF fused into the panel TRSM (one launch and one dependent-launch
-// gap fewer per 64-column block on the chain).  Every workgroup of the block
-// factors the 64 x 64 diagonal block itself (wave 0, registers) into the packed
-// LDS operand stream; the workgroups' A11 loads all precede their ticket on the
-// front's counter, so the last one to take a ticket stores L11 over A11 (and
-// resets the counter for the next block / factorization).  No waiting anywhere.
-__global__ __launch_bounds__(256) void trsm_fused_g_kernel(DevPlan P, const int4* __restrict__ tasks) {
-    __shared__ double2 S[TRSM64_STREAM / 2 + PNB / 2];  // + one dummy slot per lane
-    __shared__ double C[2 * PNB];
-    __shared__ double Ld[PNB];   // diag(L11)
-    __shared__ int last;
-    const int4 t = tasks[blockIdx.x];
-    const int s = t.x, k0 = t.y, r0 = t.z;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int c0 = P.sn_start[s];
-    const int w = P.sn_start[s + 1] - c0;
-    const int m = P.sn_m[s];
-    const int nb = min(PNB, w - k0);
-    double* pan = P.panel_pool + P.panel_off[s];
-    if (nb < PNB) return;  // partial blocks: potrf + trsm_partial_kernel
-    double* Sd = reinterpret_cast<double*>(S);
-    const __amdgpu_buffer_rsrc_t rb = buf_rsrc(pan + (int64_t)k0 * m + k0);
-    if (tid < 64) {
-        double r[PNB];
-#pragma unroll
-        for (int c = 0; c < PNB; ++c) r[c] = buf_ld(rb, lane * 8, c * m * 8);
-        const int bad = potrf64_full(r, C, lane);
-        if (bad >= 0 && lane == 0) report_fail(P.info, c0 + k0 + bad);
-        double diag = 0.0;
-#pragma unroll
-        for (int c = 0; c < PNB; ++c) {
-            Sd[c < lane ? PNB * c - c * (c - 1) / 2 + (lane - c) : TRSM64_STREAM + lane] = r[c];
-            diag = (c == lane) ? r[c] : diag;
-        }
-        Sd[PNB * lane - lane * (lane - 1) / 2] = 1.0 / diag;
-        Ld[lane] = diag;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        const int nwg = (m - (k0 + PNB) + TRSM_ROWS - 1) / TRSM_ROWS;
-        __threadfence();  // this workgroup's A11 reads precede its ticket
-        last = atomicAdd(P.blk_cnt + s, 1) == nwg - 1;
-        if (last) atomicExch(P.blk_cnt + s, 0);
-    }
-    __syncthreads();
-    if (last) {  // every workgroup has read A11: store L11 (lower, column-major, ld = m)
-        double* blk = pan + (int64_t)k0 * m + k0;
-        for (int e = tid; e < PNB * PNB; e += 256) {
-            const int j = e / PNB, q = e % PNB;
-            if (q > j) blk[(int64_t)j * m + q] = Sd[PNB * j - j * (j - 1) / 2 + (q - j)];
-            if (q == j) blk[(int64_t)j * m + q] = Ld[j];
-        }
-    }
-    const int row = r0 + tid;
-    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pan + (int64_t)k0 * m, (uint32_t)m * PNB * 8u);
-    const int voff = row < m ? row * 8 : BUF_DEAD;
-    double r[PNB];
-#pragma unroll
-    for (int c = 0; c < PNB; ++c) r[c] = buf_ld(rs, voff, c * m * 8);
-    trsm64_full(r, S);
-#pragma unroll
-    for (int c = 0; c < PNB; ++c) buf_st(r[c], rs, voff, c * m * 8);
-}
-
-// Variant 2 (default) panel TRSM: X := X W with W = inv(L11)^T from
-// potrf_inv_kernel, on fp64 MFMA (v_mfma_f64_16x16x4_f64).  Rows [r0, r0 + 64):
-// wave v owns rows r0 + 16v .. + 16 (A fragments = its 16 x 64 block of X in
-// registers), 4 column tiles of 16, k-blocks above the triangle skipped (40 MFMAs
-// per wave).  No dependent chain: the solve is one small GEMM per row block.
-__global__ __launch_bounds__(256) void trsm_panel_mfma_kernel(DevPlan P, const int4* __restrict__ tasks) {
-    __shared__ double dinv[PNB];  // 1 / L11(q, q) = W(q, q); the rest of W is read from L2
-    const int4 t = tasks[blockIdx.x];
-    const int s = t.x, k0 = t.y, r0 = t.z;
-    const int tid = threadIdx.x;
-    const int c0 = P.sn_start[s];
-    const int w = P.sn_start[s + 1] - c0;
-    const int m = P.sn_m[s];
-    const int nb = min(PNB, w - k0);
-    double* pan = P.panel_pool + P.panel_off[s];
-    if (nb < PNB) return;  // partial blocks: trsm_partial_kernel
-    const double* blk = pan + (int64_t)k0 * m + k0;
-    if (tid < PNB) dinv[tid] = 1.0 / blk[(int64_t)tid * m + tid];
-    __syncthreads();
-    const int lane = tid & 63;
-    const int i0 = r0 + 16 * (tid >> 6);
-    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pan + (int64_t)k0 * m, (uint32_t)m * PNB * 8u);
-    // A(i, k) = X(i0 + (lane & 15), 4 kk + (lane >> 4))
-    const int arow = i0 + (lane & 15);
-    const int avoff = arow < m ? arow * 8 + (lane >> 4) * m * 8 : BUF_DEAD;
-    double a[16];
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) a[kk] = buf_ld(rs, avoff, 4 * kk * m * 8);
-    double4_t acc[4];
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt) acc[jt] = (double4_t){0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk)
-#pragma unroll
-        for (int jt = kk / 4; jt < 4; ++jt) {
-            // B(k, j) = W(q, j), q = 4 kk + (lane >> 4), j = 16 jt + (lane & 15):
-            // inv(L11)(j, q) in the upper triangle for q < j, 1/L(q,q) on the diagonal
-            const int q = 4 * kk + (lane >> 4), j = 16 * jt + (lane & 15);
-            const double v = blk[(int64_t)j * m + q];
-            const double b = (q < j) ? v : ((q == j) ? dinv[q] : 0.0);
-            acc[jt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kk], b, acc[jt], 0, 0, 0);
-        }
-    // D(row, col): col = lane & 15, row = (lane >> 4) + 4 r
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int row = i0 + MFMA_F64_ROW(lane, r);
-        const int voff = row < m ? row * 8 + (lane & 15) * m * 8 : BUF_DEAD;
-#pragma unroll
-        for (int jt = 0; jt < 4; ++jt) buf_st(acc[jt][r], rs, voff, 16 * jt * m * 8);
-    }
-}
-
 // ---------------------------------------------------------------------------
 // fp64 MFMA SYRK on a lower trapezoid: C[i,j] -= sum_k A[i,k] * A[j,k] for
 // 0 <= j < N, j <= i < M.  BT x BT output tiles (ti >= tj) on WM x WN waves, each
 // wave (BT/WM) x (BT/WN) = RTM x RTN tiles of v_mfma_f64_16x16x4_f64.  A (M x K)
 // and the B operand (its first N rows) share one column-major array.  K is
 // staged through double-buffered LDS (register staging, BK = 16).
+// (BK = 8 and 32, and a 4-wave 128 x 128 instance, were measured slower on every
+// shape: DESIGN.md section 5.)
 // ---------------------------------------------------------------------------
-// FUSE: a task with potrf_col > 0 finishes the 64 x 64 diagonal block at the
-// top-left of its C (the next panel block, complete after this update): tile
-// (0, 0) keeps that quadrant in LDS instead of storing it, and one wave factors it
-// in registers (potrf64_full) and stores L11, so the block needs no POTRF launch.
-template <int BT, int WM, int WN, int TAG, bool FUSE = false, int BK = 16>
+template <int BT, int WM, int WN, int TAG>
 __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
-                                                                  const int2* __restrict__ tiles,
-                                                                  int32_t* __restrict__ info) {
+                                                                  const int2* __restrict__ tiles) {
     constexpr int NT = 64 * WM * WN;
-    // BK = 8 halves the LDS (36.9 KB at BT = 128) so that the panel chain's kernels
-    // still fit next to two resident lookahead workgroups on a CU
+    constexpr int BK = 16;
     constexpr int LDT = BT + 16;  // +128 B row pad: the two k-rows read by a half-wave hit disjoint banks
     constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
-    __shared__ double smem[2 * 2 * BK * LDT];  // A and B stages; after the K loop: the fused POTRF block
-    static_assert(!FUSE || 2 * 2 * BK * LDT >= PNB * PNB + 2 * PNB, "LDS for the fused POTRF");
+    __shared__ double smem[2 * 2 * BK * LDT];  // A and B stages
     double(*As)[BK * LDT] = reinterpret_cast<double(*)[BK * LDT]>(smem);
     double(*Bs)[BK * LDT] = reinterpret_cast<double(*)[BK * LDT]>(smem + 2 * BK * LDT);
 
@@ -805,27 +545,8 @@ __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask*
                 const int gj = col0 + wc * (BT / WN) + b * 16 + (lane & 15);
                 const bool live = gi < T.M && gi >= gj;
                 const int off = live ? (int)((gi + (int64_t)(gj - col0) * ldc) * 8) : BUF_DEAD;
-                if (FUSE && T.potrf_col > 0 && gi < PNB && gj < PNB) {
-                    if (live) smem[gj * PNB + gi] = buf_ld(rc, off, 0) - acc[a][b][r];  // tile (0, 0) only
-                } else {
-                    buf_st(buf_ld(rc, off, 0) - acc[a][b][r], rc, off, 0);
-                }
+                buf_st(buf_ld(rc, off, 0) - acc[a][b][r], rc, off, 0);
             }
-    if constexpr (FUSE) {
-        if (T.potrf_col > 0 && row0 == 0 && col0 == 0) {
-            __syncthreads();
-            if (wid == 0) {
-                double r[PNB];
-#pragma unroll
-                for (int c = 0; c < PNB; ++c) r[c] = (c <= lane) ? smem[c * PNB + lane] : 0.0;
-                const int bad = potrf64_full(r, smem + PNB * PNB, lane);
-                if (bad >= 0 && lane == 0) report_fail(info, T.potrf_col - 1 + bad);
-#pragma unroll
-                for (int c = 0; c < PNB; ++c)
-                    if (c <= lane) C[lane + (int64_t)c * ldc] = r[c];
-            }
-        }
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -839,14 +560,6 @@ hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count,
     return hipGetLastError();
 }
 
-hipError_t launch_front_chain(const DevPlan& P, const int32_t* nodes, int count, int maxm, const double* Ax,
-                              int32_t* ticket, int chain_id, hipStream_t st) {
-    if (count <= 0) return hipSuccess;
-    size_t lds = (size_t)maxm * maxm * sizeof(double);
-    hipLaunchKernelGGL(front_chain_kernel, dim3(count), dim3(256), lds, st, P, nodes, Ax, ticket, chain_id);
-    return hipGetLastError();
-}
-
 hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count, const double* Ax,
                                  hipStream_t st, bool tiled) {
     if (count <= 0) return hipSuccess;
@@ -857,81 +570,37 @@ hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count,
     return hipGetLastError();
 }
 
-hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hipStream_t st, int variant) {
+hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hipStream_t st) {
     if (count <= 0) return hipSuccess;
-    if (variant == 0)
-        hipLaunchKernelGGL(potrf_diag_kernel, dim3(count), dim3(64), 0, st, P, tasks);
-    else if (variant == 1 || variant == 3)  // 3: partial blocks / blocks with no rows below
-        hipLaunchKernelGGL(potrf_diag_g_kernel, dim3(count), dim3(64), 0, st, P, tasks);
-    else
-        hipLaunchKernelGGL(potrf_inv_kernel, dim3(count), dim3(64), 0, st, P, tasks);
+    hipLaunchKernelGGL(potrf_diag_g_kernel, dim3(count), dim3(64), 0, st, P, tasks);
     return hipGetLastError();
 }
 
-hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st, int variant,
-                             bool partial) {
+hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st, bool partial) {
     if (count <= 0) return hipSuccess;
-    if (partial && variant > 0)
-        hipLaunchKernelGGL(trsm_partial_kernel, dim3(count), dim3(256), 0, st, P, tasks, trsm_task_rows(variant));
-    else if (variant == 0)
-        hipLaunchKernelGGL(trsm_panel_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks);
-    else if (variant == 1)
-        hipLaunchKernelGGL(trsm_panel_g_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks);
-    else if (variant == 3)
-        hipLaunchKernelGGL(trsm_fused_g_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks);
+    if (partial)
+        hipLaunchKernelGGL(trsm_partial_kernel, dim3(count), dim3(256), 0, st, P, tasks, TRSM_ROWS);
     else
-        hipLaunchKernelGGL(trsm_panel_mfma_kernel, dim3(count), dim3(256), 0, st, P, tasks);
+        hipLaunchKernelGGL(trsm_panel_g_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks);
     return hipGetLastError();
 }
 
 // TAG only separates the launches in profiles: 0 = panel update, 1 = CB update.
 // bt = 64: 64x64 tiles on 4 waves (2x2); bt = 128: 128x128 tiles on 8 waves (2x4).
-// one_per_cu: reserve unused dynamic LDS so that at most one workgroup of this
-// launch sits on a CU (the overlapped lookahead GEMMs leave room for the panel
-// chain's kernels instead of filling every CU twice).
-template <int TAG, bool FUSE>
-static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int bt, int lds_mode, int32_t* info,
-                          hipStream_t st) {
-    constexpr size_t kHalfLds = 80 * 1024;
-    const bool one_per_cu = lds_mode == 1;
-    if (lds_mode == 3 && !FUSE && bt == 128) {  // BK = 32: twice the LDS, half the barriers
-        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, false, 32>), dim3(n), dim3(512), 0, st, tasks, tiles,
-                           info);
-        return;
-    }
-    if (lds_mode == 2 && !FUSE) {  // BK = 8: half the LDS per workgroup
-        if (bt == 128)
-            hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, false, 8>), dim3(n), dim3(512), 0, st, tasks, tiles,
-                               info);
-        else
-            hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG, false, 8>), dim3(n), dim3(256), 0, st, tasks, tiles,
-                               info);
-        return;
-    }
-    if (bt == SYRK_BT_LARGE_W4) {  // 128 x 128 on 4 waves of 64 x 64 (experimental)
-        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 2, TAG, FUSE>), dim3(n), dim3(256), 0, st, tasks, tiles, info);
-    } else if (bt == 128) {
-        constexpr size_t stat = 2 * 2 * 16 * (128 + 16) * sizeof(double);
-        const size_t dyn = one_per_cu ? kHalfLds + 1024 - stat : 0;
-        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, FUSE>), dim3(n), dim3(512), dyn, st, tasks, tiles,
-                           info);
-    } else {
-        constexpr size_t stat = 2 * 2 * 16 * (64 + 16) * sizeof(double);
-        const size_t dyn = one_per_cu ? kHalfLds + 1024 - stat : 0;
-        hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG, FUSE>), dim3(n), dim3(256), dyn, st, tasks, tiles,
-                           info);
-    }
+template <int TAG>
+static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int bt, hipStream_t st) {
+    if (bt == 128)
+        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG>), dim3(n), dim3(512), 0, st, tasks, tiles);
+    else
+        hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG>), dim3(n), dim3(256), 0, st, tasks, tiles);
 }
 
-hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
-                       int lds_mode, int32_t* fuse_info) {
+hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st) {
     if (total_tiles <= 0) return hipSuccess;
     if (tag)
-        launch_syrk_t<1, false>(tasks, tiles, total_tiles, bt, lds_mode, nullptr, st);
-    else if (fuse_info)
-        launch_syrk_t<0, true>(tasks, tiles, total_tiles, bt, lds_mode, fuse_info, st);
+        launch_syrk_t<1>(tasks, tiles, total_tiles, bt, st);
     else
-        launch_syrk_t<0, false>(tasks, tiles, total_tiles, bt, lds_mode, nullptr, st);
+        launch_syrk_t<0>(tasks, tiles, total_tiles, bt, st);
     return hipGetLastError();
 }
 

@@ -19,7 +19,6 @@ constexpr int ASM_TILE_MIN_M = 8192;  // fronts at least this tall use the write
 // Output tile edges of the MFMA SYRK kernel (per launch).
 constexpr int SYRK_BT_SMALL = 64;
 constexpr int SYRK_BT_LARGE = 128;
-constexpr int SYRK_BT_LARGE_W4 = 1128;  // launch code: 128 x 128 tiles on 4 waves (64 x 64 each)
 
 // C/D register map of v_mfma_f64_16x16x4_f64 on gfx950 (cdna_hip_programming.md
 // section 3): col = lane & 15, row = (lane >> 4) + 4 * reg.
@@ -43,10 +42,6 @@ struct DevPlan {
     double* panel_pool;
     double* cb_pool;
     int32_t* info;              // min failing internal column + 1
-    int32_t* blk_cnt;           // ns: arrival tickets of the fused POTRF+TRSM (panel variant 3)
-    const int32_t* chain_of;    // ns: chain launch computing the front (-1: none)
-    int32_t* chain_done;        // ns: front finished in this factorization (chain launches)
-    int32_t* chain_err;         // a chain wait timed out (never expected)
 };
 
 // One lower-trapezoid SYRK update: C[i,j] -= sum_k A[i,k] A[j,k], j < N, j <= i < M.
@@ -56,8 +51,6 @@ struct GemmTask {
     int64_t ldc;
     int64_t lda;
     int32_t M, N, K;
-    int32_t potrf_col;  // > 0: tile (0, 0) also factors the 64 x 64 block at C (fused POTRF);
-                        // value = internal column of the block + 1 (for non-PD reporting)
 };
 
 // Strided <-> packed copy of a rows x cols block (pack: a -> b; unpack: b -> a).
@@ -99,30 +92,16 @@ hipError_t launch_permute(double* dst, const double* src, const int32_t* perm, i
 
 hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count, int maxm, const double* Ax,
                               hipStream_t st);
-// runs of thin small-front levels as one ticket-ordered launch; ticket: zeroed per factorization
-hipError_t launch_front_chain(const DevPlan& P, const int32_t* nodes, int count, int maxm, const double* Ax,
-                              int32_t* ticket, int chain_id, hipStream_t st);
 // tiled: tasks are (front, (row tile << 16) | 16-column block) for the write-once
 // tile kernel (fronts with m >= ASM_TILE_MIN_M), else (front, column block)
 hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count, const double* Ax,
                                  hipStream_t st, bool tiled);
-// Panel kernel variants: 0 LDS-broadcast substitution, 1 generated pipelined
-// substitution (256 rows per TRSM task), 2 (default) POTRF + inv(L11) and MFMA TRSM
-// (TRSM_MFMA_ROWS rows per task; needs variant-2 POTRF output).  0/1 are kept
-// for A/B microbenchmarks (sc_debug_bench).
-constexpr int PANEL_VARIANT = 1;
-constexpr int TRSM_MFMA_ROWS = 64;
-inline int trsm_task_rows(int variant) { return variant == 2 ? TRSM_MFMA_ROWS : TRSM_ROWS; }
-hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hipStream_t st,
-                             int variant = PANEL_VARIANT);
-// partial: every task is a partial last block (nb < 64); variants 1/2 need those
-// in a separate launch (the full-block kernels skip them)
-hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st,
-                             int variant = PANEL_VARIANT, bool partial = false);
-// fuse_info != nullptr: panel-update launch whose tasks may carry a fused POTRF
-// lds_mode: 0 default; 1 at most one workgroup per CU; 2 BK = 8 (half the LDS)
-hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
-                       int lds_mode = 0, int32_t* fuse_info = nullptr);
+// Large-front panel kernels (generated straight-line code, panel_gen.inc): the
+// 64 x 64 diagonal POTRF (one wave per block) and the TRSM of the rows below it
+// (TRSM_ROWS rows per task).  partial: every task is a partial last block (nb < 64).
+hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hipStream_t st);
+hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st, bool partial = false);
+hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st);
 hipError_t launch_stamp(uint64_t* slot, hipStream_t st);
 hipError_t launch_fill_random(double* p, int64_t n, hipStream_t st);
 hipError_t launch_mfma_peak(double* out, int blocks, int iters, int nacc, hipStream_t st);

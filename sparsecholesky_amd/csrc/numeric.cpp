@@ -142,7 +142,6 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
     for (int32_t s = 0; s < S.ns; ++s) by_level[S.level[s]].push_back(s);
     double* panel_pool = N.P.panel_pool;
     double* cb_pool = N.P.cb_pool;
-    std::vector<int32_t> fused_at((size_t)S.ns, -1);
     // multi-GPU plan lookups
     const DistPlan& D = N.D;
     const bool real_comm = !N.owner.empty() && N.virt_ranks <= 1;
@@ -172,7 +171,6 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         L.kind = kind;
         L.level = level;
         L.strm = strm;
-        for (auto& t : tasks) L.fuse |= t.potrf_col > 0 ? 1 : 0;
         L.off = (int64_t)gemm.size();
         // 128x128 tiles on 8 waves when every task is at least 256 wide (random data,
         // 16384 x 4096: 61 vs 52 TF/s for 64x64); 64x64 on 4 waves for narrow updates
@@ -358,25 +356,10 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         // (stream 1), which overlaps the next slab's factorization.  A later outer
         // update of overlapping columns waits for the stream-1 work first.
         int b_pending = -1;
-        // cb_slab: fronts with several slabs (and a CB, not split) take their CB update
-        // slab by slab on stream 1 (K = NBO) as the slabs become final, instead of one
-        // K = w SYRK after the panel; the last slab stays in the level's CB launch
-        int cb_pending = -1;
-        auto cb_by_slab = [&](int32_t s) {
-            return S.opt.cb_slab != 0 && !is_split(s) && S.w(s) > NBO && S.mb(s) > 0;
-        };
-        // fused POTRF: the update that completes block [c_lo, c_lo + 64) of front s
-        // (its last update before its POTRF) factors that diagonal block in its tile
-        // (0, 0); the block then gets no POTRF task.  fused_at[s] = that block's start.
         auto add_update = [&](std::vector<GemmTask>& v, double& fl, double* pan, int m, int c_lo, int c_hi, int ka,
-                              int kb, int s = -1) {
+                              int kb) {
             if (c_hi <= c_lo || kb <= ka) return;
             GemmTask t {};
-            // (not with panel variant 2: its TRSM needs the inverse only potrf_inv_kernel forms)
-            if (s >= 0 && S.opt.fuse_potrf && N.panel_variant != 2 && N.panel_variant != 3 && S.w(s) - c_lo >= PNB && c_hi - c_lo >= PNB) {
-                t.potrf_col = S.sn_start[s] + c_lo + 1;
-                fused_at[s] = c_lo;
-            }
             t.C = pan + (int64_t)c_lo * m + c_lo;
             t.A = pan + (int64_t)ka * m + c_lo;
             t.ldc = m;
@@ -396,8 +379,7 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             Lt.kind = L_TRSM;
             Lt.level = lev;
             Lt.off = (int64_t)trsm.size();
-            std::vector<GemmTask> upd, outer_a, outer_b, cbs;
-            double cfl = 0.0;
+            std::vector<GemmTask> upd, outer_a, outer_b;
             std::vector<int4> trsm_part;  // partial last blocks: own launch (big = 1)
             double uflops = 0.0, afl = 0.0, bfl = 0.0;
             for (int32_t s : large) {
@@ -405,10 +387,8 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
                 if (w <= k0) continue;
                 const int nb = std::min(PNB, w - k0);
                 const int k1 = k0 + nb;
-                // variant 3: full blocks with rows below are factored inside their TRSM
-                const bool in_trsm = N.panel_variant == 3 && nb == PNB && k1 < m;
-                if (fused_at[s] != k0 && !in_trsm) potrf.push_back(make_int2(s, k0));
-                for (int r0 = k1; r0 < m; r0 += trsm_task_rows(N.panel_variant))
+                potrf.push_back(make_int2(s, k0));
+                for (int r0 = k1; r0 < m; r0 += TRSM_ROWS)
                     (nb < PNB ? trsm_part : trsm).push_back(make_int4(s, k0, r0, 0));
                 double* pan = panel_pool + S.panel_off[s];
                 const int slab0 = (k0 / NBO) * NBO;
@@ -420,28 +400,15 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
                     // right-looking, 768 instead of 1792 C columns rewritten per slab.
                     const int b = (k0 - slab0) / PNB;
                     const int span = PNB << __builtin_ctz((unsigned)(b + 1));
-                    add_update(upd, uflops, pan, m, k1, std::min(slab1, k1 + span), k1 - span, k1, s);
+                    add_update(upd, uflops, pan, m, k1, std::min(slab1, k1 + span), k1 - span, k1);
                 } else if (k1 < slab1) {
-                    add_update(upd, uflops, pan, m, k1, slab1, k0, k1, s);
+                    add_update(upd, uflops, pan, m, k1, slab1, k0, k1);
                 } else if (k1 == slab1 && slab1 < w) {
                     // outer_a is the last update of block slab1: a pending stream-1 outer
                     // update of those columns is waited for before outer_a runs
                     const int nxt = S.opt.lookahead ? std::min(w, slab1 + NBO) : w;
-                    add_update(outer_a, afl, pan, m, slab1, nxt, slab0, slab1, s);
+                    add_update(outer_a, afl, pan, m, slab1, nxt, slab0, slab1);
                     add_update(outer_b, bfl, pan, m, nxt, w, slab0, slab1);
-                    if (cb_by_slab(s)) {
-                        const int mb = m - w;
-                        GemmTask t {};
-                        t.C = cb_pool + S.cb_off[s];
-                        t.A = pan + (int64_t)slab0 * m + w;
-                        t.ldc = mb;
-                        t.lda = m;
-                        t.M = mb;
-                        t.N = mb;
-                        t.K = slab1 - slab0;
-                        cbs.push_back(t);
-                        cfl += (double)mb * (mb + 1.0) * t.K;
-                    }
                 }
             }
             Lp.count = (int32_t)((int64_t)potrf.size() - Lp.off);
@@ -465,7 +432,7 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             }
             push_gemm_launch(L_PANEL, lev, upd, 0, uflops);
             int e_trsm = -1;
-            if (!outer_b.empty() || !cbs.empty()) e_trsm = push_record(0);
+            if (!outer_b.empty()) e_trsm = push_record(0);
             if (!outer_a.empty()) {
                 if (b_pending >= 0) {
                     push_wait(0, b_pending);
@@ -478,14 +445,8 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
                 push_gemm_launch(L_PANEL, lev, outer_b, 0, bfl, 1);
                 b_pending = push_record(1);
             }
-            if (!cbs.empty()) {  // after b_pending: the chain never waits for these
-                if (outer_b.empty()) push_wait(1, e_trsm);
-                push_gemm_launch(L_CB, lev, cbs, 1, cfl, 1);
-                cb_pending = push_record(1);
-            }
         }
         if (b_pending >= 0) push_wait(0, b_pending);
-        if (cb_pending >= 0) push_wait(0, cb_pending);
         // early-delivery children: the CB SYRK in column groups, an event after each
         // (the group's comm sub-step waits for exactly that event)
         for (int32_t s : large) {
@@ -513,14 +474,13 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
                 const int w = S.w(s), m = S.sn_m[s], mb = m - w;
                 if (mb <= 0 || (w >= 256) != (big == 1) || is_split(s) || is_early_sender(s)) continue;
                 GemmTask t {};
-                const int kfrom = cb_by_slab(s) ? ((w - 1) / NBO) * NBO : 0;  // last slab only
                 t.C = cb_pool + S.cb_off[s];
-                t.A = panel_pool + S.panel_off[s] + (int64_t)kfrom * m + w;
+                t.A = panel_pool + S.panel_off[s] + w;
                 t.ldc = mb;
                 t.lda = m;
                 t.M = mb;
                 t.N = mb;
-                t.K = w - kfrom;
+                t.K = w;
                 cbt.push_back(t);
                 fl += (double)mb * (mb + 1.0) * t.K;
             }
@@ -528,38 +488,7 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         }
         };
     if (real_comm) push_wait(2, push_record(0));  // previous factorization's reads are done
-    // single device: runs of >= 2 thin levels of small fronts -> one ticket-ordered launch
-    std::vector<int32_t>& chain_of = N.chain_of;
-    chain_of.assign((size_t)S.ns, -1);
-    auto thin = [&](int32_t lev) {
-        if (by_level[lev].empty() || by_level[lev].size() > 512) return false;
-        for (int32_t s : by_level[lev])
-            if (S.fclass[s] != FRONT_SMALL) return false;
-        return true;
-    };
     for (int32_t lev = 0; lev < S.nlevels; ++lev) {
-        if (N.owner.empty() && S.opt.chain_small && lev + 1 < S.nlevels && thin(lev) && thin(lev + 1)) {
-            int32_t l2 = lev;
-            while (l2 + 1 < S.nlevels && thin(l2 + 1)) ++l2;
-            Launch L {};
-            L.kind = L_SMALL;
-            L.big = 1;
-            L.level = lev;
-            L.off = (int64_t)small.size();
-            int mx = 1;
-            for (int32_t l = lev; l <= l2; ++l)
-                for (int32_t s : by_level[l]) {
-                    small.push_back(s);
-                    chain_of[s] = N.n_chains;
-                    mx = std::max(mx, (int)S.sn_m[s]);
-                }
-            L.count = (int32_t)((int64_t)small.size() - L.off);
-            L.maxm = bucket_of(mx);
-            L.step = N.n_chains++;
-            N.sched.push_back(L);
-            lev = l2;
-            continue;
-        }
         if (N.owner.empty()) {
             emit_level(lev, by_level[lev]);
             continue;
@@ -636,18 +565,7 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     int prio_lo = 0, prio_hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     bool ok = hipStreamCreateWithPriority(&N.stream, hipStreamNonBlocking, prio_hi) == hipSuccess;
-    if (ok && S.opt.lookahead == 3) {
-        // trailing updates may not use every 8th CU: the critical path always finds room
-        hipDeviceProp_t prop;
-        (void)hipGetDeviceProperties(&prop, device);
-        const int ncu = prop.multiProcessorCount;
-        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-        for (int c = 0; c < ncu; ++c)
-            if (c % 8 != 7) mask[c / 32] |= 1u << (c % 32);
-        ok = hipExtStreamCreateWithCUMask(&N.stream2, (uint32_t)mask.size(), mask.data()) == hipSuccess;
-    } else if (ok) {
-        ok = hipStreamCreateWithPriority(&N.stream2, hipStreamNonBlocking, prio_lo) == hipSuccess;
-    }
+    if (ok) ok = hipStreamCreateWithPriority(&N.stream2, hipStreamNonBlocking, prio_lo) == hipSuccess;
     // multi-GPU comm stream.  Only there: one more stream on the device costs 13.5%
     // under hipGraph replay (569 -> 649 ms at 128^3, any priority, any
     // GPU_MAX_HW_QUEUES) though nothing runs on it; eager runs (multi-GPU) see 0.5%.
@@ -658,7 +576,6 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
         return fail(SC_ERR_HIP);
     }
     N.use_graph = S.opt.use_graph != 0;
-    N.panel_variant = (S.opt.panel_variant >= 1 && S.opt.panel_variant <= 3) ? S.opt.panel_variant : PANEL_VARIANT;
     const int32_t ns = S.ns;
     int64_t rc;
     DevPlan& P = N.P;
@@ -700,12 +617,6 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     P.cb_pool = (double*)p;
     if ((rc = dalloc(N, 64, p))) return fail(rc);
     P.info = (int32_t*)p;
-    if ((rc = dalloc(N, (size_t)std::max(ns, 1) * sizeof(int32_t), p))) return fail(rc);
-    if (hipMemset(p, 0, (size_t)std::max(ns, 1) * sizeof(int32_t)) != hipSuccess) {
-        N.err = "hipMemset failed";
-        return fail(SC_ERR_HIP);
-    }
-    P.blk_cnt = (int32_t*)p;
 
     std::vector<int32_t> small;
     std::vector<int2> asmv, potrf;
@@ -722,18 +633,6 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
         for (size_t q = 0; q < cbld.copies.size(); ++q) cbld.copies[q].b = N.staging + cbld.copy_slot[q];
     }
     if ((rc = upload(N, cbld.copies, N.d_copy)) || (rc = upload(N, cbld.ctiles, N.d_ctiles))) return fail(rc);
-    {
-        const int32_t* d_chain_of = nullptr;
-        int32_t* tmp = nullptr;
-        if ((rc = upload(N, N.chain_of, tmp))) return fail(rc);
-        d_chain_of = tmp;
-        if ((rc = dalloc(N, sizeof(int32_t) * ((size_t)N.n_chains + ns + 1), p))) return fail(rc);
-        N.d_chain_state = (int32_t*)p;
-        P.chain_of = d_chain_of;
-        P.chain_done = N.d_chain_state + N.n_chains;
-        P.chain_err = N.d_chain_state + N.n_chains + ns;
-        HIP_TRY(hipMemset(p, 0, sizeof(int32_t) * ((size_t)N.n_chains + ns + 1)));
-    }
     N.stamp_of.assign(N.sched.size(), -1);
     int nstamp = 0;
     for (size_t i = 0; i < N.sched.size(); ++i)
@@ -767,28 +666,16 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
         case L_WAIT:
             return hipStreamWaitEvent(st, N.sync_ev[L.count], 0);
         case L_SMALL:
-            if (L.big)
-                return launch_front_chain(N.P, N.d_small + L.off, L.count, L.maxm, d_Ax, N.d_chain_state + L.step,
-                                          L.step, N.stream);
             return launch_front_small(N.P, N.d_small + L.off, L.count, L.maxm, d_Ax, N.stream);
         case L_ASM:
             return launch_assemble_large(N.P, N.d_asm + L.off, L.count, d_Ax, N.stream, L.big != 0);
         case L_POTRF:
-            return launch_potrf_diag(N.P, N.d_potrf + L.off, L.count, N.stream, N.panel_variant);
+            return launch_potrf_diag(N.P, N.d_potrf + L.off, L.count, N.stream);
         case L_TRSM:
-            return launch_trsm_panel(N.P, N.d_trsm + L.off, L.count, N.stream, N.panel_variant, L.big != 0);
+            return launch_trsm_panel(N.P, N.d_trsm + L.off, L.count, N.stream, L.big != 0);
         case L_PANEL:
         case L_CB:
-        {
-            // lookahead 2: stream-1 updates at most one workgroup per CU; 4: stream-1
-            // updates with BK = 8; 5: every panel update with BK = 8
-            const int la = N.S->opt.lookahead;
-            int lds_mode = 0;
-            if (L.strm == 1 && la == 2) lds_mode = 1;
-            if ((L.strm == 1 && la == 4) || (L.kind == L_PANEL && la == 5)) lds_mode = 2;
-            return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st,
-                               lds_mode, L.fuse ? N.P.info : nullptr);
-        }
+            return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st);
         case L_COMM:
             return comm_launch(N, L);
     }
@@ -797,8 +684,6 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
 
 static int64_t enqueue_all(Numeric& N, const double* d_Ax, int prof) {
     HIP_TRY(hipMemsetAsync(N.P.info, 0x7f, sizeof(int32_t), N.stream));
-    if (N.n_chains > 0)
-        HIP_TRY(hipMemsetAsync(N.d_chain_state, 0, sizeof(int32_t) * ((size_t)N.n_chains + N.S->ns + 1), N.stream));
     for (size_t i = 0; i < N.sched.size(); ++i) {
         const Launch& L = N.sched[i];
         const bool timed = prof == 1 && L.kind < L_RECORD;
@@ -889,14 +774,6 @@ int64_t numeric_status(Numeric& N) {
     if (N.stream3) HIP_TRY(hipStreamSynchronize(N.stream3));
     int32_t info = 0;
     HIP_TRY(hipMemcpy(&info, N.P.info, sizeof(info), hipMemcpyDeviceToHost));
-    if (N.n_chains > 0) {
-        int32_t cerr = 0;
-        HIP_TRY(hipMemcpy(&cerr, N.P.chain_err, sizeof(cerr), hipMemcpyDeviceToHost));
-        if (cerr) {
-            N.err = "small-front chain launch: a dependency wait timed out";
-            return SC_ERR_HIP;
-        }
-    }
     if (info == 0x7f7f7f7f || info <= 0)
         N.status = 0;
     else
@@ -1241,12 +1118,9 @@ int64_t debug_syrk(double* dC, int ldc, const double* dA, int lda, int M, int Nn
     return (e == hipSuccess && e2 == hipSuccess) ? SC_OK : SC_ERR_HIP;
 }
 
-// Times `reps` launches of a grid of syrk tiles (M=N, K) on device buffers and of
-// the register-only MFMA peak probe; returns TFLOP/s for each.
 // Panel-kernel microbenchmarks on one synthetic front (m = M rows, w = 64):
-// which 2 = POTRF (us per launch), 3 = TRSM (us per launch), 4 = max |variant 0 -
-// variant 1| over POTRF + TRSM results.  arg = kernel variant for 2 / 3.
-static int64_t bench_panel(int which, int M, int reps, int arg, double* out) {
+// which 2 = POTRF (us per launch), 3 = TRSM (us per launch).
+static int64_t bench_panel(int which, int M, int reps, double* out) {
     const int w = PNB;
     if (M < w || reps < 1) return SC_ERR_ARG;
     const size_t nel = (size_t)M * w;
@@ -1262,22 +1136,17 @@ static int64_t bench_panel(int which, int M, int reps, int arg, double* out) {
         for (int i = 0; i < M; ++i) h[(size_t)j * M + i] = (i == j) ? 64.0 : rnd();
     int32_t hs[2] = {0, w}, hm[1] = {M};
     int64_t ho[2] = {0, (int64_t)nel};
-    // which 3: TRSM variant arg (after a POTRF of the matching variant); which 4:
-    // variant 0 vs variant arg (1 or 2)
-    const int var = std::max(1, std::min(2, arg));
-    std::vector<int4> tr, tr0;
-    for (int r0 = w; r0 < M; r0 += trsm_task_rows(var)) tr.push_back(make_int4(0, 0, r0, 0));
-    for (int r0 = w; r0 < M; r0 += trsm_task_rows(0)) tr0.push_back(make_int4(0, 0, r0, 0));
+    std::vector<int4> tr;
+    for (int r0 = w; r0 < M; r0 += TRSM_ROWS) tr.push_back(make_int4(0, 0, r0, 0));
     int2 pt = make_int2(0, 0);
-    void *d_pan = nullptr, *d_pan2 = nullptr, *d_ref = nullptr, *d_s = nullptr, *d_m = nullptr, *d_o = nullptr,
-         *d_info = nullptr, *d_pt = nullptr, *d_tr = nullptr, *d_tr0 = nullptr;
+    void *d_pan = nullptr, *d_ref = nullptr, *d_s = nullptr, *d_m = nullptr, *d_o = nullptr, *d_info = nullptr,
+         *d_pt = nullptr, *d_tr = nullptr;
     const size_t bytes = (nel + PNB) * sizeof(double);
     int64_t rc = SC_OK;
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (hipMalloc(&d_pan, bytes) || hipMalloc(&d_pan2, bytes) || hipMalloc(&d_ref, bytes) || hipMalloc(&d_s, 8) ||
-        hipMalloc(&d_m, 4) || hipMalloc(&d_o, 16) || hipMalloc(&d_info, 4) || hipMalloc(&d_pt, 8) ||
-        hipMalloc(&d_tr, std::max<size_t>(1, tr.size()) * sizeof(int4)) ||
-        hipMalloc(&d_tr0, std::max<size_t>(1, tr0.size()) * sizeof(int4)) || hipEventCreate(&e0) ||
+    if (hipMalloc(&d_pan, bytes) || hipMalloc(&d_ref, bytes) || hipMalloc(&d_s, 8) || hipMalloc(&d_m, 4) ||
+        hipMalloc(&d_o, 16) || hipMalloc(&d_info, 4) || hipMalloc(&d_pt, 8) ||
+        hipMalloc(&d_tr, std::max<size_t>(1, tr.size()) * sizeof(int4)) || hipEventCreate(&e0) ||
         hipEventCreate(&e1)) {
         rc = SC_ERR_DEVMEM;
     } else {
@@ -1288,75 +1157,51 @@ static int64_t bench_panel(int which, int M, int reps, int arg, double* out) {
         (void)hipMemset(d_info, 0, 4);
         (void)hipMemcpy(d_pt, &pt, 8, hipMemcpyHostToDevice);
         if (!tr.empty()) (void)hipMemcpy(d_tr, tr.data(), tr.size() * sizeof(int4), hipMemcpyHostToDevice);
-        if (!tr0.empty()) (void)hipMemcpy(d_tr0, tr0.data(), tr0.size() * sizeof(int4), hipMemcpyHostToDevice);
         DevPlan P {};
         P.sn_start = (const int32_t*)d_s;
         P.sn_m = (const int32_t*)d_m;
         P.panel_off = (const int64_t*)d_o;
         P.info = (int32_t*)d_info;
-        auto on = [&](void* pan) {
-            DevPlan Q = P;
-            Q.panel_pool = (double*)pan;
-            return Q;
-        };
-        const int nt = (int)tr.size(), nt0 = (int)tr0.size();
-        if (which == 4) {
-            for (int v = 0; v < 2; ++v) {
-                void* dst = v ? d_pan2 : d_pan;
-                (void)hipMemcpy(dst, d_ref, bytes, hipMemcpyDeviceToDevice);
-                (void)launch_potrf_diag(on(dst), (const int2*)d_pt, 1, nullptr, v ? var : 0);
-                if (v)
-                    (void)launch_trsm_panel(on(dst), (const int4*)d_tr, nt, nullptr, var);
-                else
-                    (void)launch_trsm_panel(on(dst), (const int4*)d_tr0, nt0, nullptr, 0);
-            }
-            (void)hipDeviceSynchronize();
-            std::vector<double> a(nel), b(nel);
-            (void)hipMemcpy(a.data(), d_pan, nel * 8, hipMemcpyDeviceToHost);
-            (void)hipMemcpy(b.data(), d_pan2, nel * 8, hipMemcpyDeviceToHost);
-            double md = 0.0;
-            for (int j = 0; j < w; ++j)
-                for (int i = j; i < M; ++i) md = std::max(md, std::fabs(a[(size_t)j * M + i] - b[(size_t)j * M + i]));
-            *out = md;
-        } else {
-            (void)hipMemcpy(d_pan, d_ref, bytes, hipMemcpyDeviceToDevice);
-            (void)launch_potrf_diag(on(d_pan), (const int2*)d_pt, 1, nullptr, arg >= 2 ? 2 : 1);
-            double tot = 0.0;
-            for (int r = 0; r < reps + 1; ++r) {
-                if (which == 2) (void)hipMemcpy(d_pan, d_ref, bytes, hipMemcpyDeviceToDevice);
-                (void)hipEventRecord(e0, nullptr);
-                if (which == 2)
-                    (void)launch_potrf_diag(on(d_pan), (const int2*)d_pt, 1, nullptr, arg);
-                else if (arg == 0)
-                    (void)launch_trsm_panel(on(d_pan), (const int4*)d_tr0, nt0, nullptr, 0);
-                else
-                    (void)launch_trsm_panel(on(d_pan), (const int4*)d_tr, nt, nullptr, arg);
-                (void)hipEventRecord(e1, nullptr);
-                (void)hipEventSynchronize(e1);
-                float ms = 0.f;
-                (void)hipEventElapsedTime(&ms, e0, e1);
-                if (r > 0) tot += ms;
-            }
-            *out = 1e3 * tot / reps;
+        P.panel_pool = (double*)d_pan;
+        const int nt = (int)tr.size();
+        (void)hipMemcpy(d_pan, d_ref, bytes, hipMemcpyDeviceToDevice);
+        (void)launch_potrf_diag(P, (const int2*)d_pt, 1, nullptr);
+        double tot = 0.0;
+        for (int r = 0; r < reps + 1; ++r) {
+            if (which == 2) (void)hipMemcpy(d_pan, d_ref, bytes, hipMemcpyDeviceToDevice);
+            (void)hipEventRecord(e0, nullptr);
+            if (which == 2)
+                (void)launch_potrf_diag(P, (const int2*)d_pt, 1, nullptr);
+            else
+                (void)launch_trsm_panel(P, (const int4*)d_tr, nt, nullptr);
+            (void)hipEventRecord(e1, nullptr);
+            (void)hipEventSynchronize(e1);
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            if (r > 0) tot += ms;
         }
+        *out = 1e3 * tot / reps;
         if (hipGetLastError() != hipSuccess) rc = SC_ERR_HIP;
     }
-    for (void* p : {d_pan, d_pan2, d_ref, d_s, d_m, d_o, d_info, d_pt, d_tr, d_tr0})
+    for (void* p : {d_pan, d_ref, d_s, d_m, d_o, d_info, d_pt, d_tr})
         if (p) (void)hipFree(p);
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     return rc;
 }
 
+// which 0: register-only fp64 MFMA peak probe (M blocks of 4 waves, K iterations,
+// arg accumulators); 1 / 5: the SYRK kernel on an M x M triangle, K deep, tile arg
+// (64 / 128), with / without the XCD tile order; 2 / 3: bench_panel.  TFLOP/s or us.
 int64_t debug_bench(int which, int M, int K, int reps, int arg, double* tflops) {
     *tflops = 0.0;
-    if (which >= 2 && which <= 4) return bench_panel(which, M, reps, arg, tflops);
+    if (which == 2 || which == 3) return bench_panel(which, M, reps, tflops);
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return SC_ERR_HIP;
     double flops = 0.0;
     void *bufA = nullptr, *bufC = nullptr, *bt = nullptr, *bl = nullptr;
     int64_t rc = SC_OK;
-    if (which == 0) {  // MFMA peak probe: arg = accumulators per wave, M = blocks
+    if (which == 0) {
         if (hipMalloc(&bufC, 8 * (size_t)std::max(M, 1)) != hipSuccess) return SC_ERR_DEVMEM;
         (void)launch_mfma_peak((double*)bufC, M, K, arg, nullptr);
         (void)hipDeviceSynchronize();
@@ -1364,7 +1209,7 @@ int64_t debug_bench(int which, int M, int K, int reps, int arg, double* tflops) 
         for (int r = 0; r < reps; ++r) (void)launch_mfma_peak((double*)bufC, M, K, arg, nullptr);
         (void)hipEventRecord(e1, nullptr);
         flops = 2.0 * 16 * 16 * 4 * (double)arg * K * M * 4.0 * reps;  // 4 waves per block
-    } else {  // SYRK kernel on an M x M lower triangle, K deep (arg = tile 64/128)
+    } else {
         const size_t na = (size_t)M * K, nc = (size_t)M * M;
         if (hipMalloc(&bufA, na * 8) != hipSuccess || hipMalloc(&bufC, nc * 8) != hipSuccess) {
             rc = SC_ERR_DEVMEM;
@@ -1381,21 +1226,18 @@ int64_t debug_bench(int which, int M, int K, int reps, int arg, double* tflops) 
             t.M = M;
             t.N = M;
             t.K = K;
-            const int tb = arg == 128 ? 128 : (arg == SYRK_BT_LARGE_W4 ? SYRK_BT_LARGE_W4 : 64);
+            const int tb = arg == 128 ? 128 : 64;
             std::vector<int2> tiles;
-            append_tiles(tiles, 0, M, M, tb == SYRK_BT_LARGE_W4 ? 128 : tb);
+            append_tiles(tiles, 0, M, M, tb);
             if (which != 5) xcd_order(tiles.data(), (int64_t)tiles.size());
             (void)hipMalloc(&bt, sizeof(GemmTask));
             (void)hipMalloc(&bl, tiles.size() * sizeof(int2));
             (void)hipMemcpy(bt, &t, sizeof(t), hipMemcpyHostToDevice);
             (void)hipMemcpy(bl, tiles.data(), tiles.size() * sizeof(int2), hipMemcpyHostToDevice);
-            // which 6 / 7: BK = 8 / 32 instances (lds_mode 2 / 3)
-            const int lm = which == 6 ? 2 : which == 7 ? 3 : 0;
-            (void)launch_syrk((GemmTask*)bt, (int2*)bl, (int)tiles.size(), tb, 1, nullptr, lm);
+            (void)launch_syrk((GemmTask*)bt, (int2*)bl, (int)tiles.size(), tb, 1, nullptr);
             (void)hipDeviceSynchronize();
             (void)hipEventRecord(e0, nullptr);
-            for (int r = 0; r < reps; ++r)
-                (void)launch_syrk((GemmTask*)bt, (int2*)bl, (int)tiles.size(), tb, 1, nullptr, lm);
+            for (int r = 0; r < reps; ++r) (void)launch_syrk((GemmTask*)bt, (int2*)bl, (int)tiles.size(), tb, 1, nullptr);
             (void)hipEventRecord(e1, nullptr);
             flops = (double)M * (M + 1.0) * K * reps;
         }

@@ -91,7 +91,6 @@ struct Launch {
     int32_t big;      // CB launch covering fronts with w >= 256
     int32_t bt;       // SYRK tile edge (64 or 128)
     int32_t strm;     // 0 = main stream, 1 = lookahead stream
-    int32_t fuse;     // panel launch whose tasks may factor the next diagonal block (potrf_col)
     double flops;     // algorithmic SYRK flops (CB launches: mb*(mb+1)*w)
     // L_COMM: copy tiles [poff, poff + pcount) pack the sends, [uoff, uoff + ucount)
     // unpack the receives (Numeric::d_ctiles)
@@ -103,7 +102,6 @@ struct Launch {
 struct Numeric {
     const Symbolic* S = nullptr;
     int device = 0;
-    int panel_variant = PANEL_VARIANT;  // large-front POTRF/TRSM kernels (kernels.hpp)
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;  // trailing panel updates overlapped with the next slab
     hipStream_t stream3 = nullptr;  // multi-GPU: comm stream (pack, RCCL group, unpack), strm == 2
@@ -118,8 +116,6 @@ struct Numeric {
     int4* d_trsm = nullptr;
     GemmTask* d_gemm = nullptr;
     int2* d_tiles = nullptr;
-    int32_t* d_chain_state = nullptr;  // tickets[n_chains], done[ns], err: zeroed per factorization
-    int32_t n_chains = 0;
     double* d_Ax_owned = nullptr;
     const double* last_Ax = nullptr;
     bool factored = false;
@@ -145,7 +141,6 @@ struct Numeric {
     // pools, no transfers) to validate the partition on one device.
     int rank = 0, nranks = 1, virt_ranks = 0;
     std::vector<int32_t> owner;
-    std::vector<int32_t> chain_of;  // supernode -> small-front chain launch, -1 = none
     DistPlan D;
     std::vector<Msg> msgs;
     Copy2D* d_copy = nullptr;     // pack / unpack descriptors

@@ -43,7 +43,7 @@ def test_default_options():
     o = sc.default_options()
     assert o.relax == 1 and list(o.nrelax) == [4, 16, 48] and o.small_front_max == 128
     assert o.panel_nb == 64 and o.panel_nb_outer == 1024 and o.syrk_tile == 0
-    assert o.lookahead == 1 and o.panel_variant == 0 and o.inner_order == 1 and o.asm_tile_min_m == 0 and o.fuse_potrf == 0
+    assert o.lookahead == 1 and o.inner_order == 1 and o.asm_tile_min_m == 0
 
 
 def test_bad_arguments_return_errors():

@@ -229,29 +229,6 @@ def test_nd_ordering_factor_and_solve(gpu, mtx, case):
     assert _backward_error(A, x, b) < 1e-14
 
 
-@pytest.mark.parametrize("case", ["bcsstk01", "1138_bus", "random", "lap10nat"])
-def test_small_front_chain_launch(gpu, mtx, case):
-    # runs of thin small-front levels in one ticket-ordered launch: bitwise the same
-    # factor as one launch per level (same per-front arithmetic), and oracle parity
-    A = {"random": lambda: random_spd(700, 0.004, 13), "lap10nat": lambda: sc.laplacian3d(10, nd=False)}.get(
-        case, lambda: mtx(case))()
-    Ls = []
-    for chain in (1, 0):
-        r = sc.chol(A, chain_small=chain)
-        assert r.has_value(), r.error()
-        Ls.append(r.value())
-    assert np.array_equal(Ls[0].x, Ls[1].x)
-    st, Lp, Li, Lx = oracle.chol(A)
-    assert np.array_equal(Ls[0].p, Lp) and np.array_equal(Ls[0].i, Li)
-    assert rel_fro(Ls[0].x, Lx) < TOL
-    # refactor through the same handle (tickets and done flags reset per factorization)
-    num = sc.Numeric(sc.Symbolic(A, chain_small=1))
-    for _ in range(3):
-        assert num.factor(A.x) == 0
-    _, L3 = num.export()
-    assert np.array_equal(L3.x, Ls[0].x)
-
-
 def test_solve_device_and_residual_lap32(gpu):
     # size-independent property at a larger size: backward-stable solve residual
     torch = pytest.importorskip("torch")
@@ -459,14 +436,10 @@ def test_dense_matrix_large_front(gpu):
     assert s["n_supernodes"] == 1 and s["max_front_w"] == n
 
 
-# large-front schedule variants: panel kernels (1 substitution, 2 inverse + MFMA
-# TRSM), inner slab update order (0 right-looking, 1 recursive), lookahead modes
-PANEL_OPTS = [dict(panel_variant=2), dict(inner_order=0), dict(panel_variant=2, inner_order=0, lookahead=0),
-              dict(lookahead=2), dict(panel_variant=2, lookahead=3), dict(lookahead=0), dict(asm_tile_min_m=1),
-              dict(asm_tile_min_m=300), dict(fuse_potrf=1), dict(fuse_potrf=1, inner_order=0, lookahead=0),
-              dict(cb_slab=1), dict(cb_slab=1, panel_nb_outer=128), dict(cb_slab=1, panel_nb_outer=64, lookahead=0),
-              dict(panel_variant=3), dict(panel_variant=3, panel_nb_outer=128, lookahead=0),
-              dict(panel_variant=3, fuse_potrf=1)]
+# large-front schedule options: inner slab update order (0 right-looking, 1
+# recursive), lookahead (0 none, 1 trailing updates on a second stream), tiled assembly
+PANEL_OPTS = [dict(inner_order=0), dict(inner_order=0, lookahead=0), dict(lookahead=0), dict(asm_tile_min_m=1),
+              dict(asm_tile_min_m=300), dict(panel_nb_outer=128, lookahead=0)]
 
 
 @pytest.mark.parametrize("opts", PANEL_OPTS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
