@@ -146,13 +146,16 @@ int64_t sc_factor(sc_numeric* num, const double* Ax);
 int64_t sc_factor_device(sc_numeric* num, const double* d_Ax, int32_t sync);
 int64_t sc_numeric_status(sc_numeric* num);
 /* Export L in the reference CSC layout (chol() output, chol.hpp:749-863):
- * Lp[n+1], Li[nnz_L], Lx[nnz_L]; any of the three may be NULL. */
+ * Lp[n+1], Li[nnz_L], Lx[nnz_L]; any of the three may be NULL.  On a multi-rank
+ * handle the call is collective (every rank calls it): the ranks exchange their
+ * panels and every rank receives the whole L, as the reference's chol() returns it
+ * (chol.hpp:858-862). */
 int64_t sc_export_L(sc_numeric* num, int64_t* Lp, int32_t* Li, double* Lx);
 /* Columns [j0, j1) of L straight from the supernodal panels (no pattern pass; for
  * factors too large for sc_export_L): column j holds its front's rows from j down
  * (row indices in the same numbering as Lp/Li, relaxed zeros included), values
  * in rx.  cp[j1-j0+1] offsets; ri / rx may be NULL to query the count.  Returns
- * the entry count (>= 0) or an error.  Single-device handles only. */
+ * the entry count (>= 0) or an error.  Collective on multi-rank handles when rx != NULL. */
 int64_t sc_export_L_cols(sc_numeric* num, int64_t j0, int64_t j1, int64_t* cp, int32_t* ri, double* rx);
 /* Device pointer of the library stream (hipStream_t) for event timing. */
 void* sc_numeric_stream(sc_numeric* num);
@@ -178,13 +181,28 @@ int64_t sc_numeric_launch_trace(sc_numeric* num, int32_t* kind, int32_t* level, 
  * tiles (one kernel instance, comparable with a kernel trace). */
 int64_t sc_numeric_syrk_stats(sc_numeric* num, int32_t wmin, double* flops, double* ms,
                               int64_t* launches);
+/* Device memory of the handle, bytes: info[0] everything allocated (pools, plan,
+ * staging, a gathered factor), info[1] panel arenas (L), info[2] work arenas (the
+ * interval-planned contribution blocks), info[3] the work arenas' lower bound (the
+ * largest sum of regions live at one level).  n = entries wanted (<= 4). */
+int64_t sc_numeric_memory(sc_numeric* num, int64_t* info, int32_t n);
+/* The memory plan without a device: per rank (nranks entries each) the panel arena,
+ * the work arena and its lower bound, bytes.  nranks = 1: the single-device plan. */
+int64_t sc_memory_plan(const sc_symbolic* sym, int32_t nranks, int64_t* panel_bytes, int64_t* work_bytes,
+                       int64_t* work_lower_bound_bytes);
+/* Test hook: checks the memory plan of every rank (no two regions overlap while both
+ * are live, all inside the arena); returns the number of violations (0 = sound). */
+int64_t sc_memory_plan_check(const sc_symbolic* sym, int32_t nranks);
 void sc_free_numeric(sc_numeric* num);
 
 /* Solve A x = b with the factor on the GPU (not in the reference):
  * level-scheduled supernodal forward (L y = P b) and backward (L^T z = y) sweeps,
  * x = P^T z.  sc_solve_host: host vectors b, x (length n; copies over PCIe);
- * sc_solve_device: device vectors (may alias), synchronous.  Returns the factor's
- * status (> 0: not positive definite, nothing solved); single-device handles only. */
+ * sc_solve_device: device vectors (may alias), synchronous; d_b must be complete
+ * on the device when the call is made (the library's stream does not order against
+ * the caller's).  Returns the factor's status (> 0: not positive definite, nothing
+ * solved).  Multi-rank handles: collective; the first solve after a factorization
+ * gathers the whole factor onto every rank, then every rank solves. */
 int64_t sc_solve_host(sc_numeric* num, const double* b, double* x);
 int64_t sc_solve_device(sc_numeric* num, const double* d_b, double* d_x);
 
@@ -234,10 +252,17 @@ int64_t sc_dist_owner_map(const sc_symbolic* sym, int32_t nranks, int32_t* owner
                           double* work_per_rank);
 /* This process is `rank` of `nranks` (one GPU each); it factors only the
  * supernodes it owns and exchanges contribution blocks with ncclSend/ncclRecv
- * after each assembly-tree level.  id128 == NULL: emulate all nranks ranks'
- * partitioned schedule inside this process on one device (validation mode). */
+ * after each assembly-tree level.  id128 == NULL: emulate all nranks ranks inside
+ * this process on one device (sc_numeric_create_dist_emulated, device copies). */
 int64_t sc_numeric_create_dist(const sc_symbolic* sym, int32_t device, int32_t rank,
                                int32_t nranks, const void* id128, sc_numeric** out);
+/* Every rank of an nranks-rank plan in this process on one device, each with its
+ * own memory plan and arenas; every message of the plan moves between them, as
+ * device copies (use_rccl = 0) or as ncclSend / ncclRecv to self inside one
+ * ncclGroupStart / ncclGroupEnd per comm step on a 1-rank RCCL communicator
+ * (use_rccl = 1).  Validation of the partition and of the message plan. */
+int64_t sc_numeric_create_dist_emulated(const sc_symbolic* sym, int32_t device, int32_t nranks, int32_t use_rccl,
+                                        sc_numeric** out);
 /* Per-rank message schedule for tests: returns number of messages; if the
  * arrays are non-NULL fills (comm step, peer, bytes, is_send) per message, in
  * posting order (comm steps ascending; all ranks follow one global step order). */

@@ -138,6 +138,10 @@ _SIGS = [
     ("sc_dist_plan_info", _I64, [_P, _I32, _P, _P, C.POINTER(_I64)]),
     ("sc_numeric_create_dist_host", _I64, [_P, _I32, _I32, _I32, C.c_void_p, _P, C.POINTER(_P)]),
     ("sc_numeric_create_dist_dry", _I64, [_P, _I32, _I32, _I32, C.POINTER(_P)]),
+    ("sc_numeric_create_dist_emulated", _I64, [_P, _I32, _I32, _I32, C.POINTER(_P)]),
+    ("sc_numeric_memory", _I64, [_P, _P, _I32]),
+    ("sc_memory_plan", _I64, [_P, _I32, _P, _P, _P]),
+    ("sc_memory_plan_check", _I64, [_P, _I32]),
     ("sc_debug_syrk", _I64, [_P, _I32, _P, _I32, _I32, _I32, _I32]),
     ("sc_debug_bench", _I64, [_I32, _I32, _I32, _I32, _I32, C.POINTER(_D)]),
     ("sc_device_count", _I64, []),
@@ -503,6 +507,13 @@ class Symbolic:
         nmsg = _check(lib().sc_dist_plan_info(self.h, nranks, _ptr(g), _ptr(cbr), C.byref(nst)), "dist_plan_info")
         return dict(gsize=g[:ns], split_cb_ranks=cbr[:ns], n_steps=nst.value, n_msgs=nmsg)
 
+    def memory_plan(self, nranks: int = 1) -> dict:
+        """Device memory plan without a device: per rank the panel arena (L), the
+        interval-planned work arena (contribution blocks) and its lower bound, bytes."""
+        pb, wb, lb = (np.zeros(nranks, dtype=np.int64) for _ in range(3))
+        _check(lib().sc_memory_plan(self.h, nranks, _ptr(pb), _ptr(wb), _ptr(lb)), "memory_plan")
+        return dict(panel=pb, work=wb, work_lower_bound=lb)
+
     def dist_schedule(self, nranks: int, rank: int):
         """This rank's messages in posting order: (comm step, peer, bytes, is_send)."""
         cnt = _check(lib().sc_dist_schedule(self.h, nranks, rank, None, None, None, None, 0), "dist_schedule")
@@ -525,12 +536,14 @@ class Numeric:
     """Device factorization handle (pools + level schedule on one HIP device)."""
 
     def __init__(self, symb: Symbolic, device: int = -1, rank: int = 0, nranks: int = 1,
-                 uid: Optional[bytes] = None, virtual: bool = False, transport=None):
+                 uid: Optional[bytes] = None, virtual: bool = False, transport=None, rccl_self: bool = False):
         """nranks > 1 with ``uid`` (from :func:`dist_unique_id` on rank 0): this process is
         ``rank`` of a subtree-partitioned multi-GPU factorization over RCCL.  ``virtual=True``
-        emulates all ``nranks`` ranks' partitioned schedule in this one process.
-        ``transport`` (e.g. :class:`GlooHostTransport`): the same multi-process protocol with
-        every transfer staged through host memory instead of RCCL (tests; ranks may share a GPU)."""
+        runs all ``nranks`` ranks in this one process, each with its own memory; every
+        message of the plan moves between them (device copies, or with ``rccl_self=True``
+        RCCL send/receive to self on a 1-rank communicator).  ``transport`` (e.g.
+        :class:`GlooHostTransport`): the multi-process protocol with every transfer staged
+        through host memory instead of RCCL (tests; ranks may share a GPU)."""
         self.symb = symb
         self.rank, self.nranks = rank, nranks
         self.transport = transport
@@ -541,11 +554,12 @@ class Numeric:
         elif transport is not None:
             _check(lib().sc_numeric_create_dist_host(symb.h, device, rank, nranks, C.cast(transport.fn, C.c_void_p),
                                                      None, C.byref(h)), "numeric_create_dist_host")
-        elif nranks > 1 or virtual:
-            idbuf = None
-            if not virtual:
-                assert uid is not None and len(uid) == 128
-                idbuf = C.create_string_buffer(uid, 128)
+        elif virtual:
+            _check(lib().sc_numeric_create_dist_emulated(symb.h, device, nranks, 1 if rccl_self else 0, C.byref(h)),
+                   "numeric_create_dist_emulated")
+        elif nranks > 1:
+            assert uid is not None and len(uid) == 128
+            idbuf = C.create_string_buffer(uid, 128)
             _check(lib().sc_numeric_create_dist(symb.h, device, rank, nranks, idbuf, C.byref(h)),
                    "numeric_create_dist")
         else:
@@ -589,6 +603,12 @@ class Numeric:
         fl, ms, nl = C.c_double(), C.c_double(), C.c_int64()
         _check(lib().sc_numeric_syrk_stats(self.h, wmin, C.byref(fl), C.byref(ms), C.byref(nl)), "syrk_stats")
         return fl.value, ms.value, nl.value
+
+    def memory(self) -> dict:
+        """Device memory held, bytes: total, panel arenas, work arenas, work lower bound."""
+        v = np.zeros(4, dtype=np.int64)
+        _check(lib().sc_numeric_memory(self.h, _ptr(v), 4), "memory")
+        return dict(total=int(v[0]), panel=int(v[1]), work=int(v[2]), work_lower_bound=int(v[3]))
 
     @property
     def stream(self) -> int:

@@ -23,8 +23,8 @@ i64 dist_owner_map(const Symbolic& S, int nranks, i32* owner, double* work);
 i64 dist_schedule(const Symbolic& S, int nranks, int rank, i32* level, i32* peer, i64* bytes, i32* is_send,
                   i64 cap);
 i64 numeric_create_dist(const Symbolic& S, int device, int rank, int nranks, const void* id128,
-                        int32_t (*xport)(void*, int32_t, int32_t, void*, int64_t), void* xport_ctx, Numeric*& out,
-                        std::string& err);
+                        int32_t (*xport)(void*, int32_t, int32_t, void*, int64_t), void* xport_ctx, int emulate,
+                        Numeric*& out, std::string& err);
 i64 dist_unique_id(void* id128);
 }  // namespace sc
 
@@ -383,7 +383,8 @@ int64_t sc_numeric_create_dist(const sc_symbolic* sym, int32_t device, int32_t r
     sc_numeric* h = new (std::nothrow) sc_numeric();
     if (!h) return SC_ERR_NOMEM;
     std::string err;
-    int64_t rc = sc::numeric_create_dist(sym->S, device, rank, nranks, id128, nullptr, nullptr, h->N, err);
+    int64_t rc = sc::numeric_create_dist(sym->S, device, rank, nranks, id128, nullptr, nullptr, id128 ? 0 : 1, h->N,
+                                         err);
     if (rc != SC_OK) {
         g_last_error = err;
         delete h;
@@ -401,7 +402,7 @@ int64_t sc_numeric_create_dist_host(const sc_symbolic* sym, int32_t device, int3
     sc_numeric* h = new (std::nothrow) sc_numeric();
     if (!h) return SC_ERR_NOMEM;
     std::string err;
-    int64_t rc = sc::numeric_create_dist(sym->S, device, rank, nranks, nullptr, fn, ctx, h->N, err);
+    int64_t rc = sc::numeric_create_dist(sym->S, device, rank, nranks, nullptr, fn, ctx, 0, h->N, err);
     if (rc != SC_OK) {
         g_last_error = err;
         delete h;
@@ -419,7 +420,7 @@ int64_t sc_numeric_create_dist_dry(const sc_symbolic* sym, int32_t device, int32
     sc_numeric* h = new (std::nothrow) sc_numeric();
     if (!h) return SC_ERR_NOMEM;
     std::string err;
-    int64_t rc = sc::numeric_create_dist(sym->S, device, rank, nranks, nullptr, DIST_DRY, nullptr, h->N, err);
+    int64_t rc = sc::numeric_create_dist(sym->S, device, rank, nranks, nullptr, DIST_DRY, nullptr, 0, h->N, err);
     if (rc != SC_OK) {
         g_last_error = err;
         delete h;
@@ -427,6 +428,57 @@ int64_t sc_numeric_create_dist_dry(const sc_symbolic* sym, int32_t device, int32
     }
     h->sym = sym;
     *out = h;
+    return SC_OK;
+}
+
+int64_t sc_numeric_create_dist_emulated(const sc_symbolic* sym, int32_t device, int32_t nranks, int32_t use_rccl,
+                                        sc_numeric** out) {
+    if (!sym || !out || nranks <= 0) return SC_ERR_ARG;
+    *out = nullptr;
+    sc_numeric* h = new (std::nothrow) sc_numeric();
+    if (!h) return SC_ERR_NOMEM;
+    std::string err;
+    int64_t rc = sc::numeric_create_dist(sym->S, device, 0, nranks, nullptr, nullptr, nullptr, use_rccl ? 2 : 1, h->N,
+                                         err);
+    if (rc != SC_OK) {
+        g_last_error = err;
+        delete h;
+        return rc;
+    }
+    h->sym = sym;
+    *out = h;
+    return SC_OK;
+}
+
+int64_t sc_memory_plan(const sc_symbolic* sym, int32_t nranks, int64_t* panel_bytes, int64_t* work_bytes,
+                       int64_t* work_lower_bound_bytes) {
+    if (!sym || nranks <= 0) return SC_ERR_ARG;
+    std::vector<int64_t> p((size_t)nranks), w((size_t)nranks), l((size_t)nranks);
+    const int64_t rc = sc::plan_memory_stats(sym->S, nranks, p.data(), w.data(), l.data());
+    if (rc != SC_OK) return rc;
+    for (int32_t r = 0; r < nranks; ++r) {
+        if (panel_bytes) panel_bytes[r] = p[r] * (int64_t)sizeof(double);
+        if (work_bytes) work_bytes[r] = w[r] * (int64_t)sizeof(double);
+        if (work_lower_bound_bytes) work_lower_bound_bytes[r] = l[r] * (int64_t)sizeof(double);
+    }
+    return SC_OK;
+}
+
+int64_t sc_memory_plan_check(const sc_symbolic* sym, int32_t nranks) {
+    if (!sym || nranks <= 0) return SC_ERR_ARG;
+    return sc::plan_check(sym->S, nranks);
+}
+
+int64_t sc_numeric_memory(sc_numeric* num, int64_t* info, int32_t n) {
+    if (!num || !num->N || !info) return SC_ERR_ARG;
+    const sc::Numeric& N = *num->N;
+    int64_t v[4] = {N.dev_bytes, 0, 0, 0};
+    for (const sc::RankMem& R : N.R) {
+        v[1] += R.panel_total * (int64_t)sizeof(double);
+        v[2] += R.work_total * (int64_t)sizeof(double);
+        v[3] += R.work_live_max * (int64_t)sizeof(double);
+    }
+    for (int32_t i = 0; i < n && i < 4; ++i) info[i] = v[i];
     return SC_OK;
 }
 

@@ -158,11 +158,11 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
     // steps (ascending supernode), then the level's DELIVER sub-steps
     std::vector<std::vector<i32>> by_level((size_t)S.nlevels);
     for (i32 s = 0; s < ns; ++s) by_level[S.level[s]].push_back(s);
+    // column block jb of c's contribution block: rows [jb cbb, mb), its cbb columns
     auto cb_block = [&](DistMsg& g, i32 c, int jb) {
         const int mbc = S.mb(c);
-        g.pool = 1;
-        g.off = S.cb_off[c] + (i64)jb * D.cbb * mbc + (i64)jb * D.cbb;
-        g.ld = mbc;
+        g.skind = g.dkind = R_CB;
+        g.srow = g.scol = g.drow = g.dcol = jb * D.cbb;
         g.rows = mbc - jb * D.cbb;
         g.cols = std::min(D.cbb, g.rows);
         g.s = c;
@@ -200,9 +200,12 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
                     g.step = id;
                     g.src = own;
                     g.dst = r;
-                    g.pool = 0;
-                    g.off = S.panel_off[s] + (i64)k0 * m + w;
-                    g.ld = m;
+                    g.skind = R_PANEL;  // rows [w, m) of the owner's panel ...
+                    g.srow = w;
+                    g.scol = k0;
+                    g.dkind = R_LAND;   // ... into the CB rank's copy of L21
+                    g.drow = 0;
+                    g.dcol = k0;
                     g.rows = mb;
                     g.cols = k1 - k0;
                     g.s = s;
@@ -289,27 +292,37 @@ i64 dist_unique_id(void* id128) {
     return SC_OK;
 }
 
-// One comm step of this rank on the comm stream: pack the sends into their
-// staging slots, one RCCL group with every send / receive of the step (both
-// sides post a step's messages in the same plan order, so the per-peer matching
-// is consistent), unpack the receives.  With a host transport (tests) the group
-// goes through host memory instead, synchronously.
-hipError_t comm_launch(Numeric& N, const Launch& L) {
-    hipStream_t st = N.stream3;
+// One transfer group: every message of msgs[off, off + count) (the packed slots are
+// ready on stream st).  RCCL: one ncclGroupStart/End with each send / receive (both
+// ends post a step's messages in the same plan order, so the per-peer matching is
+// consistent; a 1-rank communicator sends to itself in the emulated mode).  Device
+// copies: hosted-to-hosted messages of an emulated handle.  Host transport (tests):
+// through host memory, synchronously.
+static hipError_t transfer_group(Numeric& N, const Msg* msgs, int64_t count, hipStream_t st) {
     hipError_t e = hipSuccess;
-    if (L.pcount > 0 && (e = launch_copy2d(N.d_copy, N.d_ctiles + L.poff, L.pcount, false, st)) != hipSuccess)
-        return e;
-    if (N.dry_comm) {
-        // timing projection of one rank alone: packing and unpacking, no transfer
-    } else if (N.xport) {
+    if (N.dry_comm || count == 0) return hipSuccess;
+    bool any_net = false;
+    for (int64_t q = 0; q < count; ++q) {
+        if (msgs[q].op != MSG_COPY) {
+            any_net = true;
+            continue;
+        }
+        e = hipMemcpyAsync(msgs[q].buf, msgs[q].src_buf, (size_t)msgs[q].count * sizeof(double),
+                           hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return e;
+    }
+    if (!any_net) return hipSuccess;
+    if (N.xport) {
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-        std::vector<std::vector<char>> host((size_t)L.count);
-        for (int64_t q = 0; q < L.count; ++q) {
-            const Msg& g = N.msgs[L.off + q];
+        std::vector<std::vector<char>> host((size_t)count);
+        for (int64_t q = 0; q < count; ++q) {
+            const Msg& g = msgs[q];
+            if (g.op == MSG_COPY) continue;
             const size_t nb = (size_t)g.count * sizeof(double);
             host[q].resize(std::max<size_t>(nb, 1));
-            if (g.is_send && (e = hipMemcpy(host[q].data(), g.buf, nb, hipMemcpyDeviceToHost)) != hipSuccess) return e;
-            if (N.xport(N.xport_ctx, g.is_send ? 0 : 1, g.peer, host[q].data(), (int64_t)nb) != 0) {
+            if (g.op == MSG_SEND && (e = hipMemcpy(host[q].data(), g.buf, nb, hipMemcpyDeviceToHost)) != hipSuccess)
+                return e;
+            if (N.xport(N.xport_ctx, g.op == MSG_SEND ? 0 : 1, g.peer, host[q].data(), (int64_t)nb) != 0) {
                 N.err = "host transport: post failed";
                 return hipErrorUnknown;
             }
@@ -318,35 +331,136 @@ hipError_t comm_launch(Numeric& N, const Launch& L) {
             N.err = "host transport: completion failed";
             return hipErrorUnknown;
         }
-        for (int64_t q = 0; q < L.count; ++q) {
-            const Msg& g = N.msgs[L.off + q];
-            if (!g.is_send &&
+        for (int64_t q = 0; q < count; ++q) {
+            const Msg& g = msgs[q];
+            if (g.op == MSG_RECV &&
                 (e = hipMemcpy(g.buf, host[q].data(), (size_t)g.count * sizeof(double), hipMemcpyHostToDevice)) !=
                     hipSuccess)
                 return e;
         }
-    } else {
-        if (!N.comm) return hipErrorInvalidValue;
-        ncclComm_t comm = (ncclComm_t)N.comm;
-        if (ncclGroupStart() != ncclSuccess) return hipErrorUnknown;
-        for (int64_t q = L.off; q < L.off + L.count; ++q) {
-            const Msg& g = N.msgs[q];
-            ncclResult_t r = g.is_send ? ncclSend(g.buf, (size_t)g.count, ncclDouble, g.peer, comm, st)
-                                       : ncclRecv(g.buf, (size_t)g.count, ncclDouble, g.peer, comm, st);
-            if (r != ncclSuccess) {
-                N.err = std::string("rccl p2p: ") + ncclGetErrorString(r);
-                (void)ncclGroupEnd();
-                return hipErrorUnknown;
-            }
-        }
-        ncclResult_t r = ncclGroupEnd();
+        return hipSuccess;
+    }
+    if (!N.comm) {
+        N.err = "no communicator";
+        return hipErrorInvalidValue;
+    }
+    ncclComm_t comm = (ncclComm_t)N.comm;
+    if (ncclGroupStart() != ncclSuccess) return hipErrorUnknown;
+    for (int64_t q = 0; q < count; ++q) {
+        const Msg& g = msgs[q];
+        if (g.op == MSG_COPY) continue;
+        ncclResult_t r = g.op == MSG_SEND ? ncclSend(g.buf, (size_t)g.count, ncclDouble, g.peer, comm, st)
+                                          : ncclRecv(g.buf, (size_t)g.count, ncclDouble, g.peer, comm, st);
         if (r != ncclSuccess) {
-            N.err = std::string("rccl group: ") + ncclGetErrorString(r);
+            N.err = std::string("rccl p2p: ") + ncclGetErrorString(r);
+            (void)ncclGroupEnd();
             return hipErrorUnknown;
         }
     }
+    ncclResult_t r = ncclGroupEnd();
+    if (r != ncclSuccess) {
+        N.err = std::string("rccl group: ") + ncclGetErrorString(r);
+        return hipErrorUnknown;
+    }
+    return hipSuccess;
+}
+
+// One comm step of the hosted ranks on the comm stream: pack the sends into their
+// staging slots, the transfer group, unpack the receives.
+hipError_t comm_launch(Numeric& N, const Launch& L) {
+    hipStream_t st = N.stream3;
+    hipError_t e = hipSuccess;
+    if (L.pcount > 0 && (e = launch_copy2d(N.d_copy, N.d_ctiles + L.poff, L.pcount, false, st)) != hipSuccess)
+        return e;
+    if ((e = transfer_group(N, N.msgs.data() + L.off, L.count, st)) != hipSuccess) return e;
     if (L.ucount > 0) return launch_copy2d(N.d_copy, N.d_ctiles + L.uoff, L.ucount, true, st);
     return hipSuccess;
+}
+
+// Global status of a one-rank-per-process handle: the minimum failing column over
+// the ranks (each rank's info word holds its own fronts' failures only).
+int64_t dist_min_info(Numeric& N, int32_t& info) {
+    if (N.xport) {
+        std::vector<int32_t> got((size_t)N.nranks, info);
+        for (int r = 0; r < N.nranks; ++r) {
+            if (r == N.rank) continue;
+            if (N.xport(N.xport_ctx, 0, r, &info, sizeof(int32_t)) != 0 ||
+                N.xport(N.xport_ctx, 1, r, &got[r], sizeof(int32_t)) != 0) {
+                N.err = "host transport: status exchange failed";
+                return SC_ERR_COMM;
+            }
+        }
+        if (N.xport(N.xport_ctx, 2, -1, nullptr, 0) != 0) {
+            N.err = "host transport: status exchange failed";
+            return SC_ERR_COMM;
+        }
+        for (int32_t v : got) info = std::min(info, v);
+        return SC_OK;
+    }
+    if (!N.comm) return SC_OK;
+    // info lives at d_info[0] (the value this rank saw); reduce into d_info[1]
+    ncclResult_t r = ncclAllReduce(N.d_info, N.d_info + 1, 1, ncclInt32, ncclMin, (ncclComm_t)N.comm, N.stream);
+    if (r != ncclSuccess) {
+        N.err = std::string("rccl allreduce: ") + ncclGetErrorString(r);
+        return SC_ERR_COMM;
+    }
+    if (hipMemcpyAsync(N.h_info + 1, N.d_info + 1, sizeof(int32_t), hipMemcpyDeviceToHost, N.stream) != hipSuccess ||
+        hipStreamSynchronize(N.stream) != hipSuccess) {
+        N.err = "status reduction: HIP error";
+        return SC_ERR_HIP;
+    }
+    info = N.h_info[1];
+    return SC_OK;
+}
+
+// Whole factor on every rank of a one-rank-per-process handle: each rank's panel
+// arena is contiguous, so the exchange is one message per rank pair; every rank
+// lands rank q's arena at gpanel + rank_base[q] (the gathered layout).
+int64_t dist_gather_panels(Numeric& N) {
+    const int64_t tot = N.rank_base.back();
+    if (!N.gpanel) {
+        void* p = nullptr;
+        hipError_t e = hipMalloc(&p, (size_t)std::max<int64_t>(tot, 1) * sizeof(double));
+        if (e != hipSuccess) {
+            N.err = std::string("hipMalloc(gathered factor): ") + hipGetErrorString(e);
+            return SC_ERR_DEVMEM;
+        }
+        N.allocs.push_back(p);
+        N.dev_bytes += tot * (int64_t)sizeof(double);
+        N.gpanel = (double*)p;
+        N.gpanel_owned = true;
+    }
+    const RankMem& R = N.R[0];
+    hipStream_t st = N.stream3 ? N.stream3 : N.stream;
+    if (hipMemcpyAsync(N.gpanel + N.rank_base[N.rank], R.P.panel_pool, (size_t)R.panel_total * sizeof(double),
+                       hipMemcpyDeviceToDevice, st) != hipSuccess) {
+        N.err = "gather: local copy failed";
+        return SC_ERR_HIP;
+    }
+    std::vector<Msg> m;
+    for (int q = 0; q < N.nranks; ++q) {
+        if (q == N.rank) continue;
+        // in rank order on both sides: pair (a, b) posts a's send and b's receive in the
+        // same relative order
+        Msg snd {};
+        snd.buf = R.P.panel_pool;
+        snd.count = R.panel_total;
+        snd.peer = q;
+        snd.op = MSG_SEND;
+        Msg rcv {};
+        rcv.buf = N.gpanel + N.rank_base[q];
+        rcv.count = N.rank_base[q + 1] - N.rank_base[q];
+        rcv.peer = q;
+        rcv.op = MSG_RECV;
+        m.push_back(snd);
+        m.push_back(rcv);
+    }
+    if (transfer_group(N, m.data(), (int64_t)m.size(), st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+        if (N.err.empty()) N.err = "gather: transfer failed";
+        return SC_ERR_COMM;
+    }
+    return SC_OK;
 }
 
 void comm_destroy(Numeric& N) {
@@ -356,13 +470,15 @@ void comm_destroy(Numeric& N) {
     }
 }
 
-// Multi-GPU handle: this process is `rank` of `nranks` (one GPU each).  Every rank
-// allocates the full pools (288 GB HBM per GPU holds them) but computes only its
-// part of the plan.  id128 != NULL: RCCL transport; xport != NULL: host-staged
-// transport (tests); neither: in-process emulation of all ranks (shared pools).
+// Multi-rank handle.  One process per GPU: this process is `rank` of `nranks`; id128
+// != NULL: RCCL transport; xport != NULL: host-staged transport (tests); DIST_DRY:
+// nothing moves (timing projection).  Emulated (emulate != 0): every rank in this
+// process on one device, each with its own memory plan and arenas, transfers as
+// device copies (emulate == 1) or as RCCL send / receive to self on a 1-rank
+// communicator (emulate == 2), so the whole message plan is exercised.
 i64 numeric_create_dist(const Symbolic& S, int device, int rank, int nranks, const void* id128,
-                        int32_t (*xport)(void*, int32_t, int32_t, void*, int64_t), void* xport_ctx, Numeric*& out,
-                        std::string& err) {
+                        int32_t (*xport)(void*, int32_t, int32_t, void*, int64_t), void* xport_ctx, int emulate,
+                        Numeric*& out, std::string& err) {
     out = nullptr;
     Numeric* Np = new (std::nothrow) Numeric();
     if (!Np) return SC_ERR_NOMEM;
@@ -375,31 +491,54 @@ i64 numeric_create_dist(const Symbolic& S, int device, int rank, int nranks, con
         return rc;
     }
     N.owner = N.D.owner;
-    if (xport == DIST_DRY) {
-        N.dry_comm = true;
-    } else if (xport) {
-        N.xport = xport;
-        N.xport_ctx = xport_ctx;
-    } else if (!id128) {
-        N.virt_ranks = nranks;  // shared pools, no transfers
-    } else if (nranks > 1) {
+    auto comm_init = [&](const ncclUniqueId& id, int n, int r) -> i64 {
         int dev = device;
         if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
         if (hipSetDevice(dev) != hipSuccess) {
             err = "hipSetDevice failed";
-            delete Np;
             return SC_ERR_HIP;
         }
-        ncclUniqueId id;
-        std::memcpy(&id, id128, sizeof(id));
         ncclComm_t comm = nullptr;
-        ncclResult_t r = ncclCommInitRank(&comm, nranks, id, rank);
-        if (r != ncclSuccess) {
-            err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
-            delete Np;
+        ncclResult_t r2 = ncclCommInitRank(&comm, n, id, r);
+        if (r2 != ncclSuccess) {
+            err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r2);
             return SC_ERR_COMM;
         }
         N.comm = comm;
+        return SC_OK;
+    };
+    if (emulate) {
+        N.emulated = true;
+        N.rank = 0;
+        N.emul_rccl = emulate == 2 ? 1 : 0;
+        if (N.emul_rccl) {
+            ncclUniqueId id;
+            if (ncclGetUniqueId(&id) != ncclSuccess) {
+                err = "ncclGetUniqueId failed";
+                delete Np;
+                return SC_ERR_COMM;
+            }
+            if ((rc = comm_init(id, 1, 0)) != SC_OK) {
+                delete Np;
+                return rc;
+            }
+        }
+    } else if (xport == DIST_DRY) {
+        N.dry_comm = true;
+    } else if (xport) {
+        N.xport = xport;
+        N.xport_ctx = xport_ctx;
+    } else if (id128) {
+        ncclUniqueId id;
+        std::memcpy(&id, id128, sizeof(id));
+        if ((rc = comm_init(id, nranks, rank)) != SC_OK) {
+            delete Np;
+            return rc;
+        }
+    } else {
+        err = "multi-rank handle without a transport";
+        delete Np;
+        return SC_ERR_ARG;
     }
     rc = numeric_init(N, S, device);
     if (rc != SC_OK) {

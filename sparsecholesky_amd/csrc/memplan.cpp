@@ -1,0 +1,268 @@
+// Device memory plan of one rank.
+//
+// The reference allocates each supernode's update block (UpdateBlock,
+// include/chol.hpp:1161-1169) for the duration of one supernode and scatters it
+// into the working matrix at once (apply_update, :1196-1216).  Here the
+// contribution block (CB) of a front lives from its assembly (level L) until its
+// parent's assembly (level Lp) reads it, and every region's lifetime is a closed
+// interval of assembly-tree levels, fixed by the static schedule.  A sweep over
+// the levels places the regions in one work arena: regions dead before level t are
+// freed before those born at t are placed (best fit, largest first), so offsets
+// are static (hipGraph-capturable) and memory is reused across levels.
+//
+// Lifetimes (L = level of s, Lp = level of its parent):
+//   single device           CB(s)                        [L, Lp]
+//   multi-rank, comm steps  a region a comm step of level L' touches stays live
+//                           through L' + 1: the comm stream runs ahead of or behind
+//                           the main stream within that window, and the schedule
+//                           makes the main stream wait for level L' 's steps before
+//                           level L' + 2 starts (numeric.cpp)
+//   owner of s, parent here CB(s)                        [L, Lp]
+//   owner of s, parent away CB(s), sent after level L    [L, L+1]
+//   parent's owner          CB(c) of a remote child c     [Lc, Lp] (received)
+//   CB rank of split s      its column blocks (compact)  [L, L+1]; in place in a
+//                           full-square CB(s) when it also owns the parent
+//                           R_LAND(s) (the L21 slabs)     [L, L+1]
+#include <algorithm>
+#include <map>
+#include <queue>
+
+#include "numeric.hpp"
+
+namespace sc {
+
+namespace {
+
+constexpr int64_t kAlign = 64;  // doubles (512 B): region starts stay 512-B aligned
+
+struct Req {
+    int64_t size;   // doubles, aligned
+    int32_t t0, t1; // closed lifetime
+    int64_t* out;
+};
+
+int64_t align_up(int64_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
+
+// Places the requests; returns the arena size; *live_max = the largest sum of
+// sizes live at one level (no placement can use less).
+int64_t place(std::vector<Req>& reqs, int64_t* live_max) {
+    if (reqs.empty()) {
+        if (live_max) *live_max = 0;
+        return 0;
+    }
+    std::sort(reqs.begin(), reqs.end(), [](const Req& a, const Req& b) {
+        return a.t0 != b.t0 ? a.t0 < b.t0 : a.size > b.size;
+    });
+    int32_t tmax = 0;
+    for (const Req& r : reqs) tmax = std::max(tmax, r.t1);
+    std::vector<int64_t> diff((size_t)tmax + 2, 0);
+    for (const Req& r : reqs) {
+        diff[r.t0] += r.size;
+        diff[r.t1 + 1] -= r.size;
+    }
+    int64_t cur = 0, lm = 0;
+    for (int32_t t = 0; t <= tmax; ++t) lm = std::max(lm, cur += diff[t]);
+    if (live_max) *live_max = lm;
+
+    // free list by offset (coalescing) and by size (best fit), kept in step
+    std::map<int64_t, int64_t> by_off;
+    std::multimap<int64_t, int64_t> by_size;
+    auto drop = [&](std::map<int64_t, int64_t>::iterator it) {
+        auto rg = by_size.equal_range(it->second);
+        for (auto q = rg.first; q != rg.second; ++q)
+            if (q->second == it->first) {
+                by_size.erase(q);
+                break;
+            }
+        by_off.erase(it);
+    };
+    auto add = [&](int64_t off, int64_t size) {
+        by_off.emplace(off, size);
+        by_size.emplace(size, off);
+    };
+    int64_t top = 0;
+    using Live = std::pair<int32_t, std::pair<int64_t, int64_t>>;  // (t1, (off, size))
+    std::priority_queue<Live, std::vector<Live>, std::greater<Live>> live;
+    auto release = [&](int64_t off, int64_t size) {
+        auto nx = by_off.lower_bound(off);
+        if (nx != by_off.end() && off + size == nx->first) {
+            size += nx->second;
+            drop(nx);
+        }
+        auto pv = by_off.lower_bound(off);
+        if (pv != by_off.begin()) {
+            --pv;
+            if (pv->first + pv->second == off) {
+                off = pv->first;
+                size += pv->second;
+                drop(pv);
+            }
+        }
+        if (off + size == top)  // free tail: lower the top
+            top = off;
+        else
+            add(off, size);
+    };
+    int64_t peak = 0;
+    for (size_t i = 0; i < reqs.size(); ++i) {
+        Req& r = reqs[i];
+        while (!live.empty() && live.top().first < r.t0) {
+            release(live.top().second.first, live.top().second.second);
+            live.pop();
+        }
+        auto bs = by_size.lower_bound(r.size);
+        int64_t off;
+        if (bs != by_size.end()) {
+            off = bs->second;
+            const int64_t rest = bs->first - r.size;
+            drop(by_off.find(off));
+            if (rest > 0) add(off + r.size, rest);
+        } else {
+            off = top;
+            top += r.size;
+            peak = std::max(peak, top);
+        }
+        *r.out = off;
+        live.push({r.t1, {off, r.size}});
+    }
+    return peak;
+}
+
+}  // namespace
+
+int64_t plan_rank_memory(const Symbolic& S, const DistPlan* D, int rank, RankMem& R,
+                         std::vector<PlacedRegion>* placed) {
+    const i32 ns = S.ns;
+    R.rank = rank;
+    R.panel_off.assign((size_t)ns, -1);
+    R.cb_off.assign((size_t)ns, -1);
+    R.land_off.assign((size_t)ns, -1);
+    R.blk_off.assign(D ? D->split_s.size() : 0, std::vector<int64_t>());
+    auto owner = [&](i32 s) { return D ? D->owner[s] : 0; };
+    int64_t off = 0;
+    for (i32 s = 0; s < ns; ++s)
+        if (owner(s) == rank) {
+            R.panel_off[s] = off;
+            off += (int64_t)S.sn_m[s] * S.w(s);
+        }
+    R.panel_total = off + PNB;
+    std::vector<Req> reqs;
+    auto req = [&](int64_t size, i32 t0, i32 t1, int64_t* out) { reqs.push_back({align_up(size), t0, t1, out}); };
+    for (i32 s = 0; s < ns; ++s) {
+        const int64_t mb = S.mb(s);
+        if (mb <= 0) continue;
+        const i32 L = S.level[s], p = S.sn_parent[s], Lp = S.level[p];
+        const bool mine = owner(s) == rank, here = owner(p) == rank;
+        const int64_t sq = mb * mb;
+        if (!D || D->split[s] < 0) {
+            if (mine)
+                req(sq, L, here ? Lp : L + 1, &R.cb_off[s]);
+            else if (here)
+                req(sq, L, Lp, &R.cb_off[s]);
+            continue;
+        }
+        const int sp = D->split[s];
+        const std::vector<i32>& cbr = D->cb_rank[sp];
+        bool cbrank = false;
+        for (i32 r : cbr) cbrank |= r == rank;
+        if (here)  // the parent's owner keeps the whole CB (its blocks computed in place)
+            req(sq, L, Lp, &R.cb_off[s]);
+        else if (mine)  // assembled, then sent to the CB ranks (STEP_INIT)
+            req(sq, L, L + 1, &R.cb_off[s]);
+        else if (cbrank) {
+            R.blk_off[sp].assign(cbr.size(), -1);
+            for (size_t jb = 0; jb < cbr.size(); ++jb) {
+                if (cbr[jb] != rank) continue;
+                const int64_t rows = mb - (int64_t)jb * D->cbb, cols = std::min<int64_t>(D->cbb, rows);
+                req(rows * cols, L, L + 1, &R.blk_off[sp][jb]);
+            }
+        }
+        if (cbrank) req(mb * S.w(s), L, L + 1, &R.land_off[s]);
+    }
+    R.work_total = place(reqs, &R.work_live_max);
+    if (placed)
+        for (const Req& q : reqs) placed->push_back({*q.out, q.size, q.t0, q.t1});
+    return SC_OK;
+}
+
+// Checks a plan: no two regions of one rank overlap in memory while both are live,
+// and every region lies inside the work arena.  Returns the number of violations.
+int64_t plan_check(const Symbolic& S, int nranks) {
+    DistPlan D;
+    if (nranks > 1 && dist_plan(S, nranks, D) != SC_OK) return -1;
+    int64_t bad = 0;
+    for (int r = 0; r < nranks; ++r) {
+        RankMem R;
+        std::vector<PlacedRegion> pl;
+        plan_rank_memory(S, nranks > 1 ? &D : nullptr, r, R, &pl);
+        int32_t tmax = 0;
+        for (const PlacedRegion& q : pl) {
+            tmax = std::max(tmax, q.t1);
+            if (q.off < 0 || q.off + q.size > R.work_total) ++bad;
+        }
+        std::vector<std::vector<int32_t>> at((size_t)tmax + 1);
+        for (size_t i = 0; i < pl.size(); ++i)
+            for (int32_t t = pl[i].t0; t <= pl[i].t1; ++t) at[t].push_back((int32_t)i);
+        for (auto& v : at) {
+            std::sort(v.begin(), v.end(), [&](int32_t a, int32_t b) { return pl[a].off < pl[b].off; });
+            for (size_t k = 1; k < v.size(); ++k)
+                if (pl[v[k - 1]].off + pl[v[k - 1]].size > pl[v[k]].off) ++bad;
+        }
+    }
+    return bad;
+}
+
+bool region_addr(const Symbolic& S, const DistPlan* D, const RankMem& R, int kind, int s, int row, int col,
+                 int& arena, int64_t& off, int64_t& ld) {
+    switch (kind) {
+        case R_PANEL:
+            if (R.panel_off[s] < 0) return false;
+            arena = 0;
+            ld = S.sn_m[s];
+            off = R.panel_off[s] + (int64_t)col * ld + row;
+            return true;
+        case R_LAND:
+            if (R.land_off[s] < 0) return false;
+            arena = 1;
+            ld = S.mb(s);
+            off = R.land_off[s] + (int64_t)col * ld + row;
+            return true;
+        case R_CB: {
+            arena = 1;
+            if (R.cb_off[s] >= 0) {
+                ld = S.mb(s);
+                off = R.cb_off[s] + (int64_t)col * ld + row;
+                return true;
+            }
+            if (!D || D->split[s] < 0) return false;
+            const std::vector<int64_t>& bo = R.blk_off[D->split[s]];
+            const int jb = col / D->cbb;
+            if (jb >= (int)bo.size() || bo[jb] < 0) return false;
+            const int r0 = jb * D->cbb;
+            ld = S.mb(s) - r0;
+            off = bo[jb] + (int64_t)(col - r0) * ld + (row - r0);
+            return row >= r0;
+        }
+    }
+    return false;
+}
+
+int64_t plan_memory_stats(const Symbolic& S, int nranks, int64_t* panel_doubles, int64_t* work_doubles,
+                          int64_t* work_lower_bound) {
+    if (nranks < 1) return SC_ERR_ARG;
+    DistPlan D;
+    if (nranks > 1) {
+        const int64_t rc = dist_plan(S, nranks, D);
+        if (rc != SC_OK) return rc;
+    }
+    for (int r = 0; r < nranks; ++r) {
+        RankMem R;
+        plan_rank_memory(S, nranks > 1 ? &D : nullptr, r, R, nullptr);
+        if (panel_doubles) panel_doubles[r] = R.panel_total;
+        if (work_doubles) work_doubles[r] = R.work_total;
+        if (work_lower_bound) work_lower_bound[r] = R.work_live_max;
+    }
+    return SC_OK;
+}
+
+}  // namespace sc

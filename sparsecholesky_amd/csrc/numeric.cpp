@@ -36,6 +36,7 @@ static int64_t upload(Numeric& N, const std::vector<T>& v, T*& dptr) {
         return SC_ERR_DEVMEM;
     }
     N.allocs.push_back(p);
+    N.dev_bytes += (int64_t)bytes;
     if (!v.empty()) {
         e = hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
         if (e != hipSuccess) {
@@ -55,6 +56,7 @@ static int64_t dalloc(Numeric& N, size_t bytes, void*& p) {
         return SC_ERR_DEVMEM;
     }
     N.allocs.push_back(p);
+    N.dev_bytes += (int64_t)std::max<size_t>(bytes, 8);
     return SC_OK;
 }
 
@@ -123,33 +125,49 @@ void xcd_order_tasks(int2* tiles, int64_t n, const GemmTask* tasks, int ntasks) 
     for (int64_t b = 0; b < n; ++b) tiles[b] = per[b % 8][b / 8];
 }
 
-// Staging slots of this rank's messages (patched to device addresses once the
-// staging pool is allocated): slot < 0 = the message moves in place.
+// Staging slots of the hosted ranks' messages (patched to device addresses once
+// the staging pool is allocated): slot < 0 = the buffer is the region itself.
 struct CommBuild {
     std::vector<Copy2D> copies;
     std::vector<int64_t> copy_slot;
     std::vector<int2> ctiles;
-    std::vector<int64_t> msg_slot;
+    std::vector<int64_t> msg_slot, msg_src_slot;
     int64_t stage_total = 0;
 };
 
-static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vector<int2>& asmv,
-                              std::vector<int2>& potrf, std::vector<int4>& trsm,
-                              std::vector<GemmTask>& gemm, std::vector<int2>& tiles, CommBuild& cbld) {
+struct SchedBuild {
+    std::vector<int32_t> small;
+    std::vector<int2> asmv, potrf;
+    std::vector<int4> trsm;
+    std::vector<GemmTask> gemm;
+    std::vector<int2> tiles;
+    CommBuild cb;
+};
+
+static int64_t build_schedule(Numeric& N, SchedBuild& B) {
     const Symbolic& S = *N.S;
+    std::vector<int32_t>& small = B.small;
+    std::vector<int2>& asmv = B.asmv;
+    std::vector<int2>& potrf = B.potrf;
+    std::vector<int4>& trsm = B.trsm;
+    std::vector<GemmTask>& gemm = B.gemm;
+    std::vector<int2>& tiles = B.tiles;
+    CommBuild& cbld = B.cb;
     const int NBO = std::max(PNB, (S.opt.panel_nb_outer / PNB) * PNB);
     std::vector<std::vector<int32_t>> by_level((size_t)S.nlevels);
     for (int32_t s = 0; s < S.ns; ++s) by_level[S.level[s]].push_back(s);
-    double* panel_pool = N.P.panel_pool;
-    double* cb_pool = N.P.cb_pool;
-    // multi-GPU plan lookups
+    // multi-rank plan lookups
     const DistPlan& D = N.D;
-    const bool real_comm = !N.owner.empty() && N.virt_ranks <= 1;
-    auto is_split = [&](int32_t s) { return !D.split.empty() && D.split[s] >= 0; };
+    const bool multi = !N.owner.empty();
+    const DistPlan* Dp = multi ? &D : nullptr;
+    auto is_split = [&](int32_t s) { return multi && D.split[s] >= 0; };
+    std::vector<int32_t> hosted_of((size_t)std::max(N.nranks, 1), -1);  // rank -> index into N.R
+    for (size_t v = 0; v < N.R.size(); ++v) hosted_of[N.R[v].rank] = (int32_t)v;
     std::vector<int32_t> init_step, slab_step0, early_step0, deliver_step((size_t)S.nlevels, -1);
     std::vector<std::vector<int>> early_ev((size_t)S.ns);  // sender: event after each CB column group
     std::vector<int64_t> step_beg;
-    if (!N.owner.empty()) {
+    std::vector<char> emitted;
+    if (multi) {
         init_step.assign((size_t)S.ns, -1);
         slab_step0.assign((size_t)S.ns, -1);
         early_step0.assign((size_t)S.ns, -1);
@@ -163,7 +181,15 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         step_beg.assign(D.steps.size() + 1, 0);
         for (const DistMsg& g : D.msgs) step_beg[g.step + 1]++;
         for (size_t i = 0; i < D.steps.size(); ++i) step_beg[i + 1] += step_beg[i];
+        emitted.assign(D.steps.size(), 0);
     }
+    // device address of logical element (row, col) of a region on hosted rank v
+    auto addr = [&](int v, int kind, int s, int row, int col, int64_t& ld) -> double* {
+        int arena = 0;
+        int64_t off = 0;
+        if (!region_addr(S, Dp, N.R[v], kind, s, row, col, arena, off, ld)) return nullptr;
+        return (arena == 0 ? N.R[v].P.panel_pool : N.R[v].P.cb_pool) + off;
+    };
     auto push_gemm_launch = [&](int kind, int level, const std::vector<GemmTask>& tasks, int big,
                                 double flops, int strm = 0) {
         if (tasks.empty()) return;
@@ -174,13 +200,10 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         L.off = (int64_t)gemm.size();
         // 128x128 tiles on 8 waves when every task is at least 256 wide (random data,
         // 16384 x 4096: 61 vs 52 TF/s for 64x64); 64x64 on 4 waves for narrow updates
-        int minN = INT32_MAX, minK = INT32_MAX;
-        for (auto& t : tasks) {
-            minN = std::min(minN, (int)t.N);
-            minK = std::min(minK, (int)t.K);
-        }
-        const bool wide_deep = minN >= 256;
-        L.bt = (S.opt.syrk_tile == 128 || (S.opt.syrk_tile == 0 && wide_deep)) ? SYRK_BT_LARGE : SYRK_BT_SMALL;
+        int minN = INT32_MAX;
+        for (auto& t : tasks) minN = std::min(minN, (int)t.N);
+        const bool wide = minN >= 256;
+        L.bt = (S.opt.syrk_tile == 128 || (S.opt.syrk_tile == 0 && wide)) ? SYRK_BT_LARGE : SYRK_BT_SMALL;
         L.toff = (int64_t)tiles.size();
         for (size_t q = 0; q < tasks.size(); ++q) {
             append_tiles(tiles, (int)q, tasks[q].M, tasks[q].N, L.bt);
@@ -209,49 +232,86 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         L.count = ev;
         N.sched.push_back(L);
     };
-    // this rank's part of comm step `id` on the comm stream (strm 2): it waits for
-    // the main stream's work so far (the data it sends), and the main stream waits
-    // for it when it receives.  Messages keep the plan order, so every peer pair
-    // posts its matching sends and receives in the same order.
+    // The hosted ranks' part of comm step `id` on the comm stream (strm 2), emitted
+    // once, at the first call (the sender's point in an emulated schedule).  Sends
+    // wait for the main stream's work so far (their data); the main stream waits
+    // for the step when it receives.  Messages keep the plan order, so every peer
+    // pair posts its matching sends and receives in the same order.
     auto emit_step = [&](int32_t id, int send_ev = -1) {
-        if (!real_comm || id < 0) return;
+        if (!multi || id < 0 || emitted[id]) return;
+        emitted[id] = 1;
         Launch L {};
         L.kind = L_COMM;
         L.level = D.steps[id].level;
         L.strm = 2;
         L.step = id;
         L.off = (int64_t)N.msgs.size();
-        int nrecv = 0;
+        bool any_send = false, any_recv = false;
         std::vector<int32_t> pack_d, unpack_d;  // copy descriptors of the sends / receives
+        // (buffer, staging slot) of one end: the region itself when contiguous
+        auto end_of = [&](int v, int kind, int s, int row, int col, int rows, int cols, bool pack, double*& buf,
+                          int64_t& slot) {
+            int64_t ld = 0;
+            double* a = addr(v, kind, s, row, col, ld);
+            if (!a) return false;
+            if (ld == rows || cols == 1) {
+                buf = a;
+                slot = -1;
+                return true;
+            }
+            buf = nullptr;
+            slot = cbld.stage_total;
+            Copy2D c {};
+            c.a = a;
+            c.lda = ld;
+            c.rows = rows;
+            c.cols = cols;
+            (pack ? pack_d : unpack_d).push_back((int32_t)cbld.copies.size());
+            cbld.copies.push_back(c);
+            cbld.copy_slot.push_back(slot);
+            cbld.stage_total += (int64_t)rows * cols;
+            return true;
+        };
         for (int64_t q = step_beg[id]; q < step_beg[id + 1]; ++q) {
             const DistMsg& g = D.msgs[q];
-            const bool snd = g.src == N.rank, rcv = g.dst == N.rank;
-            if (!snd && !rcv) continue;
-            double* base = (g.pool == 0 ? panel_pool : cb_pool) + g.off;
+            const int vs = hosted_of[g.src], vd = hosted_of[g.dst];
+            if (vs < 0 && vd < 0) continue;
             const int64_t cnt = (int64_t)g.rows * g.cols;
-            Msg m {};
-            m.count = cnt;
-            m.peer = snd ? g.dst : g.src;
-            m.is_send = snd ? 1 : 0;
-            m.child = g.s;
-            nrecv += rcv ? 1 : 0;
-            if (g.ld == g.rows || g.cols == 1) {  // contiguous: moves in place
-                m.buf = base;
-                N.msgs.push_back(m);
-                cbld.msg_slot.push_back(-1);
-                continue;
+            double *sb = nullptr, *db = nullptr;
+            int64_t ss = -1, ds = -1;
+            if (vs >= 0 && !end_of(vs, g.skind, g.s, g.srow, g.scol, g.rows, g.cols, true, sb, ss)) {
+                N.err = "comm plan: send region missing";
+                return;
             }
-            N.msgs.push_back(m);
-            cbld.msg_slot.push_back(cbld.stage_total);
-            Copy2D c {};
-            c.a = base;
-            c.lda = g.ld;
-            c.rows = g.rows;
-            c.cols = g.cols;
-            (snd ? pack_d : unpack_d).push_back((int32_t)cbld.copies.size());
-            cbld.copies.push_back(c);
-            cbld.copy_slot.push_back(cbld.stage_total);
-            cbld.stage_total += cnt;
+            if (vd >= 0 && !end_of(vd, g.dkind, g.s, g.drow, g.dcol, g.rows, g.cols, false, db, ds)) {
+                N.err = "comm plan: receive region missing";
+                return;
+            }
+            any_send |= vs >= 0;
+            any_recv |= vd >= 0;
+            auto push = [&](double* b, int64_t slot, double* src, int64_t src_slot, int peer, int op) {
+                Msg m {};
+                m.buf = b;
+                m.src_buf = src;
+                m.count = cnt;
+                m.peer = peer;
+                m.op = op;
+                N.msgs.push_back(m);
+                cbld.msg_slot.push_back(slot);
+                cbld.msg_src_slot.push_back(src_slot);
+            };
+            if (vs >= 0 && vd >= 0) {  // both ends in this process (emulated ranks)
+                if (N.emul_rccl) {
+                    push(sb, ss, nullptr, -1, 0, MSG_SEND);
+                    push(db, ds, nullptr, -1, 0, MSG_RECV);
+                } else {
+                    push(db, ds, sb, ss, 0, MSG_COPY);
+                }
+            } else if (vs >= 0) {
+                push(sb, ss, nullptr, -1, g.dst, MSG_SEND);
+            } else {
+                push(db, ds, nullptr, -1, g.src, MSG_RECV);
+            }
         }
         L.count = (int32_t)((int64_t)N.msgs.size() - L.off);
         if (L.count == 0) return;
@@ -266,19 +326,19 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         add_tiles(unpack_d);
         L.ucount = (int32_t)((int64_t)cbld.ctiles.size() - L.uoff);
         // sends wait for the data (default: everything the main stream has so far);
-        // receive-only steps post right away (their targets are never touched by this
-        // rank's compute before the step, and the comm stream joins the main stream at
-        // the start and end of every factorization)
-        if (nrecv < L.count) push_wait(2, send_ev >= 0 ? send_ev : push_record(0));
+        // receive-only steps post as soon as the main stream has finished the previous
+        // level (the per-level guard below)
+        if (any_send) push_wait(2, send_ev >= 0 ? send_ev : push_record(0));
         N.sched.push_back(L);
-        if (nrecv > 0) push_wait(0, push_record(2));
+        if (any_recv) push_wait(0, push_record(2));
     };
-    auto is_early_sender = [&](int32_t s) {
-        return real_comm && !D.early.empty() && D.early[s] && D.owner[s] == N.rank;
+    auto is_early_sender = [&](int32_t s, int v) {
+        return multi && D.early[s] && D.owner[s] == N.R[v].rank;
     };
-    // CB rank `who` of split front s: per final panel slab, CB -= L21_k L21_k^T on
-    // the column blocks it owns (K = slab width)
-    auto emit_cb_rank = [&](int32_t lev, int32_t s, int who) {
+    // CB rank (hosted index v) of split front s: per final panel slab, CB -= L21_k
+    // L21_k^T on the column blocks it owns (K = slab width), from its R_LAND copy
+    auto emit_cb_rank = [&](int32_t lev, int32_t s, int v) {
+        const int who = N.R[v].rank;
         const std::vector<int32_t>& cbr = D.cb_rank[D.split[s]];
         const int w = S.w(s), m = S.sn_m[s], mb = m - w;
         emit_step(init_step[s]);
@@ -291,10 +351,11 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
                 if (cbr[jb] != who) continue;
                 const int r0 = jb * D.cbb;
                 GemmTask t {};
-                t.C = cb_pool + S.cb_off[s] + (int64_t)r0 * mb + r0;
-                t.A = panel_pool + S.panel_off[s] + (int64_t)k0 * m + w + r0;
-                t.ldc = mb;
-                t.lda = m;
+                int64_t ldc = 0, lda = 0;
+                t.C = addr(v, R_CB, s, r0, r0, ldc);
+                t.A = addr(v, R_LAND, s, r0, k0, lda);
+                t.ldc = ldc;
+                t.lda = lda;
                 t.M = mb - r0;
                 t.N = std::min(D.cbb, mb - r0);
                 t.K = k1 - k0;
@@ -304,13 +365,18 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             push_gemm_launch(L_CB, lev, cbt, w >= 256 ? 1 : 0, fl);
         }
     };
-    // one level's fronts (already filtered to the ranks this process runs)
-    auto emit_level = [&](int32_t lev, const std::vector<int32_t>& nodes) {
+    // one level's fronts of hosted rank v
+    auto emit_level = [&](int32_t lev, const std::vector<int32_t>& nodes, int v) {
+        double* panel_pool = N.R[v].P.panel_pool;
+        double* cb_pool = N.R[v].P.cb_pool;
+        const std::vector<int64_t>& poff = N.R[v].panel_off;
+        const std::vector<int64_t>& coff = N.R[v].cb_off;
         // small fronts by LDS bucket
         for (int b : {32, 64, 96, 128}) {
             Launch L {};
             L.kind = L_SMALL;
             L.level = lev;
+            L.vr = v;
             L.off = (int64_t)small.size();
             L.maxm = b;
             for (int32_t s : nodes)
@@ -330,6 +396,7 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             Launch L {};
             L.kind = L_ASM;
             L.level = lev;
+            L.vr = v;
             L.big = tiled;
             L.off = (int64_t)asmv.size();
             for (int32_t s : large) {
@@ -356,7 +423,7 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         // (stream 1), which overlaps the next slab's factorization.  A later outer
         // update of overlapping columns waits for the stream-1 work first.
         int b_pending = -1;
-        auto add_update = [&](std::vector<GemmTask>& v, double& fl, double* pan, int m, int c_lo, int c_hi, int ka,
+        auto add_update = [&](std::vector<GemmTask>& vec, double& fl, double* pan, int m, int c_lo, int c_hi, int ka,
                               int kb) {
             if (c_hi <= c_lo || kb <= ka) return;
             GemmTask t {};
@@ -367,17 +434,19 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             t.M = m - c_lo;
             t.N = c_hi - c_lo;
             t.K = kb - ka;
-            v.push_back(t);
+            vec.push_back(t);
             fl += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
         };
         for (int k0 = 0; k0 < maxw; k0 += PNB) {
             Launch Lp {};
             Lp.kind = L_POTRF;
             Lp.level = lev;
+            Lp.vr = v;
             Lp.off = (int64_t)potrf.size();
             Launch Lt {};
             Lt.kind = L_TRSM;
             Lt.level = lev;
+            Lt.vr = v;
             Lt.off = (int64_t)trsm.size();
             std::vector<GemmTask> upd, outer_a, outer_b;
             std::vector<int4> trsm_part;  // partial last blocks: own launch (big = 1)
@@ -390,7 +459,7 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
                 potrf.push_back(make_int2(s, k0));
                 for (int r0 = k1; r0 < m; r0 += TRSM_ROWS)
                     (nb < PNB ? trsm_part : trsm).push_back(make_int4(s, k0, r0, 0));
-                double* pan = panel_pool + S.panel_off[s];
+                double* pan = panel_pool + poff[s];
                 const int slab0 = (k0 / NBO) * NBO;
                 const int slab1 = std::min(w, slab0 + NBO);
                 if (k1 < slab1 && S.opt.inner_order == 1) {
@@ -450,12 +519,12 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
         // early-delivery children: the CB SYRK in column groups, an event after each
         // (the group's comm sub-step waits for exactly that event)
         for (int32_t s : large) {
-            if (!is_early_sender(s)) continue;
+            if (!is_early_sender(s, v)) continue;
             const int w = S.w(s), m = S.sn_m[s], mb = m - w;
             for (int j0 = 0; j0 < mb; j0 += D.early_gw) {
                 GemmTask t {};
-                t.C = cb_pool + S.cb_off[s] + (int64_t)j0 * mb + j0;
-                t.A = panel_pool + S.panel_off[s] + w + j0;
+                t.C = cb_pool + coff[s] + (int64_t)j0 * mb + j0;
+                t.A = panel_pool + poff[s] + w + j0;
                 t.ldc = mb;
                 t.lda = m;
                 t.M = mb - j0;
@@ -472,10 +541,10 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             double fl = 0.0;
             for (int32_t s : large) {
                 const int w = S.w(s), m = S.sn_m[s], mb = m - w;
-                if (mb <= 0 || (w >= 256) != (big == 1) || is_split(s) || is_early_sender(s)) continue;
+                if (mb <= 0 || (w >= 256) != (big == 1) || is_split(s) || is_early_sender(s, v)) continue;
                 GemmTask t {};
-                t.C = cb_pool + S.cb_off[s];
-                t.A = panel_pool + S.panel_off[s] + w;
+                t.C = cb_pool + coff[s];
+                t.A = panel_pool + poff[s] + w;
                 t.ldc = mb;
                 t.lda = m;
                 t.M = mb;
@@ -486,43 +555,54 @@ static int64_t build_schedule(Numeric& N, std::vector<int32_t>& small, std::vect
             }
             push_gemm_launch(L_CB, lev, cbt, big, fl);
         }
-        };
-    if (real_comm) push_wait(2, push_record(0));  // previous factorization's reads are done
+    };
+    if (multi) push_wait(2, push_record(0));  // previous factorization's reads are done
+    // multi-rank work-arena reuse guard (memplan.cpp): the comm steps of level L run
+    // after the main stream has finished level L - 1, and the main stream starts level
+    // L + 2 only after the comm steps of level L, so a region a step of level L touches
+    // is never reused before level L + 2
+    std::vector<int> comm_done((size_t)S.nlevels, -1);
     for (int32_t lev = 0; lev < S.nlevels; ++lev) {
-        if (N.owner.empty()) {
-            emit_level(lev, by_level[lev]);
-            continue;
+        if (multi) {
+            if (lev >= 2 && comm_done[lev - 2] >= 0) push_wait(0, comm_done[lev - 2]);
+            push_wait(2, push_record(0));
         }
-        const int nr = N.virt_ranks > 1 ? N.virt_ranks : 1;
-        for (int r = 0; r < nr; ++r) {
-            const int who = N.virt_ranks > 1 ? r : N.rank;
+        for (size_t v = 0; v < N.R.size(); ++v) {
+            if (!multi) {
+                emit_level(lev, by_level[lev], (int)v);
+                continue;
+            }
             std::vector<int32_t> mine;
             for (int32_t s : by_level[lev])
-                if (N.owner[s] == who) mine.push_back(s);
-            if (!mine.empty()) emit_level(lev, mine);
+                if (D.owner[s] == N.R[v].rank) mine.push_back(s);
+            if (!mine.empty()) emit_level(lev, mine, (int)v);
         }
-        // contribution-block ranks of this level's split fronts (in the emulation
-        // after the owners' panels: shared pools, nothing moves)
+        if (!multi) continue;
+        // contribution-block ranks of this level's split fronts (emulated: after the
+        // owners' panels, whose steps already moved the data)
         for (int32_t s : by_level[lev]) {
             if (!is_split(s)) continue;
             const std::vector<int32_t>& cbr = D.cb_rank[D.split[s]];
-            for (int r = 0; r < nr; ++r) {
-                const int who = N.virt_ranks > 1 ? r : N.rank;
+            for (size_t v = 0; v < N.R.size(); ++v) {
+                const int who = N.R[v].rank;
                 if (who != D.owner[s] && std::find(cbr.begin(), cbr.end(), who) != cbr.end())
-                    emit_cb_rank(lev, s, who);
+                    emit_cb_rank(lev, s, (int)v);
             }
         }
-        // contribution blocks that leave / enter this rank after this level: early
-        // children's column groups first, then the rest
+        // contribution blocks that leave / enter the hosted ranks after this level:
+        // early children's column groups first, then the rest
         for (int32_t c : by_level[lev]) {
-            if (D.early.empty() || !D.early[c] || early_step0[c] < 0) continue;
+            if (!D.early[c] || early_step0[c] < 0) continue;
             const int ng = (S.mb(c) + D.early_gw - 1) / D.early_gw;
+            const int vs = hosted_of[D.owner[c]];
             for (int g = 0; g < ng; ++g)
-                emit_step(early_step0[c] + g, is_early_sender(c) ? early_ev[c][g] : -1);
+                emit_step(early_step0[c] + g, vs >= 0 && !early_ev[c].empty() ? early_ev[c][g] : -1);
         }
         emit_step(deliver_step[lev]);
+        comm_done[lev] = push_record(2);
     }
-    if (real_comm) push_wait(0, push_record(2));  // join the comm stream (its last sends)
+    if (multi) push_wait(0, push_record(2));  // join the comm stream (its last sends)
+    if (!N.err.empty()) return SC_ERR_ARG;
     return SC_OK;
 }
 
@@ -538,6 +618,22 @@ int64_t numeric_create(const Symbolic& S, int device, Numeric*& out, std::string
     }
     out = Np;
     return SC_OK;
+}
+
+// Gathered panel layout: every rank's arena back to back (rank_base), each arena the
+// panels of the supernodes the rank owns in supernode order (plan_rank_memory).
+static void panel_layout(const Symbolic& S, const std::vector<int32_t>& owner, int nranks,
+                         std::vector<int64_t>& rank_base, std::vector<int64_t>& gpo) {
+    std::vector<int64_t> tot((size_t)nranks, 0);
+    gpo.assign((size_t)S.ns, 0);
+    for (int32_t s = 0; s < S.ns; ++s) {
+        const int r = owner.empty() ? 0 : owner[s];
+        gpo[s] = tot[r];
+        tot[r] += (int64_t)S.sn_m[s] * S.w(s);
+    }
+    rank_base.assign((size_t)nranks + 1, 0);
+    for (int r = 0; r < nranks; ++r) rank_base[r + 1] = rank_base[r] + tot[r] + PNB;
+    for (int32_t s = 0; s < S.ns; ++s) gpo[s] += rank_base[owner.empty() ? 0 : owner[s]];
 }
 
 int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
@@ -560,17 +656,17 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
         N.err = "hipSetDevice failed";
         return fail(SC_ERR_HIP);
     }
+    const bool multi = !N.owner.empty();
     // critical path (assembly, POTRF/TRSM chain, next-slab updates) on the high
     // priority stream; the overlapped trailing updates on the low priority one
     int prio_lo = 0, prio_hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     bool ok = hipStreamCreateWithPriority(&N.stream, hipStreamNonBlocking, prio_hi) == hipSuccess;
     if (ok) ok = hipStreamCreateWithPriority(&N.stream2, hipStreamNonBlocking, prio_lo) == hipSuccess;
-    // multi-GPU comm stream.  Only there: one more stream on the device costs 13.5%
+    // comm stream only on multi-rank handles: one more stream on the device costs 13.5%
     // under hipGraph replay (569 -> 649 ms at 128^3, any priority, any
-    // GPU_MAX_HW_QUEUES) though nothing runs on it; eager runs (multi-GPU) see 0.5%.
-    if (ok && !N.owner.empty() && N.virt_ranks <= 1)
-        ok = hipStreamCreateWithPriority(&N.stream3, hipStreamNonBlocking, prio_hi) == hipSuccess;
+    // GPU_MAX_HW_QUEUES) though nothing runs on it; eager runs (multi-rank) see 0.5%.
+    if (ok && multi) ok = hipStreamCreateWithPriority(&N.stream3, hipStreamNonBlocking, prio_hi) == hipSuccess;
     if (!ok) {
         N.err = "hipStreamCreate failed";
         return fail(SC_ERR_HIP);
@@ -578,58 +674,92 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     N.use_graph = S.opt.use_graph != 0;
     const int32_t ns = S.ns;
     int64_t rc;
-    DevPlan& P = N.P;
     static_assert(ASM_ROWS == kAsmRows, "assembly row tile");
     for (int32_t s = 0; s < S.ns; ++s)
         if (S.sn_m[s] >= (1 << 20)) {  // assembly task encoding: 16-bit column block index
             N.err = "front with >= 2^20 rows is not supported";
             return fail(SC_ERR_NOTIMPL);
         }
+    // ---- memory plan of the hosted ranks ----
+    N.R.clear();
+    if (!multi) {
+        N.R.resize(1);
+    } else if (N.emulated) {
+        N.R.resize((size_t)N.nranks);
+    } else {
+        N.R.resize(1);
+    }
+    for (size_t v = 0; v < N.R.size(); ++v) {
+        const int r = (multi && N.emulated) ? (int)v : (multi ? N.rank : 0);
+        plan_rank_memory(S, multi ? &N.D : nullptr, r, N.R[v]);
+    }
+    panel_layout(S, N.owner, multi ? N.nranks : 1, N.rank_base, N.gpo);
+    // ---- shared plan arrays ----
+    DevPlan P0 {};
     int32_t *d_sn_start, *d_sn_m, *d_child_ptr, *d_child_list, *d_relind, *d_apos, *d_relbnd;
-    int64_t *d_panel_off, *d_cb_off, *d_rel_ptr, *d_aptr, *d_asrc, *d_rbptr;
+    int64_t *d_rel_ptr, *d_aptr, *d_asrc, *d_rbptr;
     if ((rc = upload(N, S.sn_start, d_sn_start)) || (rc = upload(N, S.sn_m, d_sn_m)) ||
-        (rc = upload(N, S.panel_off, d_panel_off)) || (rc = upload(N, S.cb_off, d_cb_off)) ||
         (rc = upload(N, S.child_ptr, d_child_ptr)) || (rc = upload(N, S.child_list, d_child_list)) ||
         (rc = upload(N, S.rel_ptr, d_rel_ptr)) || (rc = upload(N, S.relind, d_relind)) ||
         (rc = upload(N, S.rb_ptr, d_rbptr)) || (rc = upload(N, S.rel_bnd, d_relbnd)) ||
         (rc = upload(N, S.a_ptr, d_aptr)) || (rc = upload(N, S.a_pos, d_apos)) ||
-        (rc = upload(N, S.a_src, d_asrc)))
+        (rc = upload(N, S.a_src, d_asrc)) || (rc = upload(N, N.gpo, N.d_gpo)))
         return fail(rc);
-    P.sn_start = d_sn_start;
-    P.sn_m = d_sn_m;
-    P.panel_off = d_panel_off;
-    P.cb_off = d_cb_off;
-    P.child_ptr = d_child_ptr;
-    P.child_list = d_child_list;
-    P.rel_ptr = d_rel_ptr;
-    P.relind = d_relind;
-    P.rb_ptr = d_rbptr;
-    P.rel_bnd = d_relbnd;
-    P.a_ptr = d_aptr;
-    P.a_pos = d_apos;
-    P.a_src = d_asrc;
+    P0.sn_start = d_sn_start;
+    P0.sn_m = d_sn_m;
+    P0.child_ptr = d_child_ptr;
+    P0.child_list = d_child_list;
+    P0.rel_ptr = d_rel_ptr;
+    P0.relind = d_relind;
+    P0.rb_ptr = d_rbptr;
+    P0.rel_bnd = d_relbnd;
+    P0.a_ptr = d_aptr;
+    P0.a_pos = d_apos;
+    P0.a_src = d_asrc;
     void* p = nullptr;
-    // + PNB doubles: the panel TRSM reads L11 columns unconditionally (rows past the
-    // block feed only registers that are never stored)
-    if ((rc = dalloc(N, (size_t)(S.panel_off[ns] + PNB) * sizeof(double), p))) return fail(rc);
-    P.panel_pool = (double*)p;
-    if ((rc = dalloc(N, (size_t)S.cb_off[ns] * sizeof(double), p))) return fail(rc);
-    P.cb_pool = (double*)p;
     if ((rc = dalloc(N, 64, p))) return fail(rc);
-    P.info = (int32_t*)p;
+    N.d_info = (int32_t*)p;
+    P0.info = N.d_info;
+    if (hipHostMalloc((void**)&N.h_info, sizeof(int32_t) * 16, hipHostMallocDefault) != hipSuccess) {
+        N.err = "hipHostMalloc failed";
+        return fail(SC_ERR_NOMEM);
+    }
+    // ---- pools: the hosted ranks' panel arenas back to back in one allocation (so an
+    // emulated handle's allocation IS the gathered factor), work arenas likewise ----
+    int64_t ptot = 0, wtot = 0;
+    for (const RankMem& R : N.R) {
+        ptot += R.panel_total;
+        wtot += R.work_total;
+    }
+    if ((rc = dalloc(N, (size_t)ptot * sizeof(double), p))) return fail(rc);
+    double* pbase = (double*)p;
+    if ((rc = dalloc(N, (size_t)std::max<int64_t>(wtot, 1) * sizeof(double), p))) return fail(rc);
+    double* wbase = (double*)p;
+    int64_t po = 0, wo = 0;
+    for (RankMem& R : N.R) {
+        R.P = P0;
+        R.P.panel_pool = pbase + po;
+        R.P.cb_pool = wbase + wo;
+        po += R.panel_total;
+        wo += R.work_total;
+        int64_t* dp = nullptr;
+        if ((rc = upload(N, R.panel_off, dp))) return fail(rc);
+        R.P.panel_off = dp;
+        if ((rc = upload(N, R.cb_off, dp))) return fail(rc);
+        R.P.cb_off = dp;
+    }
+    if (!multi || N.emulated) N.gpanel = pbase;  // gathered layout == the arenas
 
-    std::vector<int32_t> small;
-    std::vector<int2> asmv, potrf;
-    std::vector<int4> trsm;
-    std::vector<GemmTask> gemm;
-    std::vector<int2> tiles;
-    CommBuild cbld;
-    if ((rc = build_schedule(N, small, asmv, potrf, trsm, gemm, tiles, cbld))) return fail(rc);
-    if (cbld.stage_total > 0) {  // multi-GPU: packed staging slots of this rank's messages
+    SchedBuild B;
+    if ((rc = build_schedule(N, B))) return fail(rc);
+    CommBuild& cbld = B.cb;
+    if (cbld.stage_total > 0) {  // multi-rank: packed staging slots of the hosted ranks' messages
         if ((rc = dalloc(N, (size_t)cbld.stage_total * sizeof(double), p))) return fail(rc);
         N.staging = (double*)p;
-        for (size_t q = 0; q < N.msgs.size(); ++q)
+        for (size_t q = 0; q < N.msgs.size(); ++q) {
             if (cbld.msg_slot[q] >= 0) N.msgs[q].buf = N.staging + cbld.msg_slot[q];
+            if (cbld.msg_src_slot[q] >= 0) N.msgs[q].src_buf = N.staging + cbld.msg_src_slot[q];
+        }
         for (size_t q = 0; q < cbld.copies.size(); ++q) cbld.copies[q].b = N.staging + cbld.copy_slot[q];
     }
     if ((rc = upload(N, cbld.copies, N.d_copy)) || (rc = upload(N, cbld.ctiles, N.d_ctiles))) return fail(rc);
@@ -645,14 +775,17 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
             N.err = "hipEventCreate failed";
             return fail(SC_ERR_HIP);
         }
-    if ((rc = upload(N, small, N.d_small)) || (rc = upload(N, asmv, N.d_asm)) ||
-        (rc = upload(N, potrf, N.d_potrf)) || (rc = upload(N, trsm, N.d_trsm)) ||
-        (rc = upload(N, gemm, N.d_gemm)) || (rc = upload(N, tiles, N.d_tiles)))
+    if ((rc = upload(N, B.small, N.d_small)) || (rc = upload(N, B.asmv, N.d_asm)) ||
+        (rc = upload(N, B.potrf, N.d_potrf)) || (rc = upload(N, B.trsm, N.d_trsm)) ||
+        (rc = upload(N, B.gemm, N.d_gemm)) || (rc = upload(N, B.tiles, N.d_tiles)))
         return fail(rc);
+    (void)ns;
     return SC_OK;
 }
 
 hipError_t comm_launch(Numeric& N, const Launch& L);  // dist.cpp
+int64_t dist_min_info(Numeric& N, int32_t& info);      // dist.cpp
+int64_t dist_gather_panels(Numeric& N);                // dist.cpp
 
 static hipStream_t stream_of(const Numeric& N, int strm) {
     return strm == 2 ? N.stream3 : strm == 1 ? N.stream2 : N.stream;
@@ -666,13 +799,13 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
         case L_WAIT:
             return hipStreamWaitEvent(st, N.sync_ev[L.count], 0);
         case L_SMALL:
-            return launch_front_small(N.P, N.d_small + L.off, L.count, L.maxm, d_Ax, N.stream);
+            return launch_front_small(N.R[L.vr].P, N.d_small + L.off, L.count, L.maxm, d_Ax, N.stream);
         case L_ASM:
-            return launch_assemble_large(N.P, N.d_asm + L.off, L.count, d_Ax, N.stream, L.big != 0);
+            return launch_assemble_large(N.R[L.vr].P, N.d_asm + L.off, L.count, d_Ax, N.stream, L.big != 0);
         case L_POTRF:
-            return launch_potrf_diag(N.P, N.d_potrf + L.off, L.count, N.stream);
+            return launch_potrf_diag(N.R[L.vr].P, N.d_potrf + L.off, L.count, N.stream);
         case L_TRSM:
-            return launch_trsm_panel(N.P, N.d_trsm + L.off, L.count, N.stream, L.big != 0);
+            return launch_trsm_panel(N.R[L.vr].P, N.d_trsm + L.off, L.count, N.stream, L.big != 0);
         case L_PANEL:
         case L_CB:
             return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st);
@@ -683,7 +816,7 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
 }
 
 static int64_t enqueue_all(Numeric& N, const double* d_Ax, int prof) {
-    HIP_TRY(hipMemsetAsync(N.P.info, 0x7f, sizeof(int32_t), N.stream));
+    HIP_TRY(hipMemsetAsync(N.d_info, 0x7f, sizeof(int32_t), N.stream));
     for (size_t i = 0; i < N.sched.size(); ++i) {
         const Launch& L = N.sched[i];
         const bool timed = prof == 1 && L.kind < L_RECORD;
@@ -695,6 +828,9 @@ static int64_t enqueue_all(Numeric& N, const double* d_Ax, int prof) {
         if (stamped) HIP_TRY(launch_stamp(N.d_stamps + 2 * N.stamp_of[i] + 1, st));
         if (timed) HIP_TRY(hipEventRecord(N.ev[2 * i + 1], st));
     }
+    // the status word to pinned host memory on the main stream, which every other
+    // stream has joined by now: the status read needs one stream sync, no extra copy
+    HIP_TRY(hipMemcpyAsync(N.h_info, N.d_info, sizeof(int32_t), hipMemcpyDeviceToHost, N.stream));
     return SC_OK;
 }
 
@@ -761,6 +897,7 @@ int64_t numeric_factor(Numeric& N, const double* d_Ax, bool sync) {
         TRY(enqueue_all(N, d_Ax, N.profile));
     }
     N.factored = true;
+    N.factor_gen++;
     if (sync) return numeric_status(N);
     return SC_OK;
 }
@@ -769,11 +906,13 @@ int64_t numeric_status(Numeric& N) {
     if (!N.factored) return SC_ERR_STATE;
     if (N.status_valid) return N.status;
     HIP_TRY(hipSetDevice(N.device));
+    // every stream's work is joined into the main stream before the status copy
     HIP_TRY(hipStreamSynchronize(N.stream));
-    HIP_TRY(hipStreamSynchronize(N.stream2));
-    if (N.stream3) HIP_TRY(hipStreamSynchronize(N.stream3));
-    int32_t info = 0;
-    HIP_TRY(hipMemcpy(&info, N.P.info, sizeof(info), hipMemcpyDeviceToHost));
+    int32_t info = *N.h_info;
+    if (!N.owner.empty() && !N.emulated && !N.dry_comm) {  // one rank per process: the global minimum
+        const int64_t rc = dist_min_info(N, info);
+        if (rc != SC_OK) return rc;
+    }
     if (info == 0x7f7f7f7f || info <= 0)
         N.status = 0;
     else
@@ -887,50 +1026,79 @@ int64_t numeric_syrk_stats(Numeric& N, int wmin, double* flops, double* ms, int6
     return SC_OK;
 }
 
+int64_t numeric_gather(Numeric& N) {
+    if (!N.factored) return SC_ERR_STATE;
+    const int64_t st = numeric_status(N);
+    if (st < 0) return st;
+    if (N.owner.empty() || N.emulated) return SC_OK;  // the arenas are the gathered layout
+    if (N.gather_gen == N.factor_gen) return SC_OK;
+    const int64_t rc = dist_gather_panels(N);
+    if (rc != SC_OK) return rc;
+    N.gather_gen = N.factor_gen;
+    return SC_OK;
+}
+
 int64_t numeric_export(Numeric& N, int64_t* Lp, int32_t* Li, double* Lx) {
     if (!N.factored) return SC_ERR_STATE;
-    int64_t st = numeric_status(N);
+    const int64_t st = numeric_status(N);
     if (st < 0) return st;
     const Symbolic& S = *N.S;
     std::vector<double> host;
     if (Lx) {
-        host.resize((size_t)std::max<int64_t>(S.panel_off[S.ns], 1));
-        HIP_TRY(hipMemcpy(host.data(), N.P.panel_pool, (size_t)S.panel_off[S.ns] * sizeof(double),
-                          hipMemcpyDeviceToHost));
+        TRY(numeric_gather(N));
+        const int64_t tot = N.rank_base.back();
+        host.resize((size_t)std::max<int64_t>(tot, 1));
+        HIP_TRY(hipMemcpy(host.data(), N.gpanel, (size_t)tot * sizeof(double), hipMemcpyDeviceToHost));
     }
-    export_L(S, Lx ? host.data() : nullptr, Lp, Li, Lx);
+    export_L(S, Lx ? host.data() : nullptr, N.gpo.data(), Lp, Li, Lx);
     return st;
 }
 
 int64_t numeric_export_cols(Numeric& N, int64_t j0, int64_t j1, int64_t* cp, int32_t* ri, double* rx) {
     if (!N.factored) return SC_ERR_STATE;
-    if (!N.owner.empty() && N.virt_ranks <= 1) {
-        N.err = "export_cols needs the whole factor on one device";
-        return SC_ERR_NOTIMPL;
-    }
     const int64_t st = numeric_status(N);
     if (st < 0) return st;
     const Symbolic& S = *N.S;
     if (j0 < 0 || j1 < j0 || j1 > S.n || !cp) return SC_ERR_ARG;
     HIP_TRY(hipSetDevice(N.device));
-    std::vector<double> buf;  // panel of the last supernode touched
-    int32_t cached = -1;
+    if (rx) TRY(numeric_gather(N));
+    // per supernode touched, only the columns [lo, hi] the request needs, each copied
+    // once (a column of supernode s holds rows [off, m) of its front: the copy starts
+    // at the diagonal of column lo)
+    std::vector<int64_t> lo, hi;
+    std::vector<int32_t> touched;
+    if (rx) {
+        lo.assign((size_t)S.ns, INT64_MAX);
+        hi.assign((size_t)S.ns, -1);
+        for (int64_t j = j0; j < j1; ++j) {
+            const int32_t c = S.ipost[j], s = S.sn_of[c];
+            const int64_t off = c - S.sn_start[s];
+            if (hi[s] < 0) touched.push_back(s);
+            lo[s] = std::min(lo[s], off);
+            hi[s] = std::max(hi[s], off);
+        }
+    }
+    std::vector<int64_t> base((size_t)(rx ? S.ns : 0), -1);
+    std::vector<double> buf;
+    for (int32_t s : touched) {
+        const int64_t m = S.sn_m[s];
+        const int64_t first = lo[s] * m + lo[s], last = hi[s] * m + m;  // [first, last) in the panel
+        base[s] = (int64_t)buf.size() - first;
+        const size_t at = buf.size();
+        buf.resize(at + (size_t)(last - first));
+        HIP_TRY(hipMemcpy(buf.data() + at, N.gpanel + N.gpo[s] + first, (size_t)(last - first) * sizeof(double),
+                          hipMemcpyDeviceToHost));
+    }
     int64_t tot = 0;
     cp[0] = 0;
     for (int64_t j = j0; j < j1; ++j) {
         const int32_t c = S.ipost[j], s = S.sn_of[c];
         const int64_t m = S.sn_m[s], off = c - S.sn_start[s];
         if (ri) {
-            if (rx && s != cached) {
-                buf.resize((size_t)(m * S.w(s)));
-                HIP_TRY(hipMemcpy(buf.data(), N.P.panel_pool + S.panel_off[s], buf.size() * sizeof(double),
-                                  hipMemcpyDeviceToHost));
-                cached = s;
-            }
             const int32_t* rows = S.rows.data() + S.rows_ptr[s];
             for (int64_t t = off; t < m; ++t) {
                 ri[tot + t - off] = S.post[rows[t]];
-                if (rx) rx[tot + t - off] = buf[(size_t)(off * m + t)];
+                if (rx) rx[tot + t - off] = buf[(size_t)(base[s] + off * m + t)];
             }
         }
         tot += m - off;
@@ -991,12 +1159,12 @@ static int64_t solve_build(Numeric& N) {
     if ((rc = dalloc(N, (size_t)std::max<int64_t>(S.n, 1) * 3 * sizeof(double), p))) return rc;
     N.d_sbuf = (double*)p;
     N.SP.y = N.d_sbuf + 2 * S.n;  // forward result of the fused steps
-    N.SP.sn_start = N.P.sn_start;
-    N.SP.sn_m = N.P.sn_m;
-    N.SP.panel_off = N.P.panel_off;
+    N.SP.sn_start = N.R[0].P.sn_start;
+    N.SP.sn_m = N.R[0].P.sn_m;
+    N.SP.panel_off = N.d_gpo;
     N.SP.rows_ptr = d_rows_ptr;
     N.SP.rows = d_rows;
-    N.SP.panel_pool = N.P.panel_pool;
+    N.SP.panel_pool = N.gpanel;
     N.SP.c = N.d_sbuf + S.n;  // internal-order work vector
     N.solve_ready = true;
     return SC_OK;
@@ -1004,13 +1172,17 @@ static int64_t solve_build(Numeric& N) {
 
 int64_t numeric_solve_device(Numeric& N, const double* d_b, double* d_x) {
     if (!N.factored) return SC_ERR_STATE;
-    if (!N.owner.empty() && N.virt_ranks <= 1) {
-        N.err = "solve needs the whole factor on one device (multi-rank handles hold only their part)";
-        return SC_ERR_NOTIMPL;
-    }
     const int64_t st = numeric_status(N);
     if (st != SC_OK) return st;
     HIP_TRY(hipSetDevice(N.device));
+    TRY(numeric_gather(N));  // multi-rank: every rank solves with the whole factor
+    if (N.solve_ready && N.SP.panel_pool != N.gpanel) {
+        N.SP.panel_pool = N.gpanel;  // gathered buffer allocated after the plan was built
+        if (N.solve_gexec) (void)hipGraphExecDestroy(N.solve_gexec);
+        if (N.solve_graph) (void)hipGraphDestroy(N.solve_graph);
+        N.solve_gexec = nullptr;
+        N.solve_graph = nullptr;
+    }
     if (!N.solve_ready) TRY(solve_build(N));
     const int64_t n = N.S->n;
     if (n == 0) return SC_OK;
@@ -1081,6 +1253,7 @@ void numeric_free(Numeric* Np) {
     for (auto e : N.sync_ev)
         if (e) (void)hipEventDestroy(e);
     for (void* p : N.allocs) (void)hipFree(p);
+    if (N.h_info) (void)hipHostFree(N.h_info);
     if (N.d_Ax_owned) (void)hipFree(N.d_Ax_owned);
     if (N.stream) (void)hipStreamDestroy(N.stream);
     if (N.stream2) (void)hipStreamDestroy(N.stream2);

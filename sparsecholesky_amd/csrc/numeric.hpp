@@ -1,4 +1,4 @@
-// Device numeric factorization driver: pools, level schedule, launches, export.
+// Device numeric factorization driver: memory plan, level schedule, launches, export.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -18,7 +18,7 @@ enum LaunchKind : int32_t {
     L_TRSM = 3,
     L_PANEL = 4,
     L_CB = 5,
-    L_COMM = 6,    // CB send/recv group after a level (multi-GPU)
+    L_COMM = 6,    // one comm step of the hosted ranks (pack, transfer group, unpack)
     L_RECORD = 7,  // record sync event `count` on stream `strm`
     L_WAIT = 8,    // stream `strm` waits for sync event `count`
     L_KINDS = 9
@@ -26,7 +26,7 @@ enum LaunchKind : int32_t {
 
 // ---------------- multi-GPU plan (dist.cpp) ----------------
 // Comm steps, in one global order every rank follows (each rank posts exactly its
-// part of every step it takes part in, as one RCCL group, on its comm stream):
+// part of every step it takes part in, as one transfer group, on its comm stream):
 //   STEP_INIT(s)    split front s: the owner sends the assembled CB column blocks to
 //                   the ranks that compute them
 //   STEP_SLAB(s,k)  split front s: the owner sends rows [w, m) of panel slab k (final)
@@ -39,16 +39,26 @@ enum StepKind : int32_t { STEP_INIT = 0, STEP_SLAB = 1, STEP_DELIVER = 2 };
 struct DistStep {
     int32_t kind, level, s, k;
 };
-// One 2D block transfer: rows x cols doubles at pool + off, leading dimension ld,
-// moved packed (rows-contiguous) through a staging slot.
+
+// Device memory regions of a rank (memplan.cpp).  Messages and tasks name a region
+// by kind, supernode and LOGICAL coordinates; every rank maps them to its own
+// physical layout, so sender and receiver may store a block differently.
+//   R_PANEL  the L panel of s: m x w, row = front row (owner only; permanent)
+//   R_CB     the contribution block of s: mb x mb, row/col = front row - w.  Held as a
+//            full square (ld = mb) or, on a rank computing only some of a split
+//            front's column blocks, as compact blocks (ld = rows of the block)
+//   R_LAND   a split front's L21 (rows [w, m) of its panel) on a CB rank: mb x w
+enum RegionKind : int32_t { R_PANEL = 0, R_CB = 1, R_LAND = 2 };
+
+// One 2D block transfer: rows x cols doubles from (skind, s, srow, scol) on src to
+// (dkind, s, drow, dcol) on dst, moved packed (column-contiguous) through staging.
 struct DistMsg {
     int32_t step;
     int32_t src, dst;
-    int32_t pool;  // 0 = panel pool, 1 = CB pool
-    int64_t off;
-    int64_t ld;
+    int32_t skind, dkind;
+    int32_t s;
+    int32_t srow, scol, drow, dcol;
     int32_t rows, cols;
-    int32_t s;     // supernode the block belongs to
 };
 struct DistPlan {
     int nranks = 1;
@@ -68,16 +78,52 @@ struct DistPlan {
     std::vector<double> work;      // estimated flops per rank
 };
 int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D);
+
+// Memory of one rank (a process hosts one rank, or every rank when emulated).
+//   panel arena  the L panels of the supernodes this rank owns, back to back
+//   work arena   transient regions (contribution blocks, landing slabs), each live
+//                over a closed interval of assembly-tree levels; offsets from an
+//                interval plan (memplan.cpp), so a region is reused once dead
+struct RankMem {
+    int32_t rank = 0;
+    std::vector<int64_t> panel_off;  // per supernode: doubles into the panel arena, -1 = not here
+    std::vector<int64_t> cb_off;     // per supernode: full-square CB in the work arena, -1
+    std::vector<int64_t> land_off;   // per supernode: R_LAND slab (ld = mb) in the work arena, -1
+    std::vector<std::vector<int64_t>> blk_off;  // per split front, per column block: compact block, -1
+    int64_t panel_total = 0;     // doubles (incl. the PNB tail the TRSM reads past)
+    int64_t work_total = 0;      // doubles: high-water mark of the interval plan
+    int64_t work_live_max = 0;   // doubles: max over levels of the live region sizes (lower bound)
+    DevPlan P {};                // pools + device copies of panel_off / cb_off
+};
+// Plan rank `rank`'s regions (D == nullptr: single device, every front here);
+// `placed` (optional) receives every work-arena region with its lifetime.
+struct PlacedRegion {
+    int64_t off, size;
+    int32_t t0, t1;
+};
+int64_t plan_rank_memory(const Symbolic& S, const DistPlan* D, int rank, RankMem& R,
+                         std::vector<PlacedRegion>* placed = nullptr);
+int64_t plan_check(const Symbolic& S, int nranks);
+// Physical location of logical element (row, col) of region (kind, s) on R: arena
+// (0 panel, 1 work), offset in doubles and leading dimension.  false: not on R.
+bool region_addr(const Symbolic& S, const DistPlan* D, const RankMem& R, int kind, int s, int row, int col,
+                 int& arena, int64_t& off, int64_t& ld);
+// Region lifetimes of the plan, in assembly-tree levels (exposed for tests):
+// fills the peak and the lower bound of the work arena of every rank.
+int64_t plan_memory_stats(const Symbolic& S, int nranks, int64_t* panel_doubles, int64_t* work_doubles,
+                          int64_t* work_lower_bound);
+
 // transport argument of numeric_create_dist selecting the dry mode
 #define DIST_DRY ((int32_t(*)(void*, int32_t, int32_t, void*, int64_t))1)
 
-// One point-to-point block transfer of this rank (device addresses resolved).
+// One transfer of a comm step, device addresses resolved.
+enum MsgOp : int32_t { MSG_SEND = 0, MSG_RECV = 1, MSG_COPY = 2 };
 struct Msg {
-    double* buf;      // staging slot (packed rows x cols)
+    double* buf;      // staging slot (packed rows x cols), or the region itself when contiguous
+    double* src_buf;  // MSG_COPY (both ends hosted, device-copy transport): the sender's slot
     int64_t count;    // doubles
-    int32_t peer;
-    int32_t is_send;
-    int32_t child;    // supernode whose data moves
+    int32_t peer;     // communicator rank of the other end
+    int32_t op;       // MsgOp
 };
 
 struct Launch {
@@ -90,7 +136,8 @@ struct Launch {
     int32_t maxm;     // small-front LDS edge
     int32_t big;      // CB launch covering fronts with w >= 256
     int32_t bt;       // SYRK tile edge (64 or 128)
-    int32_t strm;     // 0 = main stream, 1 = lookahead stream
+    int32_t strm;     // 0 = main stream, 1 = lookahead stream, 2 = comm stream
+    int32_t vr;       // hosted rank whose DevPlan the kernel uses
     double flops;     // algorithmic SYRK flops (CB launches: mb*(mb+1)*w)
     // L_COMM: copy tiles [poff, poff + pcount) pack the sends, [uoff, uoff + ucount)
     // unpack the receives (Numeric::d_ctiles)
@@ -104,11 +151,13 @@ struct Numeric {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;  // trailing panel updates overlapped with the next slab
-    hipStream_t stream3 = nullptr;  // multi-GPU: comm stream (pack, RCCL group, unpack), strm == 2
+    hipStream_t stream3 = nullptr;  // multi-rank: comm stream (pack, transfer group, unpack), strm == 2
     std::vector<hipEvent_t> sync_ev;
     int32_t n_sync_events = 0;
-    DevPlan P {};
+    std::vector<RankMem> R;          // hosted ranks
+    std::vector<int64_t> rank_base;  // gathered panel layout: first double of each rank's arena
     std::vector<void*> allocs;
+    int64_t dev_bytes = 0;           // device memory held (pools, plan, staging)
     std::vector<Launch> sched;
     int32_t* d_small = nullptr;
     int2* d_asm = nullptr;
@@ -116,9 +165,12 @@ struct Numeric {
     int4* d_trsm = nullptr;
     GemmTask* d_gemm = nullptr;
     int2* d_tiles = nullptr;
+    int32_t* d_info = nullptr;       // shared by the hosted ranks' DevPlans
+    int32_t* h_info = nullptr;       // pinned host copy, written at the end of each factorization
     double* d_Ax_owned = nullptr;
     const double* last_Ax = nullptr;
     bool factored = false;
+    int64_t factor_gen = 0;          // factorizations enqueued
     int64_t status = 0;
     bool status_valid = false;
 
@@ -136,23 +188,31 @@ struct Numeric {
     const double* graph_Ax = nullptr;
     int graph_profiled = 0;
 
-    // multi-GPU: owner rank per supernode (empty = single GPU).  virt_ranks > 1
-    // runs the partitioned schedule of all ranks in this one process (shared
-    // pools, no transfers) to validate the partition on one device.
-    int rank = 0, nranks = 1, virt_ranks = 0;
-    std::vector<int32_t> owner;
+    // multi-rank: this process hosts R (one rank of nranks, or all of them when
+    // emulated on one device with private per-rank memory)
+    int rank = 0, nranks = 1;
+    bool emulated = false;
+    int emul_rccl = 0;  // emulated: 1 = hosted-to-hosted transfers as RCCL self send/recv
+    std::vector<int32_t> owner;  // empty = single device
     DistPlan D;
     std::vector<Msg> msgs;
     Copy2D* d_copy = nullptr;     // pack / unpack descriptors
     int2* d_ctiles = nullptr;     // (descriptor, first column) per copy workgroup
-    double* staging = nullptr;    // one packed slot per message of this rank
+    double* staging = nullptr;    // packed slots of the hosted ranks' messages
     void* comm = nullptr;  // ncclComm_t
     // host-staged transport (tests: several processes on one GPU, no RCCL):
     // op 0 post send, 1 post recv, 2 complete everything posted
     int32_t (*xport)(void* ctx, int32_t op, int32_t peer, void* buf, int64_t bytes) = nullptr;
     void* xport_ctx = nullptr;
     bool dry_comm = false;  // comm steps pack / unpack but move nothing (one-rank timing projection)
-    double comm_ms = 0.0;
+
+    // gathered factor (every supernode's panel in the rank_base layout): the panel
+    // arena itself for single-device and emulated handles, else gathered on demand
+    double* gpanel = nullptr;
+    bool gpanel_owned = false;
+    int64_t gather_gen = -1;         // factor_gen the gathered copy belongs to
+    std::vector<int64_t> gpo;        // per supernode: offset in gpanel
+    int64_t* d_gpo = nullptr;
 
     // triangular solves (built at the first solve)
     struct SolveStep {
@@ -175,12 +235,15 @@ struct Numeric {
     std::string err;
 };
 
-// Builds pools + schedule; owner/rank restrict the schedule to one rank's fronts.
+// Builds the memory plan, pools and schedule of the hosted ranks.
 int64_t numeric_init(Numeric& N, const Symbolic& S, int device);
 
 int64_t numeric_create(const Symbolic& S, int device, Numeric*& out, std::string& err);
 int64_t numeric_factor(Numeric& N, const double* d_Ax, bool sync);
 int64_t numeric_status(Numeric& N);
+// Makes gpanel / gpo hold the whole factor of the last factorization (multi-rank
+// handles: a collective exchange of every rank's panel arena; all ranks call it).
+int64_t numeric_gather(Numeric& N);
 int64_t numeric_export(Numeric& N, int64_t* Lp, int32_t* Li, double* Lx);
 // Natural columns [j0, j1) in front-row form (count only when ri == NULL): column j
 // holds the rows of its supernode's front from its own position down (natural
@@ -193,7 +256,8 @@ int64_t numeric_launch_trace(Numeric& N, int32_t* kind, int32_t* level, int32_t*
 int64_t numeric_syrk_stats(Numeric& N, int wmin, double* flops, double* ms, int64_t* launches);
 void numeric_free(Numeric* N);
 // x = A^{-1} b with the factor: device vectors of length n (may alias), on the
-// library stream, synchronous.  Single-device factors only.
+// library stream, synchronous.  Multi-rank handles gather the factor first
+// (collective) and every rank solves with the whole factor.
 int64_t numeric_solve_device(Numeric& N, const double* d_b, double* d_x);
 int64_t numeric_solve_host(Numeric& N, const double* b, double* x);
 int64_t debug_syrk(double* dC, int ldc, const double* dA, int lda, int M, int N, int K);

@@ -477,7 +477,7 @@ void pattern_L(const Symbolic& S, i64* Lp, i32* Li) {
     }
 }
 
-void export_L(const Symbolic& S, const double* panels, i64* Lp, i32* Li, double* Lx) {
+void export_L(const Symbolic& S, const double* panels, const i64* poff, i64* Lp, i32* Li, double* Lx) {
     const i64 n = S.n;
     std::vector<i64> Lp_loc;
     std::vector<i32> Li_loc;
@@ -497,7 +497,7 @@ void export_L(const Symbolic& S, const double* panels, i64* Lp, i32* Li, double*
         const i64 m = S.sn_m[s];
         const i32* rows = S.rows.data() + S.rows_ptr[s];
         for (i64 t = 0; t < m; ++t) pos[rows[t]] = (i32)t;
-        const double* P = panels + S.panel_off[s];
+        const double* P = panels + poff[s];
         for (i32 c = c0; c < c1; ++c) {
             const i32 j = S.post[c];
             const double* col = P + (i64)(c - c0) * m;

@@ -106,7 +106,8 @@ void permute_upper(i64 n, const i64* Ap, const i32* Ai, const i32* perm, std::ve
 // Reference-layout pattern of L (schol().p()/i()), natural numbering.
 void pattern_L(const Symbolic& S, i64* Lp, i32* Li);
 
-// Export: supernodal panels (host copy of the panel pool) -> reference CSC.
-void export_L(const Symbolic& S, const double* panels, i64* Lp, i32* Li, double* Lx);
+// Export: supernodal panels (host copy of the gathered panels; supernode s at
+// panels + poff[s], m x w, ld = m) -> reference CSC.
+void export_L(const Symbolic& S, const double* panels, const i64* poff, i64* Lp, i32* Li, double* Lx);
 
 }  // namespace sc

@@ -36,27 +36,33 @@ def _rank_main(rank, world, port, k, opts, out):
         sts = []
         for _ in range(2):  # refactor: the comm stream is joined at the end of each run
             sts.append(num.factor(A.x))
+        # the drop-in boundary on a multi-rank handle: sc_export_L is collective and
+        # every rank gets the whole L (chol.hpp:858-862), then a collective solve
         st, L = num.export()
-        own, _ = symb.owner_map(world)
-        sn = symb.supernodes()
-        _, post = symb.etree()
-        cols = [post[sn["start"][s]:sn["start"][s + 1]] for s in range(len(own)) if own[s] == rank]
-        cols = np.concatenate(cols) if cols else np.zeros(0, dtype=np.int32)
+        b = np.random.default_rng(11).standard_normal(A.size())
+        x = num.solve(b)
+        mem = num.memory()
         parts = [None] * world
-        dist.all_gather_object(parts, (cols, [L.x[L.p[j]:L.p[j + 1]] for j in cols], sts, tr.error))
+        dist.all_gather_object(parts, (L.x, x, sts, st, tr.error, mem))
         if rank == 0:
-            Lx = np.full(L.x.shape, np.nan)
-            for c, xs, _, _ in parts:
-                for j, x in zip(c, xs):
-                    Lx[L.p[j]:L.p[j + 1]] = x
             sto, Lp, Li, Lxo = oracle.chol(A)
             ok_pat = np.array_equal(L.p, Lp) and np.array_equal(L.i, Li)
-            covered = not np.isnan(Lx).any()
-            err = float(np.linalg.norm(Lx - Lxo) / np.linalg.norm(Lxo)) if covered else float("inf")
-            out["res"] = (ok_pat, covered, err, [p[2] for p in parts], [p[3] for p in parts])
+            same = all(np.array_equal(p[0], parts[0][0]) and np.array_equal(p[1], parts[0][1]) for p in parts)
+            err = float(np.linalg.norm(L.x - Lxo) / np.linalg.norm(Lxo))
+            U = _sym_full(A)
+            be = float(np.abs(U @ x - b).max() / (np.abs(U).sum(axis=1).max() * np.abs(x).max() + np.abs(b).max()))
+            out["res"] = (ok_pat, same, err, be, [p[2] for p in parts], [p[3] for p in parts],
+                          [p[4] for p in parts], [p[5] for p in parts])
         dist.barrier()
     finally:
         dist.destroy_process_group()
+
+
+def _sym_full(A):
+    import scipy.sparse as sp
+
+    U = sp.triu(sp.csc_matrix((A.x, A.i, A.p), shape=(A.size(), A.size())))
+    return (U + sp.triu(U, 1).T).tocsr()
 
 
 @pytest.mark.parametrize("world,k,opts", [
@@ -74,8 +80,12 @@ def test_multiprocess_host_transport(gpu, world, k, opts):
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_rank_main, args=(world, port, k, opts, out), nprocs=world, join=True)
-    ok_pat, covered, err, sts, errs = out["res"]
+    ok_pat, same, err, be, sts, exp_st, errs, mems = out["res"]
     assert all(e is None for e in errs), errs
     assert all(s == [0, 0] for s in sts), sts
-    assert ok_pat and covered
+    assert all(s == 0 for s in exp_st), exp_st
+    assert ok_pat and same
     assert err < TOL, err
+    assert be < 1e-14, be
+    # each rank holds its own panels and work arena, not the whole factor's pools
+    assert all(m["panel"] < mems[0]["total"] for m in mems)

@@ -337,8 +337,9 @@ def test_device_resident_factor(gpu):
 
 @pytest.mark.parametrize("nranks", [2, 3, 8])
 def test_partitioned_schedule_bitwise_equal(gpu, nranks):
-    # the multi-GPU partition with every front on one rank (dist_split=0), emulated in
-    # one process, must reproduce the single-GPU factor bitwise
+    # the multi-GPU partition with every front on one rank (dist_split=0), every rank
+    # emulated in one process with its own memory and every contribution block moved
+    # by the message plan, must reproduce the single-GPU factor bitwise
     A = sc.laplacian3d(20)
     s = sc.Symbolic(A, dist_split=0)
     ref = sc.Numeric(s)
@@ -352,20 +353,42 @@ def test_partitioned_schedule_bitwise_equal(gpu, nranks):
     assert rel_fro(L1.x, Lx) < TOL
 
 
-@pytest.mark.parametrize("nranks", [2, 3, 4, 8])
-def test_partitioned_split_fronts_emulated(gpu, nranks):
+@pytest.mark.parametrize("nranks,rccl", [(2, False), (3, False), (4, False), (8, False),
+                                         (2, True), (4, True), (8, True)])
+def test_partitioned_split_fronts_emulated(gpu, nranks, rccl):
     # split top fronts (panel on the owner, CB column blocks updated per slab by the
-    # other ranks of the group), emulated in one process: the same factor to 1e-12
+    # other ranks of the group): every rank in one process with private memory, the
+    # messages moved as device copies or (rccl=True) as ncclSend/ncclRecv to self in
+    # one group per comm step on a 1-rank RCCL communicator (dist.cpp transfer_group).
+    # A missing or misplaced message leaves a rank with stale data: parity catches it.
     A = sc.laplacian3d(20)
     s = sc.Symbolic(A, panel_nb_outer=128, dist_cbb=64, small_front_max=32)
     info = s.dist_plan_info(nranks)
     assert nranks == 2 or (info["split_cb_ranks"] > 0).any()
-    v = sc.Numeric(s, nranks=nranks, virtual=True)
-    assert v.factor(A.x) == 0
+    v = sc.Numeric(s, nranks=nranks, virtual=True, rccl_self=rccl)
+    for _ in range(2):  # refactor through the same handle: arenas reused
+        assert v.factor(A.x) == 0
     _, L1 = v.export()
     st, Lp, Li, Lx = oracle.chol(A)
     assert np.array_equal(L1.p, Lp) and np.array_equal(L1.i, Li)
     assert rel_fro(L1.x, Lx) < TOL
+    b = np.random.default_rng(5).standard_normal(A.size())
+    x = v.solve(b)
+    assert _backward_error(A, x, b) < 1e-14
+
+
+def test_memory_matches_plan(gpu):
+    A = sc.laplacian3d(24)
+    s = sc.Symbolic(A)
+    num = sc.Numeric(s)
+    mem = num.memory()
+    mp = s.memory_plan(1)
+    assert mem["panel"] == int(mp["panel"][0]) and mem["work"] == int(mp["work"][0])
+    assert mem["total"] >= mem["panel"] + mem["work"]
+    assert num.factor(A.x) == 0
+    _, L = num.export()
+    st, Lp, Li, Lx = oracle.chol(A)
+    assert rel_fro(L.x, Lx) < TOL
 
 
 def random_spd(n, density, seed, dup=False, lower_noise=False):

@@ -1,0 +1,50 @@
+"""Device memory plan (sparsecholesky_amd/csrc/memplan.cpp), checked on the host.
+
+The reference keeps one transient UpdateBlock per supernode (include/chol.hpp:1161-1169,
+1315-1316).  Here each contribution block lives over a closed interval of assembly-tree
+levels and the regions are placed in one work arena by a sweep; these tests check that
+the plan is sound (no two live regions overlap) and that it stays within the budgets
+of the 128^3 workload: <= 60 GB on one GPU, and per rank at 8 ranks at most a third of
+the single-GPU plan.
+"""
+import numpy as np
+import pytest
+
+import sparsecholesky_amd as sc
+
+
+@pytest.mark.parametrize("k,opts", [(12, {}), (16, {}), (20, dict(panel_nb_outer=128, dist_cbb=64, small_front_max=32)),
+                                    (24, dict(dist_cbb=128))])
+def test_plan_sound_every_rank(k, opts):
+    s = sc.Symbolic(sc.laplacian3d(k), **opts)
+    for nranks in (1, 2, 3, 4, 8):
+        assert sc.lib().sc_memory_plan_check(s.h, nranks) == 0, nranks
+
+
+@pytest.mark.parametrize("name", ["bcsstk01", "1138_bus"])
+def test_plan_sound_reference_matrices(mtx, name):
+    s = sc.Symbolic(mtx(name))
+    for nranks in (1, 2, 4):
+        assert sc.lib().sc_memory_plan_check(s.h, nranks) == 0
+
+
+def test_plan_near_lower_bound_and_below_static_pools():
+    s = sc.Symbolic(sc.laplacian3d(48))
+    st = s.stats()
+    mp = s.memory_plan(1)
+    work, lb = int(mp["work"][0]), int(mp["work_lower_bound"][0])
+    assert lb <= work <= 1.3 * lb
+    # the round-1 static pools held every contribution block at once
+    assert work < 0.5 * st["cb_entries"] * 8
+    assert int(mp["panel"][0]) >= st["panel_entries"] * 8
+
+
+def test_plan_lap128_budgets():
+    s = sc.Symbolic(sc.laplacian3d(128))
+    one = s.memory_plan(1)
+    single = int(one["panel"][0] + one["work"][0])
+    assert single <= 60e9, single / 1e9
+    eight = s.memory_plan(8)
+    per_rank = eight["panel"] + eight["work"]
+    assert per_rank.max() <= single / 3, (per_rank / 1e9).round(1)
+    assert sc.lib().sc_memory_plan_check(s.h, 8) == 0
