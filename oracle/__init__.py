@@ -44,6 +44,8 @@ def lib():
         L.oracle_chol.argtypes = [I64, P, P, P, P, P, P, P, C.c_int]
         L.oracle_chol.restype = I64
         L.oracle_schol.argtypes = [I64, P, P, P, P, P]
+        L.oracle_time_chol.argtypes = [I64, P, P, P, C.c_int, C.c_int, C.POINTER(C.c_double)]
+        L.oracle_time_chol.restype = I64
         _lib = L
     return _lib
 
@@ -133,6 +135,16 @@ def chol(A, faithful_workspace=False):
     st = lib().oracle_chol(n, _p(Ap), _p(Ai), _p(Ax), _p(sy["parent"]), _p(Lp), _p(Li), _p(Lx),
                            1 if faithful_workspace else 0)
     return int(st), Lp, Li[:nz], Lx[:nz]
+
+
+def time_chol(A, reps=5, faithful_workspace=True):
+    """Best-of-`reps` seconds of the whole reference chol() call (symbolic + numeric),
+    timed in C.  Returns (status, seconds)."""
+    Ap, Ai, Ax = _csc(A)
+    n = len(Ap) - 1
+    best = C.c_double()
+    st = lib().oracle_time_chol(n, _p(Ap), _p(Ai), _p(Ax), reps, 1 if faithful_workspace else 0, C.byref(best))
+    return int(st), best.value
 
 
 def schol(A):

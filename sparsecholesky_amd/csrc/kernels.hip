@@ -24,83 +24,6 @@ __device__ __forceinline__ void report_fail(int32_t* info, int32_t col_internal)
 }
 
 // ---------------------------------------------------------------------------
-// Small fronts: whole front in LDS, one 256-thread workgroup per front.
-// Assemble A columns + children CBs (extend-add, children in a fixed order:
-// deterministic, no atomics), right-looking partial Cholesky of the w pivots
-// (the CB is updated in place = the SYRK), write L panel and CB.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void small_front(const DevPlan& P, const int s, const double* __restrict__ Ax,
-                                            double* F, double& s_piv) {
-    const int tid = threadIdx.x;
-    const int c0 = P.sn_start[s];
-    const int w = P.sn_start[s + 1] - c0;
-    const int m = P.sn_m[s];
-    const int mb = m - w;
-    const int mm = m * m;
-
-    for (int idx = tid; idx < mm; idx += 256) F[idx] = 0.0;
-    __syncthreads();
-    // A entries of the pivot columns
-    for (int lc = 0; lc < w; ++lc) {
-        const int64_t a0 = P.a_ptr[c0 + lc], a1 = P.a_ptr[c0 + lc + 1];
-        for (int64_t q = a0 + tid; q < a1; q += 256) F[lc * m + P.a_pos[q]] = Ax[P.a_src[q]];
-    }
-    __syncthreads();
-    // extend-add of the children's contribution blocks
-    for (int ci = P.child_ptr[s]; ci < P.child_ptr[s + 1]; ++ci) {
-        const int c = P.child_list[ci];
-        const int mbc = P.sn_m[c] - (P.sn_start[c + 1] - P.sn_start[c]);
-        const int32_t* rel = P.relind + P.rel_ptr[c];
-        const double* cb = P.cb_pool + P.cb_off[c];
-        const int tot = mbc * mbc;
-        for (int idx = tid; idx < tot; idx += 256) {
-            const int ic = idx % mbc, jc = idx / mbc;
-            if (ic >= jc) F[rel[jc] * m + rel[ic]] += cb[idx];
-        }
-        __syncthreads();
-    }
-    // right-looking partial factorization
-    const int G = (m <= 256) ? (256 / m) : 1;  // column groups
-    const int i = tid % m;
-    const int g = tid / m;
-    for (int k = 0; k < w; ++k) {
-        if (tid == 0) {
-            double d = F[k * m + k];
-            if (!(d > 0.0)) report_fail(P.info, c0 + k);
-            s_piv = sqrt(d);
-            F[k * m + k] = s_piv;
-        }
-        __syncthreads();
-        const double dk = s_piv;
-        for (int r = k + 1 + tid; r < m; r += 256) F[k * m + r] = F[k * m + r] / dk;
-        __syncthreads();
-        if (g < G && i > k) {
-            const double lik = F[k * m + i];
-            for (int j = k + 1 + g; j <= i; j += G) F[j * m + i] -= lik * F[k * m + j];
-        }
-        __syncthreads();
-    }
-    // write back the L panel (contiguous m*w) and the CB (lower)
-    double* panel = P.panel_pool + P.panel_off[s];
-    for (int idx = tid; idx < m * w; idx += 256) panel[idx] = F[idx];
-    if (mb > 0) {
-        double* cb = P.cb_pool + P.cb_off[s];
-        const int tot = mb * mb;
-        for (int idx = tid; idx < tot; idx += 256) {
-            const int ic = idx % mb, jc = idx / mb;
-            if (ic >= jc) cb[idx] = F[(jc + w) * m + (ic + w)];
-        }
-    }
-}
-
-__global__ __launch_bounds__(256) void front_small_kernel(DevPlan P, const int32_t* __restrict__ nodes,
-                                                           const double* __restrict__ Ax) {
-    extern __shared__ double F[];
-    __shared__ double s_piv;
-    small_front(P, nodes[blockIdx.x], Ax, F, s_piv);
-}
-
-// ---------------------------------------------------------------------------
 // Large fronts, assembly: one workgroup per (front, 64-column block).  Zeroes its
 // panel / CB columns, stores the A entries, then adds every child's CB entries
 // whose parent column falls in the block (children in fixed order: deterministic).
@@ -291,6 +214,130 @@ __device__ __forceinline__ void trsm_steps(double (&r)[PNB], const double* Lc, c
             trsm_steps<J + 1>(r, Lc, invd, nb);
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// Small fronts (m <= 128): the whole front in LDS, one 256-thread workgroup per
+// front, the lower triangle packed by columns (column j holds rows j..m-1 at
+// j m - j (j - 1) / 2): 64.5 KB at m = 128, two workgroups per CU.
+//   1. assemble: zero, A entries of the pivot columns, the children's CBs
+//      (extend-add, one wave per child column, children in a fixed order:
+//      deterministic, no atomics);
+//   2. POTRF of the w x w diagonal block by one wave in registers (w <= 64);
+//   3. TRSM: one thread per row of L21 (independent rows);
+//   4. the panel and CB = F22 - L21 L21^T (the SYRK, one wave per CB column,
+//      w-long dot products from LDS) written straight to HBM.
+// Fronts wider than 64 take a right-looking loop over the panel columns instead.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int pk_col(int m, int j) { return j * m - ((j * (j - 1)) >> 1); }
+
+__device__ __forceinline__ void small_front(const DevPlan& P, const int s, const double* __restrict__ Ax,
+                                            double* F, double* colj) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int c0 = P.sn_start[s];
+    const int w = P.sn_start[s + 1] - c0;
+    const int m = P.sn_m[s];
+    const int mb = m - w;
+    const int tot = (m * (m + 1)) >> 1;
+    for (int idx = tid; idx < tot; idx += 256) F[idx] = 0.0;
+    __syncthreads();
+    for (int lc = wid; lc < w; lc += 4) {
+        const int64_t a0 = P.a_ptr[c0 + lc], a1 = P.a_ptr[c0 + lc + 1];
+        double* Fc = F + pk_col(m, lc) - lc;
+        for (int64_t q = a0 + lane; q < a1; q += 64) Fc[P.a_pos[q]] = Ax[P.a_src[q]];
+    }
+    __syncthreads();
+    for (int ci = P.child_ptr[s]; ci < P.child_ptr[s + 1]; ++ci) {
+        const int c = P.child_list[ci];
+        const int mbc = P.sn_m[c] - (P.sn_start[c + 1] - P.sn_start[c]);
+        const int32_t* __restrict__ rel = P.relind + P.rel_ptr[c];
+        const double* __restrict__ cb = P.cb_pool + P.cb_off[c];
+        for (int jc = wid; jc < mbc; jc += 4) {
+            const int pj = rel[jc];
+            double* Fc = F + pk_col(m, pj) - pj;
+            const double* __restrict__ src = cb + (int64_t)jc * mbc;
+            for (int ic = jc + lane; ic < mbc; ic += 64) Fc[rel[ic]] += src[ic];
+        }
+        __syncthreads();
+    }
+    if (w <= PNB) {
+        if (wid == 0) {  // 2. POTRF, lane = row of the diagonal block
+            const bool live = lane < w;
+            double r[PNB];
+#pragma unroll
+            for (int c = 0; c < PNB; ++c) r[c] = (live && c <= lane && c < w) ? F[pk_col(m, c) + lane - c] : 0.0;
+            potrf_steps<0>(r, colj, lane, w, P.info, c0);
+            if (live) {
+#pragma unroll
+                for (int c = 0; c < PNB; ++c)
+                    if (c < w && c <= lane) F[pk_col(m, c) + lane - c] = r[c];
+            }
+        }
+        __syncthreads();
+        if (tid < mb) {  // 3. TRSM, thread = row w + tid: x_j = (F_ij - sum_t<j x_t L_jt) / L_jj
+            const int i = w + tid;
+            int oj = 0;  // pk_col(m, j)
+            for (int j = 0; j < w; ++j) {
+                double acc = F[oj + i - j];
+                int ot = 0;
+                for (int t = 0; t < j; ++t) {
+                    acc -= F[ot + i - t] * F[ot + j - t];
+                    ot += m - t;
+                }
+                F[oj + i - j] = acc / F[oj];
+                oj += m - j;
+            }
+        }
+    } else {
+        for (int k = 0; k < w; ++k) {  // right-looking over the panel columns
+            double* Fk = F + pk_col(m, k) - k;
+            if (tid == 0) {
+                const double d = Fk[k];
+                if (!(d > 0.0)) report_fail(P.info, c0 + k);
+                Fk[k] = sqrt(d);
+            }
+            __syncthreads();
+            const double inv = 1.0 / Fk[k];
+            for (int r = k + 1 + tid; r < m; r += 256) Fk[r] *= inv;
+            __syncthreads();
+            for (int j = k + 1 + wid; j < w; j += 4) {
+                double* Fj = F + pk_col(m, j) - j;
+                const double ljk = Fk[j];
+                for (int r = j + lane; r < m; r += 64) Fj[r] -= Fk[r] * ljk;
+            }
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+    double* panel = P.panel_pool + P.panel_off[s];
+    for (int j = wid; j < w; j += 4) {
+        const double* Fj = F + pk_col(m, j) - j;
+        for (int i = j + lane; i < m; i += 64) panel[(int64_t)j * m + i] = Fj[i];
+    }
+    if (mb > 0) {  // 4. CB(ic, jc) = F22(ic, jc) - sum_t L21(ic, t) L21(jc, t)
+        double* cb = P.cb_pool + P.cb_off[s];
+        for (int jc = wid; jc < mb; jc += 4) {
+            const int jj = w + jc;
+            for (int ic = jc + lane; ic < mb; ic += 64) {
+                const int ii = w + ic;
+                double v = F[pk_col(m, jj) + ii - jj];
+                int ot = 0;
+                for (int t = 0; t < w; ++t) {
+                    v -= F[ot + ii - t] * F[ot + jj - t];
+                    ot += m - t;
+                }
+                cb[(int64_t)jc * mb + ic] = v;
+            }
+        }
+    }
+}
+
+// maxm: LDS edge of the launch (the packed front plus the POTRF column buffer)
+__global__ __launch_bounds__(256) void front_small_kernel(DevPlan P, const int32_t* __restrict__ nodes,
+                                                           const double* __restrict__ Ax) {
+    extern __shared__ double F[];
+    __shared__ double colj[PNB];
+    small_front(P, nodes[blockIdx.x], Ax, F, colj);
 }
 
 // ---------------------------------------------------------------------------
@@ -555,7 +602,7 @@ __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask*
 hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count, int maxm, const double* Ax,
                               hipStream_t st) {
     if (count <= 0) return hipSuccess;
-    size_t lds = (size_t)maxm * maxm * sizeof(double);
+    const size_t lds = (size_t)maxm * (maxm + 1) / 2 * sizeof(double);
     hipLaunchKernelGGL(front_small_kernel, dim3(count), dim3(256), lds, st, P, nodes, Ax);
     return hipGetLastError();
 }

@@ -371,8 +371,17 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
         double* cb_pool = N.R[v].P.cb_pool;
         const std::vector<int64_t>& poff = N.R[v].panel_off;
         const std::vector<int64_t>& coff = N.R[v].cb_off;
-        // small fronts by LDS bucket
+        // small fronts: one launch sized for the level's largest front when the level
+        // fits one workgroup per CU (fewer dependent launches on thin levels), else one
+        // launch per LDS bucket (small fronts keep their occupancy on wide levels)
+        int nsmall = 0, bmax = 0;
+        for (int32_t s : nodes)
+            if (S.fclass[s] == FRONT_SMALL) {
+                ++nsmall;
+                bmax = std::max(bmax, bucket_of(S.sn_m[s]));
+            }
         for (int b : {32, 64, 96, 128}) {
+            if (nsmall <= 256 && b != bmax) continue;
             Launch L {};
             L.kind = L_SMALL;
             L.level = lev;
@@ -380,7 +389,7 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
             L.off = (int64_t)small.size();
             L.maxm = b;
             for (int32_t s : nodes)
-                if (S.fclass[s] == FRONT_SMALL && bucket_of(S.sn_m[s]) == b) small.push_back(s);
+                if (S.fclass[s] == FRONT_SMALL && (nsmall <= 256 || bucket_of(S.sn_m[s]) == b)) small.push_back(s);
             L.count = (int32_t)((int64_t)small.size() - L.off);
             if (L.count > 0) N.sched.push_back(L);
         }

@@ -47,7 +47,9 @@ def _rank_main(rank, world, port, k, opts, out):
         if rank == 0:
             sto, Lp, Li, Lxo = oracle.chol(A)
             ok_pat = np.array_equal(L.p, Lp) and np.array_equal(L.i, Li)
-            same = all(np.array_equal(p[0], parts[0][0]) and np.array_equal(p[1], parts[0][1]) for p in parts)
+            # L bitwise equal on every rank; x up to the solve's fp64-atomic summation order
+            same = all(np.array_equal(p[0], parts[0][0]) for p in parts) and all(
+                np.linalg.norm(p[1] - parts[0][1]) <= 1e-12 * np.linalg.norm(parts[0][1]) for p in parts)
             err = float(np.linalg.norm(L.x - Lxo) / np.linalg.norm(Lxo))
             U = _sym_full(A)
             be = float(np.abs(U @ x - b).max() / (np.abs(U).sum(axis=1).max() * np.abs(x).max() + np.abs(b).max()))
