@@ -82,6 +82,35 @@ def cb_syrk_traffic():
                       "profiles/r01/pmc_summary.json; L2-miss bytes incl. Infinity-Cache hits")
 
 
+def cb_syrk_mfma_counters():
+    """MFMA utilisation and clock of the CB SYRK from the committed counter pass
+    (scripts/gpu_mfma_util.sh: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024
+    SIMDs) on an eager bench step); None when the profile is absent."""
+    p = os.path.join(ROOT, "profiles", "r02", "mfma_util.json")
+    try:
+        with open(p) as f:
+            ks = json.load(f)["step_kernels"]
+    except (OSError, KeyError, ValueError):
+        return None
+    for name, v in ks.items():
+        if "syrk_mfma_kernel<128, 2, 4, 1>" in name:
+            return {"mfma_busy_frac": v["raw_mfma_ratio"], "clock_GHz": v["clock_GHz"],
+                    "source": "profiles/r02/mfma_util.json (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE)"}
+    return None
+
+
+def backward_error(A, x, b):
+    """Normwise backward error of x for the symmetric A held as upper CSC."""
+    import scipy.sparse as sp
+
+    U = sp.csc_matrix((A.x, A.i, A.p), shape=(A.n_cols, A.n_cols))
+    d = U.diagonal()
+    Ax = U @ x + U.T @ x - d * x
+    r = np.abs(Ax - b).max()
+    anorm = np.abs(U).sum(axis=0).A1 + np.abs(U).sum(axis=1).A1 - np.abs(d)
+    return float(r / (anorm.max() * np.abs(x).max() + np.abs(b).max()))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -209,6 +238,7 @@ def main():
         }
         if gms > 0:
             roof["gate_w256_tflops"] = round(gfl / (gms * 1e-3) / 1e12, 3)
+        roof["counters"] = cb_syrk_mfma_counters()
     pfl, pms, pnl = num.syrk_stats(-1) if not args.graph else (0.0, -1.0, 0)
     cfl, cms, cnl = num.syrk_stats(0)
     if roof is not None and pms > 0 and cms > 0:
@@ -216,13 +246,24 @@ def main():
                               "panel_update_ms": round(pms, 2), "panel_update_flops": pfl,
                               "cb_all_tflops": round(cfl / (cms * 1e-3) / 1e12, 2)}
 
+    mem = num.memory()  # before the solve allocates its buffers (and, multi-rank, the gathered factor)
+    # Validation of the factor just timed (outside the timed region): x = A^-1 b by
+    # the GPU triangular solves with that factor (multi-rank handles gather
+    # the factor collectively first), then the normwise backward error on the host,
+    # ||A x - b||_inf / (||A||_inf ||x||_inf + ||b||_inf), with A from the upper CSC.
+    # A wrong factor cannot pass: the bound is 1e-12 (measured 6.9e-16 at 128^3).
     solve = None
+    d_b = torch.ones(st["n"], dtype=torch.float64, device=f"cuda:{dev}")
+    d_x = torch.empty_like(d_b)
+    torch.cuda.synchronize()  # d_b complete before the library stream reads it
+    num.solve_device(d_b.data_ptr(), d_x.data_ptr())
+    x = d_x.cpu().numpy()
+    berr = backward_error(A, x, np.ones(st["n"]))
+    if not berr < 1e-12:
+        raise SystemExit(f"validation failed: backward error {berr:.3e} of the timed factor")
     if world == 1 and not args.no_solve:
-        # triangular solves with the factor: forward + backward sweep, each
-        # reads L once (8 * panel entries bytes, relaxed zeros included)
-        d_b = torch.ones(st["n"], dtype=torch.float64, device=f"cuda:{dev}")
-        d_x = torch.empty_like(d_b)
-        num.solve_device(d_b.data_ptr(), d_x.data_ptr())
+        # solve timing: forward + backward sweep, each reads L once (8 * panel entries
+        # bytes, relaxed zeros included)
         reps = 3
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -233,7 +274,6 @@ def main():
         lbytes = 2.0 * 8.0 * st["panel_entries"]
         solve = {"ms": round(sms, 3), "L_read_GBs": round(lbytes / (sms * 1e-3) / 1e9, 1),
                  "note": "x = A^-1 b, device vectors, forward + backward sweep; GB/s = 2 x 8 B x panel entries / time"}
-
     out = {
         "metric": "numeric-factorization fp64 GFLOP/s (F=sum colcount^2)",
         "value": round(gflops, 2),
@@ -263,6 +303,11 @@ def main():
         "roofline": roof,
         "timing_s": {"generate": round(t_gen, 3), "analyze": round(t_an, 3), "numeric_create": round(t_alloc, 3)},
         "phase_ms": phases,
+        "validation": {"backward_error": float(f"{berr:.3e}"), "bound": 1e-12,
+                       "check": "GPU solve with the timed factor, ||Ax-b||/(||A|| ||x||+||b||), inf-norms"},
+        "device_memory_GB": {"total": round(mem["total"] / 1e9, 2), "panels_L": round(mem["panel"] / 1e9, 2),
+                             "work_arena_CB": round(mem["work"] / 1e9, 2),
+                             "note": "rank 0 of the handle, factorization only (solve buffers excluded)"},
         "solve": solve,
     }
     if not args.no_cpu_baseline and rank == 0 and world == 1:

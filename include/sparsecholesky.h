@@ -44,7 +44,8 @@ enum sc_status {
     SC_ERR_DEVMEM = -4,   /* device allocation failed */
     SC_ERR_STATE = -5,    /* call out of order (e.g. export before factor) */
     SC_ERR_COMM = -6,     /* RCCL / transport error */
-    SC_ERR_NOTIMPL = -7
+    SC_ERR_NOTIMPL = -7,
+    SC_ERR_NOTSYM = -8    /* MatrixMarket input that is not symmetric (general / skew-symmetric) */
 };
 
 typedef struct sc_symbolic sc_symbolic;
@@ -234,7 +235,11 @@ int64_t sc_atree(int64_t n, const int64_t* Lp, const int32_t* Li, const int32_t*
 int64_t sc_triplet_to_csc(int64_t n, int64_t nt, const int32_t* ti, const int32_t* tj,
                           const double* tx, int64_t* Ap, int32_t* Ai, double* Ax);
 /* load_matrix_market_to_csc(filename)  include/mtx_reader.hpp:16-62, with the
- * banner honoured (symmetric / general / pattern).  Two-phase like above:
+ * banner honoured: coordinate real / integer / pattern (value 1); symmetric,
+ * hermitian or no banner as the reference; general must hold a symmetric matrix
+ * (both triangles, equal after summing duplicates; else SC_ERR_NOTSYM) and keeps
+ * its upper entries; skew-symmetric SC_ERR_NOTSYM; array / complex
+ * SC_ERR_NOTIMPL; out-of-range indices SC_ERR_ARG.  Two-phase like above:
  * first call with Ai==NULL returns n in *n and nnz; second fills. */
 int64_t sc_read_mtx(const char* path, int64_t* n, int64_t* Ap, int32_t* Ai, double* Ax);
 /* Synthetic 3D 7-point Laplacian on a k^3 grid in deterministic geometric

@@ -53,6 +53,7 @@ const char* sc_status_string(int64_t st) {
         case SC_ERR_STATE: return "call out of order";
         case SC_ERR_COMM: return "communication error";
         case SC_ERR_NOTIMPL: return "not implemented";
+        case SC_ERR_NOTSYM: return "matrix is not symmetric";
     }
     return "unknown status";
 }

@@ -709,9 +709,13 @@ __global__ __launch_bounds__(256) void mfma_peak_kernel(double* out, int iters) 
 #pragma unroll
     for (int j = 0; j < NACC; ++j) acc[j] = (double4_t){0.0, 0.0, 0.0, 0.0};
     const double a = 1.0 + threadIdx.x * 1e-9, b = 1.0 - blockIdx.x * 1e-9;
-    for (int i = 0; i < iters; ++i) {
+    // 16 MFMAs per accumulator per trip: the compiler moves the accumulators between
+    // VGPRs and AGPRs at the loop edge, which a short body would not amortise
+    for (int i = 0; i < iters; i += 16) {
 #pragma unroll
-        for (int j = 0; j < NACC; ++j) acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[j], 0, 0, 0);
+        for (int u = 0; u < 16; ++u)
+#pragma unroll
+            for (int j = 0; j < NACC; ++j) acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[j], 0, 0, 0);
     }
     double s = 0.0;
 #pragma unroll
@@ -720,7 +724,9 @@ __global__ __launch_bounds__(256) void mfma_peak_kernel(double* out, int iters) 
 }
 
 hipError_t launch_mfma_peak(double* out, int blocks, int iters, int nacc, hipStream_t st) {
-    if (nacc == 8)
+    if (nacc == 16)
+        hipLaunchKernelGGL((mfma_peak_kernel<16>), dim3(blocks), dim3(256), 0, st, out, iters);
+    else if (nacc == 8)
         hipLaunchKernelGGL((mfma_peak_kernel<8>), dim3(blocks), dim3(256), 0, st, out, iters);
     else if (nacc == 2)
         hipLaunchKernelGGL((mfma_peak_kernel<2>), dim3(blocks), dim3(256), 0, st, out, iters);
@@ -731,12 +737,13 @@ hipError_t launch_mfma_peak(double* out, int blocks, int iters, int nacc, hipStr
 
 // ---------------------------------------------------------------------------
 // Triangular solves with the supernodal factor (the
-// reference has no solve).  Level-scheduled like the factorization; per 64-column
-// block of every supernode of a level: a one-wave diagonal solve (block staged in
-// LDS, pivot broadcast by readlane) and a multi-workgroup GEMV over the rows
-// below it.  HBM-bound: L is read once per sweep.
+// reference has no solve).  Level-scheduled like the factorization.  Forward:
+// one fused launch per 64-column step (solve_fwd_kernel).  Backward, per step in
+// reverse: the transposed GEMV over the rows below each 64-column block
+// (solve_gemv_kernel), then the one-wave diagonal solve L11^T x = c
+// (solve_diag_kernel).  HBM-bound: L is read once per sweep.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void solve_diag_kernel(SolvePlan P, const int2* __restrict__ tasks, int backward) {
+__global__ __launch_bounds__(256) void solve_diag_kernel(SolvePlan P, const int2* __restrict__ tasks) {
     __shared__ double Lb[PNB * (PNB + 1)];  // Lb[j * (PNB + 1) + i] = L(k0 + i, k0 + j)
     __shared__ double dinv[PNB];
     const int2 t = tasks[blockIdx.x];
@@ -758,34 +765,27 @@ __global__ __launch_bounds__(256) void solve_diag_kernel(SolvePlan P, const int2
     if (tid < nb) dinv[tid] = 1.0 / Lb[tid * (PNB + 1) + tid];
     __syncthreads();
     if (tid >= 64) return;
-    // lane i keeps its row (forward: L(i, j)) or column (backward: L(j, i)) of the
-    // block in registers; all 64 steps run (zero padding past nb is inert), fully
-    // unrolled so the pivot and its reciprocal come from readlane, not LDS
+    // lane i keeps column i of the block (L(j, i)) in registers; all 64 steps run
+    // (zero padding past nb is inert), fully unrolled so the pivot and its
+    // reciprocal come from readlane, not LDS
     double r[PNB];
 #pragma unroll
-    for (int j = 0; j < PNB; ++j) r[j] = backward ? Lb[lane * (PNB + 1) + j] : Lb[j * (PNB + 1) + lane];
+    for (int j = 0; j < PNB; ++j) r[j] = Lb[lane * (PNB + 1) + j];
     const double d = dinv[lane];
     double v = lane < nb ? P.c[c0 + k0 + lane] : 0.0;
-    if (!backward) {
 #pragma unroll
-        for (int j = 0; j < PNB; ++j) {  // y_j = v_j / L_jj; v_i -= L_ij y_j (i > j)
-            const double yj = readlane_f64(v, j) * readlane_f64(d, j);
-            v = lane == j ? yj : (lane > j ? v - r[j] * yj : v);
-        }
-    } else {
-#pragma unroll
-        for (int j = PNB - 1; j >= 0; --j) {  // x_j = v_j / L_jj; v_i -= L_ji x_j (i < j)
-            const double xj = readlane_f64(v, j) * readlane_f64(d, j);
-            v = lane == j ? xj : (lane < j ? v - r[j] * xj : v);
-        }
+    for (int j = PNB - 1; j >= 0; --j) {  // x_j = v_j / L_jj; v_i -= L_ji x_j (i < j)
+        const double xj = readlane_f64(v, j) * readlane_f64(d, j);
+        v = lane == j ? xj : (lane < j ? v - r[j] * xj : v);
     }
     if (lane < nb) P.c[c0 + k0 + lane] = v;
 }
 
-__global__ __launch_bounds__(SOLVE_ROWS) void solve_gemv_kernel(SolvePlan P, const int4* __restrict__ tasks,
-                                                                int backward) {
-    __shared__ double vb[SOLVE_ROWS];             // forward: y_blk; backward: x of the rows
-    __shared__ double T[PNB * (PNB + 1)];         // backward: 64-row chunk, T[j * (PNB + 1) + i]
+// c[blk] -= L[rows, blk]^T x[rows].  Per 64-row chunk: coalesced column loads into
+// LDS, then thread (column j, quarter g) sums 16 rows of column j.
+__global__ __launch_bounds__(SOLVE_ROWS) void solve_gemv_kernel(SolvePlan P, const int4* __restrict__ tasks) {
+    __shared__ double vb[SOLVE_ROWS];             // x of the rows
+    __shared__ double T[PNB * (PNB + 1)];         // 64-row chunk, T[j * (PNB + 1) + i]
     __shared__ double part[SOLVE_ROWS / 64][PNB];
     const int4 t = tasks[blockIdx.x];
     const int s = t.x, k0 = t.y, r0 = t.z;
@@ -798,24 +798,6 @@ __global__ __launch_bounds__(SOLVE_ROWS) void solve_gemv_kernel(SolvePlan P, con
     const int32_t* __restrict__ rows = P.rows + P.rows_ptr[s];
     const int r = r0 + tid;
     const bool live = r < m;
-    if (!backward) {
-        // one thread per row; 16 independent loads in flight per chunk
-        if (tid < PNB) vb[tid] = tid < nb ? P.c[c0 + k0 + tid] : 0.0;
-        __syncthreads();
-        double acc = 0.0;
-#pragma unroll
-        for (int jc = 0; jc < PNB; jc += 16) {
-            double v[16];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) v[q] = (live && jc + q < nb) ? pan[(int64_t)(jc + q) * m + r] : 0.0;
-#pragma unroll
-            for (int q = 0; q < 16; ++q) acc += v[q] * vb[jc + q];
-        }
-        if (live) unsafeAtomicAdd(P.c + rows[r], -acc);
-        return;
-    }
-    // backward: c[blk] -= L[rows, blk]^T x[rows].  Per 64-row chunk: coalesced
-    // column loads into LDS, then thread (column j, quarter g) sums 16 rows of column j.
     vb[tid] = live ? P.c[rows[r]] : 0.0;
     const int j = tid & 63, g = tid >> 6;
     double acc = 0.0;
@@ -910,15 +892,15 @@ __global__ void permute_kernel(double* __restrict__ dst, const double* __restric
         dst[i] = src[perm[i]];
 }
 
-hipError_t launch_solve_diag(const SolvePlan& P, const int2* tasks, int count, bool backward, hipStream_t st) {
+hipError_t launch_solve_diag(const SolvePlan& P, const int2* tasks, int count, hipStream_t st) {
     if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(solve_diag_kernel, dim3(count), dim3(256), 0, st, P, tasks, backward ? 1 : 0);
+    hipLaunchKernelGGL(solve_diag_kernel, dim3(count), dim3(256), 0, st, P, tasks);
     return hipGetLastError();
 }
 
-hipError_t launch_solve_gemv(const SolvePlan& P, const int4* tasks, int count, bool backward, hipStream_t st) {
+hipError_t launch_solve_gemv(const SolvePlan& P, const int4* tasks, int count, hipStream_t st) {
     if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(solve_gemv_kernel, dim3(count), dim3(SOLVE_ROWS), 0, st, P, tasks, backward ? 1 : 0);
+    hipLaunchKernelGGL(solve_gemv_kernel, dim3(count), dim3(SOLVE_ROWS), 0, st, P, tasks);
     return hipGetLastError();
 }
 

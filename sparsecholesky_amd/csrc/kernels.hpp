@@ -77,14 +77,15 @@ struct SolvePlan {
     double* y;                // forward result (fused steps write here; copied to c after the sweep)
 };
 constexpr int SOLVE_ROWS = 256;  // front rows per GEMV workgroup
-// tasks (s, k0): the 64-column diagonal block of supernode s at column k0;
-// forward L11 y = c, backward L11^T x = c, in place in c
-hipError_t launch_solve_diag(const SolvePlan& P, const int2* tasks, int count, bool backward, hipStream_t st);
-// tasks (s, k0, r0): front rows [r0, r0 + SOLVE_ROWS) below the block.  Forward:
-// c[rows[r]] -= L[r, blk] y_blk (fp64 atomics: fronts of a level share ancestors);
-// backward: c[blk] -= L[r, blk]^T x[rows[r]]
-hipError_t launch_solve_gemv(const SolvePlan& P, const int4* tasks, int count, bool backward, hipStream_t st);
-// fused forward step: tasks (s, k0, r0, writer); r0 < 0 = diagonal block only
+// Backward sweep.  tasks (s, k0): the 64-column diagonal block of supernode s at
+// column k0, L11^T x = c in place in c
+hipError_t launch_solve_diag(const SolvePlan& P, const int2* tasks, int count, hipStream_t st);
+// tasks (s, k0, r0): front rows [r0, r0 + SOLVE_ROWS) below the block,
+// c[blk] -= L[r, blk]^T x[rows[r]] (fp64 atomics across the block's workgroups)
+hipError_t launch_solve_gemv(const SolvePlan& P, const int4* tasks, int count, hipStream_t st);
+// Forward sweep, one fused launch per step: tasks (s, k0, r0, writer); every
+// workgroup solves L11 y = c_blk itself and applies c[rows[r]] -= L[r, blk] y
+// (fp64 atomics: fronts of a level share ancestors); r0 < 0 = diagonal block only
 hipError_t launch_solve_fwd(const SolvePlan& P, const int4* tasks, int count, hipStream_t st);
 // c[i] = b[perm[i]] (gather) or x[perm[i]] = c[i] (scatter)
 hipError_t launch_permute(double* dst, const double* src, const int32_t* perm, int64_t n, bool scatter,

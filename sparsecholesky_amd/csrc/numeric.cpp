@@ -1118,9 +1118,10 @@ int64_t numeric_export_cols(Numeric& N, int64_t j0, int64_t j1, int64_t* cp, int
 
 // ---------------- triangular solves ----------------
 // A = P^T L L^T P (P = etree postorder): c = P b; L y = c (levels up); L^T x = y
-// (levels down); x = P^T c.  Per level and 64-column step: diagonal solves of every
-// supernode with w > k0 (one wave each), GEMVs over the rows below (SOLVE_ROWS per
-// workgroup).  Forward runs the steps in order, backward in reverse (GEMV first).
+// (levels down); x = P^T c.  Per level and 64-column step, over every supernode with
+// w > k0: forward, one fused launch (each workgroup solves the diagonal block and
+// applies its SOLVE_ROWS rows below); backward, in reverse order, the transposed
+// GEMV over the rows below, then the one-wave diagonal solve.
 static int64_t solve_build(Numeric& N) {
     const Symbolic& S = *N.S;
     std::vector<std::vector<int32_t>> by_level((size_t)S.nlevels);
@@ -1196,14 +1197,13 @@ int64_t numeric_solve_device(Numeric& N, const double* d_b, double* d_x) {
     const int64_t n = N.S->n;
     if (n == 0) return SC_OK;
     hipStream_t s0 = N.stream;
-    if (!N.solve_gexec || N.solve_b != d_b || N.solve_x != d_x) {
+    // the graph reads b from and writes x to the handle's own vector io = d_sbuf[0, n),
+    // so it is captured once, whatever buffers the caller passes
+    double* io = N.d_sbuf;
+    if (!N.solve_gexec) {
         // ~700 dependent steps per sweep at 128^3: replayed as one hipGraph
-        if (N.solve_gexec) (void)hipGraphExecDestroy(N.solve_gexec);
-        if (N.solve_graph) (void)hipGraphDestroy(N.solve_graph);
-        N.solve_gexec = nullptr;
-        N.solve_graph = nullptr;
         HIP_TRY(hipStreamBeginCapture(s0, hipStreamCaptureModeThreadLocal));
-        hipError_t e = launch_permute(N.SP.c, d_b, N.d_post, n, false, s0);
+        hipError_t e = launch_permute(N.SP.c, io, N.d_post, n, false, s0);
         // forward: one fused launch per step (y to SP.y), then y -> c
         for (size_t i = 0; e == hipSuccess && i < N.solve_steps.size(); ++i) {
             const Numeric::SolveStep& t = N.solve_steps[i];
@@ -1213,20 +1213,21 @@ int64_t numeric_solve_device(Numeric& N, const double* d_b, double* d_x) {
             e = hipMemcpyAsync(N.SP.c, N.SP.y, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s0);
         for (size_t i = N.solve_steps.size(); e == hipSuccess && i-- > 0;) {
             const Numeric::SolveStep& t = N.solve_steps[i];
-            e = launch_solve_gemv(N.SP, N.d_sgemv + t.goff, t.gcount, true, s0);
-            if (e == hipSuccess) e = launch_solve_diag(N.SP, N.d_sdiag + t.doff, t.dcount, true, s0);
+            e = launch_solve_gemv(N.SP, N.d_sgemv + t.goff, t.gcount, s0);
+            if (e == hipSuccess) e = launch_solve_diag(N.SP, N.d_sdiag + t.doff, t.dcount, s0);
         }
-        if (e == hipSuccess) e = launch_permute(d_x, N.SP.c, N.d_post, n, true, s0);
+        if (e == hipSuccess) e = launch_permute(io, N.SP.c, N.d_post, n, true, s0);
         hipGraph_t g = nullptr;
         hipError_t e2 = hipStreamEndCapture(s0, &g);
         HIP_TRY(e);
         HIP_TRY(e2);
         N.solve_graph = g;
         HIP_TRY(hipGraphInstantiate(&N.solve_gexec, g, nullptr, nullptr, 0));
-        N.solve_b = d_b;
-        N.solve_x = d_x;
     }
+    const size_t nb = (size_t)n * sizeof(double);
+    if (d_b != io) HIP_TRY(hipMemcpyAsync(io, d_b, nb, hipMemcpyDeviceToDevice, s0));
     HIP_TRY(hipGraphLaunch(N.solve_gexec, s0));
+    if (d_x != io) HIP_TRY(hipMemcpyAsync(d_x, io, nb, hipMemcpyDeviceToDevice, s0));
     HIP_TRY(hipStreamSynchronize(s0));
     return SC_OK;
 }

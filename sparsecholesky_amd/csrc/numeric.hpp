@@ -227,10 +227,8 @@ struct Numeric {
     int4* d_sfwd = nullptr;  // fused forward steps (s, k0, r0, writer)
     int32_t* d_post = nullptr;
     double* d_sbuf = nullptr;  // host-interface staging (b in, x out)
-    hipGraph_t solve_graph = nullptr;  // both sweeps captured once per (b, x) pair
+    hipGraph_t solve_graph = nullptr;  // both sweeps captured once (b in / x out through d_sbuf)
     hipGraphExec_t solve_gexec = nullptr;
-    const double* solve_b = nullptr;
-    double* solve_x = nullptr;
 
     std::string err;
 };

@@ -58,9 +58,17 @@ i64 triplet_to_csc(i64 n, i64 nt, const i32* ti, const i32* tj, const double* tx
 }
 
 // MatrixMarket coordinate reader.  The reference skips '%' lines, reads
-// "m n nnz" and swaps every entry to the upper triangle (mtx_reader.hpp:26-52);
-// here the banner decides: symmetric -> as the reference; general -> only the
-// upper entries are kept (the lower ones are their mirrors); pattern -> value 1.
+// "m n nnz" and swaps every entry to the upper triangle (mtx_reader.hpp:26-52).
+// Here the banner "%%MatrixMarket matrix <format> <field> <symmetry>" decides:
+//   coordinate only (array: SC_ERR_NOTIMPL); field real / integer / pattern
+//   (pattern: value 1; complex: SC_ERR_NOTIMPL);
+//   symmetric, hermitian (real field) or no banner -> as the reference;
+//   general -> the file must hold both triangles of a symmetric matrix: after
+//     summing duplicates, every off-diagonal (r, c) must equal (c, r) exactly,
+//     else SC_ERR_NOTSYM; only the upper entries are kept (the reference's swap
+//     would add each mirror onto its twin and double the off-diagonal);
+//   skew-symmetric -> SC_ERR_NOTSYM (zero diagonal: never positive definite).
+// Indices out of [1, n], a non-square size or a short file: SC_ERR_ARG.
 i64 read_mtx(const char* path, i64* n_out, i64* Ap, i32* Ai, double* Ax) {
     std::ifstream f(path);
     if (!f) return SC_ERR_ARG;
@@ -71,33 +79,74 @@ i64 read_mtx(const char* path, i64* n_out, i64* Ap, i32* Ai, double* Ax) {
         std::string low = line;
         for (auto& ch : low) ch = (char)std::tolower((unsigned char)ch);
         if (low.rfind("%%matrixmarket", 0) == 0) {
-            if (low.find("pattern") != std::string::npos) pattern = true;
-            if (low.find("general") != std::string::npos) general = true;
-            if (low.find("complex") != std::string::npos) return SC_ERR_NOTIMPL;
+            std::istringstream hs(low);
+            std::string tag, object, format, field, symmetry;
+            hs >> tag >> object >> format >> field >> symmetry;
+            if (object != "matrix") return SC_ERR_ARG;
+            if (format == "array") return SC_ERR_NOTIMPL;
+            if (format != "coordinate") return SC_ERR_ARG;
+            if (field == "complex") return SC_ERR_NOTIMPL;
+            if (field == "pattern")
+                pattern = true;
+            else if (field != "real" && field != "integer" && field != "double")
+                return SC_ERR_ARG;
+            if (symmetry == "general")
+                general = true;
+            else if (symmetry == "skew-symmetric")
+                return SC_ERR_NOTSYM;
+            else if (symmetry != "symmetric" && symmetry != "hermitian")
+                return SC_ERR_ARG;
         } else {
             f.seekg(0);
         }
     }
-    while (f.peek() == '%') std::getline(f, line);
+    while (f.peek() == '%' || f.peek() == '\n') std::getline(f, line);
     i64 nr = 0, nc = 0, nl = 0;
     if (!(f >> nr >> nc >> nl)) return SC_ERR_ARG;
-    if (nr != nc || nr < 0) return SC_ERR_ARG;
+    if (nr != nc || nr < 0 || nl < 0 || nr > INT32_MAX) return SC_ERR_ARG;
     std::vector<i32> ti, tj;
     std::vector<double> tx;
     ti.reserve((size_t)nl);
     tj.reserve((size_t)nl);
     tx.reserve((size_t)nl);
+    struct Off {  // general: one off-diagonal entry of the pair {lo, hi}, side = (r > c)
+        i32 lo, hi;
+        int side;
+        double v;
+    };
+    std::vector<Off> off;
     for (i64 l = 0; l < nl; ++l) {
         i64 r, c;
         double v = 1.0;
         if (!(f >> r >> c)) return SC_ERR_ARG;
         if (!pattern && !(f >> v)) return SC_ERR_ARG;
+        if (r < 1 || c < 1 || r > nr || c > nr) return SC_ERR_ARG;
         --r;
         --c;
+        if (general && r != c) off.push_back({(i32)std::min(r, c), (i32)std::max(r, c), r > c ? 1 : 0, v});
         if (general && r > c) continue;
         ti.push_back((i32)r);
         tj.push_back((i32)c);
         tx.push_back(v);
+    }
+    if (general) {
+        // per pair, the summed upper side must equal the summed lower side (in input
+        // order per side, as triplet_to_csc sums duplicates)
+        std::stable_sort(off.begin(), off.end(), [](const Off& a, const Off& b) {
+            return a.hi != b.hi ? a.hi < b.hi : a.lo < b.lo;
+        });
+        for (size_t q = 0; q < off.size();) {
+            size_t e = q;
+            double sum[2] = {0.0, 0.0};
+            bool seen[2] = {false, false};
+            while (e < off.size() && off[e].lo == off[q].lo && off[e].hi == off[q].hi) {
+                sum[off[e].side] += off[e].v;
+                seen[off[e].side] = true;
+                ++e;
+            }
+            if (!seen[0] || !seen[1] || sum[0] != sum[1]) return SC_ERR_NOTSYM;
+            q = e;
+        }
     }
     *n_out = nr;
     return triplet_to_csc(nr, (i64)ti.size(), ti.data(), tj.data(), tx.data(), Ap, Ai, Ax);
