@@ -76,6 +76,10 @@ typedef struct sc_options {
                                 and the statistics are then those of P A P^T, solves take and return A's order */
     int32_t dist_early;      /* multi-GPU: a large child whose parent runs on another rank computes its CB in
                                 4-block column groups and sends each group as soon as it is done (1, default) */
+    int32_t dist_panel;      /* multi-GPU: a shared front wider than one slab (panel_nb_outer) has its panel
+                                factored 1D slab-cyclic over its rank group, each final slab sent to the ranks
+                                that update later slabs or its contribution block (1, default); 0: the panel
+                                on the front's owner */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };
@@ -273,11 +277,12 @@ int64_t sc_numeric_create_dist_emulated(const sc_symbolic* sym, int32_t device, 
  * posting order (comm steps ascending; all ranks follow one global step order). */
 int64_t sc_dist_schedule(const sc_symbolic* sym, int32_t nranks, int32_t rank, int32_t* step,
                          int32_t* peer, int64_t* bytes, int32_t* is_send, int64_t cap);
-/* Plan summary: per supernode the rank-group size (1 = inside one rank's subtree)
- * and, for split fronts, the number of ranks computing its contribution block
- * (0 = not split); *n_steps = comm steps.  Returns the total message count. */
+/* Plan summary: per supernode the rank-group size (1 = inside one rank's subtree),
+ * for split fronts the number of ranks computing its contribution block (0 = not
+ * split), for distributed panels the number of ranks factoring its slabs (0 = the
+ * panel on one rank); *n_steps = comm steps.  Returns the total message count. */
 int64_t sc_dist_plan_info(const sc_symbolic* sym, int32_t nranks, int32_t* gsize, int32_t* split_cb_ranks,
-                          int64_t* n_steps);
+                          int32_t* slab_ranks, int64_t* n_steps);
 /* Host-staged transport (tests / debugging without RCCL: several processes may
  * share one GPU).  The library calls fn(ctx, op, peer, buf, bytes) with op 0 =
  * post a send of host buffer buf, 1 = post a receive into buf, 2 = complete every

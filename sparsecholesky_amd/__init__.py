@@ -69,7 +69,7 @@ class Options(C.Structure):
         ("use_graph", C.c_int32), ("relax_wmax", C.c_int32), ("syrk_tile", C.c_int32),
         ("lookahead", C.c_int32), ("inner_order", C.c_int32),
         ("asm_tile_min_m", C.c_int32), ("dist_split", C.c_int32), ("dist_cbb", C.c_int32),
-        ("ordering", C.c_int32), ("dist_early", C.c_int32),
+        ("ordering", C.c_int32), ("dist_early", C.c_int32), ("dist_panel", C.c_int32),
     ]
 
 
@@ -135,7 +135,7 @@ _SIGS = [
     ("sc_dist_owner_map", _I64, [_P, _I32, _P, _P]),
     ("sc_numeric_create_dist", _I64, [_P, _I32, _I32, _I32, _P, C.POINTER(_P)]),
     ("sc_dist_schedule", _I64, [_P, _I32, _I32, _P, _P, _P, _P, _I64]),
-    ("sc_dist_plan_info", _I64, [_P, _I32, _P, _P, C.POINTER(_I64)]),
+    ("sc_dist_plan_info", _I64, [_P, _I32, _P, _P, _P, C.POINTER(_I64)]),
     ("sc_numeric_create_dist_host", _I64, [_P, _I32, _I32, _I32, C.c_void_p, _P, C.POINTER(_P)]),
     ("sc_numeric_create_dist_dry", _I64, [_P, _I32, _I32, _I32, C.POINTER(_P)]),
     ("sc_numeric_create_dist_emulated", _I64, [_P, _I32, _I32, _I32, C.POINTER(_P)]),
@@ -499,13 +499,15 @@ class Symbolic:
 
     def dist_plan_info(self, nranks: int) -> dict:
         """Multi-GPU plan summary: rank-group size per supernode, CB ranks of split fronts,
-        comm steps and total messages."""
+        slab ranks of distributed panels, comm steps and total messages."""
         ns = self.stats()["n_supernodes"]
         g = np.zeros(max(ns, 1), dtype=np.int32)
         cbr = np.zeros(max(ns, 1), dtype=np.int32)
+        slr = np.zeros(max(ns, 1), dtype=np.int32)
         nst = C.c_int64()
-        nmsg = _check(lib().sc_dist_plan_info(self.h, nranks, _ptr(g), _ptr(cbr), C.byref(nst)), "dist_plan_info")
-        return dict(gsize=g[:ns], split_cb_ranks=cbr[:ns], n_steps=nst.value, n_msgs=nmsg)
+        nmsg = _check(lib().sc_dist_plan_info(self.h, nranks, _ptr(g), _ptr(cbr), _ptr(slr), C.byref(nst)),
+                      "dist_plan_info")
+        return dict(gsize=g[:ns], split_cb_ranks=cbr[:ns], slab_ranks=slr[:ns], n_steps=nst.value, n_msgs=nmsg)
 
     def memory_plan(self, nranks: int = 1) -> dict:
         """Device memory plan without a device: per rank the panel arena (L), the

@@ -82,6 +82,7 @@ void sc_default_options(sc_options* opt) {
     opt->dist_split = 1;
     opt->dist_cbb = 1024;
     opt->dist_early = 1;
+    opt->dist_panel = 1;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,
@@ -484,7 +485,7 @@ int64_t sc_numeric_memory(sc_numeric* num, int64_t* info, int32_t n) {
 }
 
 int64_t sc_dist_plan_info(const sc_symbolic* sym, int32_t nranks, int32_t* gsize, int32_t* split_cb_ranks,
-                          int64_t* n_steps) {
+                          int32_t* slab_ranks, int64_t* n_steps) {
     if (!sym || nranks <= 0) return SC_ERR_ARG;
     sc::DistPlan D;
     int64_t rc = sc::dist_plan(sym->S, nranks, D);
@@ -499,6 +500,15 @@ int64_t sc_dist_plan_info(const sc_symbolic* sym, int32_t nranks, int32_t* gsize
                 v = (int32_t)(std::unique(r.begin(), r.end()) - r.begin());
             }
             split_cb_ranks[s] = v;
+        }
+        if (slab_ranks) {
+            int32_t v = 0;
+            if (D.pd[s] >= 0) {
+                std::vector<int32_t> r = D.slab_rank[D.pd[s]];
+                std::sort(r.begin(), r.end());
+                v = (int32_t)(std::unique(r.begin(), r.end()) - r.begin());
+            }
+            slab_ranks[s] = v;
         }
     }
     if (n_steps) *n_steps = (int64_t)D.steps.size();

@@ -17,6 +17,16 @@
 // front's flops) runs on the group in parallel and overlaps the owner's panel
 // chain.  Shared fronts without a CB (the root) run on their owner.
 //
+// Distributed panels (dist_panel).  A shared front wider than one slab has its
+// panel factored 1D slab-cyclic over its group (right-looking with lookahead, the
+// reference's level loop include/chol.hpp:1423-1443 parallelised inside the front):
+// the owner assembles the front and factors slab 0; slab k goes to group rank
+// (owner + k) mod g, which receives its assembled columns once (STEP_INIT).  When
+// slab k is final its owner sends its rows [need, m) (STEP_SLAB) to every rank that
+// updates a later slab or a CB block with it; each rank applies the slab's update
+// to the slabs and CB blocks it owns (the next slab first, on the critical path).
+// This covers the root, whose panel is the whole front.
+//
 // Transfers.  After each level, every CB column block whose producer is not the
 // executing rank of the parent goes there (STEP_DELIVER), packed (only rows
 // >= the block's first column: the lower part), so several links feed one parent
@@ -46,6 +56,36 @@ static double cb_work(const Symbolic& S, i32 s) {
     return mb * (mb + 1.0) * w;
 }
 
+// Panel work of columns [c0, c1) in right-looking order: column c takes the
+// updates of the c columns before it over rows [c, m)
+static double slab_work(const Symbolic& S, i32 s, int c0, int c1) {
+    const double m = S.sn_m[s];
+    double v = 0.0;
+    for (int c = c0; c < c1; ++c) v += 2.0 * (c + 1.0) * (m - c);
+    return v;
+}
+
+bool DistPlan::holds(int32_t s, int r) const {
+    if (owner[s] == r) return true;
+    if (pd.empty() || pd[s] < 0) return false;
+    const std::vector<int32_t>& h = holders[pd[s]];
+    return std::binary_search(h.begin(), h.end(), r);
+}
+
+int DistPlan::need_row(const Symbolic& S, int32_t s, int k, int r) const {
+    const int m = S.sn_m[s];
+    const std::vector<int32_t>& sr = slab_rank[pd[s]];
+    for (int j = k + 1; j < (int)sr.size(); ++j)
+        if (sr[j] == r) return j * nbo;
+    if (split[s] >= 0) {
+        for (i32 q : cb_rank[split[s]])
+            if (q == r) return S.w(s);
+    } else if (S.mb(s) > 0 && r == owner[s]) {  // unsplit: the owner updates the whole CB
+        return S.w(s);
+    }
+    return m;
+}
+
 int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
     if (nranks <= 0) return SC_ERR_ARG;
     D = DistPlan();
@@ -56,6 +96,7 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
     D.owner.assign((size_t)ns, 0);
     D.gsize.assign((size_t)ns, 1);
     D.split.assign((size_t)ns, -1);
+    D.pd.assign((size_t)ns, -1);
     D.work.assign((size_t)nranks, 0.0);
     std::vector<double> sub((size_t)ns, 0.0);
     for (i32 s = 0; s < ns; ++s) {  // children precede parents (postorder)
@@ -125,11 +166,24 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
         D.owner[s] = own;
         const int mb = S.mb(s), w = S.w(s);
         const bool split = S.opt.dist_split != 0 && S.fclass[s] == FRONT_LARGE && mb > 0;
+        const bool dpanel = S.opt.dist_panel != 0 && S.fclass[s] == FRONT_LARGE && w > D.nbo;
+        if (dpanel) {  // slab k on group rank (owner + k) mod g
+            const int g = hi - lo, nsl = (w + D.nbo - 1) / D.nbo;
+            std::vector<i32> sr((size_t)nsl);
+            for (int k = 0; k < nsl; ++k) {
+                sr[k] = lo + (own - lo + k) % g;
+                D.work[sr[k]] += slab_work(S, s, k * D.nbo, std::min(w, (k + 1) * D.nbo));
+            }
+            D.pd[s] = (i32)D.pd_s.size();
+            D.pd_s.push_back(s);
+            D.slab_rank.push_back(std::move(sr));
+            if (!split) D.work[own] += cb_work(S, s);
+        }
         if (!split) {
-            D.work[own] += front_work(S, s);
+            if (!dpanel) D.work[own] += front_work(S, s);
             continue;
         }
-        D.work[own] += front_work(S, s) - cb_work(S, s);
+        if (!dpanel) D.work[own] += front_work(S, s) - cb_work(S, s);
         const int nblk = (mb + D.cbb - 1) / D.cbb;
         std::vector<int> ord((size_t)nblk);
         for (int b = 0; b < nblk; ++b) ord[b] = b;  // block b has mb - b*cbb rows: descending work
@@ -146,12 +200,21 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
         D.split_s.push_back(s);
         D.cb_rank.push_back(std::move(cbr));
     }
+    D.holders.assign(D.pd_s.size(), std::vector<i32>());
+    for (size_t q = 0; q < D.pd_s.size(); ++q) {
+        const i32 s = D.pd_s[q];
+        std::vector<i32> h(D.slab_rank[q]);
+        if (D.split[s] >= 0) h.insert(h.end(), D.cb_rank[D.split[s]].begin(), D.cb_rank[D.split[s]].end());
+        std::sort(h.begin(), h.end());
+        h.erase(std::unique(h.begin(), h.end()), h.end());
+        D.holders[q] = std::move(h);
+    }
 
     D.early_gw = 4 * D.cbb;
     D.early.assign((size_t)ns, 0);
     for (i32 c = 0; c < ns; ++c) {
         const i32 p = S.sn_parent[c];
-        D.early[c] = S.opt.dist_early != 0 && p >= 0 && D.split[c] < 0 && D.owner[c] != D.owner[p] &&
+        D.early[c] = S.opt.dist_early != 0 && p >= 0 && D.split[c] < 0 && D.pd[c] < 0 && D.owner[c] != D.owner[p] &&
                      S.fclass[c] == FRONT_LARGE && S.mb(c) >= 2 * D.cbb;
     }
     // comm steps in the global order: per level, the split fronts' INIT and SLAB
@@ -174,9 +237,59 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
     auto close_step = [&](int32_t id) {  // drop a step without messages
         if (D.msgs.empty() || D.msgs.back().step != id) D.steps.pop_back();
     };
+    // a distributed panel's slab (panel columns [c0, c1), rows [r0, m)) from src to dst
+    auto panel_msg = [&](int32_t id, i32 s, int src, int dst, int r0, int c0, int c1) {
+        DistMsg g {};
+        g.step = id;
+        g.src = src;
+        g.dst = dst;
+        g.skind = g.dkind = R_PANEL;
+        g.srow = g.drow = r0;
+        g.scol = g.dcol = c0;
+        g.rows = S.sn_m[s] - r0;
+        g.cols = c1 - c0;
+        g.s = s;
+        D.msgs.push_back(g);
+    };
     for (i32 lev = 0; lev < S.nlevels; ++lev) {
         for (i32 s : by_level[lev]) {
-            if (D.split[s] < 0) continue;
+            if (D.pd[s] < 0) continue;
+            const std::vector<i32>& sr = D.slab_rank[D.pd[s]];
+            const int own = D.owner[s], w = S.w(s), nsl = (int)sr.size();
+            // INIT: assembled slab columns to their owners, CB blocks to the CB ranks
+            int32_t id = open_step(STEP_INIT, lev, s, 0);
+            for (int k = 1; k < nsl; ++k)
+                if (sr[k] != own) panel_msg(id, s, own, sr[k], k * D.nbo, k * D.nbo, std::min(w, (k + 1) * D.nbo));
+            if (D.split[s] >= 0) {
+                const std::vector<i32>& cbr = D.cb_rank[D.split[s]];
+                for (int jb = 0; jb < (int)cbr.size(); ++jb) {
+                    DistMsg g {};
+                    g.step = id;
+                    g.src = own;
+                    g.dst = cbr[jb];
+                    cb_block(g, s, jb);
+                    D.msgs.push_back(g);
+                }
+            }
+            close_step(id);
+            // SLAB k: rows [need, m) of the final slab to every holder that uses them,
+            // the next slab's owner first (its update is on the critical path)
+            for (int k = 0; k < nsl; ++k) {
+                const int k0 = k * D.nbo, k1 = std::min(w, k0 + D.nbo);
+                id = open_step(STEP_SLAB, lev, s, k);
+                std::vector<i32> dsts;
+                if (k + 1 < nsl && sr[k + 1] != sr[k]) dsts.push_back(sr[k + 1]);
+                for (i32 r : D.holders[D.pd[s]])
+                    if (r != sr[k] && (k + 1 >= nsl || r != sr[k + 1])) dsts.push_back(r);
+                for (i32 r : dsts) {
+                    const int need = D.need_row(S, s, k, r);
+                    if (need < S.sn_m[s]) panel_msg(id, s, sr[k], r, std::max(need, k1), k0, k1);
+                }
+                close_step(id);
+            }
+        }
+        for (i32 s : by_level[lev]) {
+            if (D.split[s] < 0 || D.pd[s] >= 0) continue;
             const std::vector<i32>& cbr = D.cb_rank[D.split[s]];
             const int own = D.owner[s], m = S.sn_m[s], w = S.w(s), mb = m - w;
             int32_t id = open_step(STEP_INIT, lev, s, 0);

@@ -23,6 +23,8 @@
 //   CB rank of split s      its column blocks (compact)  [L, L+1]; in place in a
 //                           full-square CB(s) when it also owns the parent
 //                           R_LAND(s) (the L21 slabs)     [L, L+1]
+//   holder of distributed s a full panel copy in the panel arena (permanent: its
+//                           slabs are part of the factor; gathered for export)
 #include <algorithm>
 #include <map>
 #include <queue>
@@ -130,6 +132,17 @@ int64_t place(std::vector<Req>& reqs, int64_t* live_max) {
 
 }  // namespace
 
+int64_t plan_rank_panels(const Symbolic& S, const DistPlan* D, int rank, std::vector<int64_t>& panel_off) {
+    panel_off.assign((size_t)S.ns, -1);
+    int64_t off = 0;
+    for (i32 s = 0; s < S.ns; ++s)
+        if (D ? D->holds(s, rank) : rank == 0) {
+            panel_off[s] = off;
+            off += (int64_t)S.sn_m[s] * S.w(s);
+        }
+    return off + PNB;
+}
+
 int64_t plan_rank_memory(const Symbolic& S, const DistPlan* D, int rank, RankMem& R,
                          std::vector<PlacedRegion>* placed) {
     const i32 ns = S.ns;
@@ -139,13 +152,7 @@ int64_t plan_rank_memory(const Symbolic& S, const DistPlan* D, int rank, RankMem
     R.land_off.assign((size_t)ns, -1);
     R.blk_off.assign(D ? D->split_s.size() : 0, std::vector<int64_t>());
     auto owner = [&](i32 s) { return D ? D->owner[s] : 0; };
-    int64_t off = 0;
-    for (i32 s = 0; s < ns; ++s)
-        if (owner(s) == rank) {
-            R.panel_off[s] = off;
-            off += (int64_t)S.sn_m[s] * S.w(s);
-        }
-    R.panel_total = off + PNB;
+    R.panel_total = plan_rank_panels(S, D, rank, R.panel_off);
     std::vector<Req> reqs;
     auto req = [&](int64_t size, i32 t0, i32 t1, int64_t* out) { reqs.push_back({align_up(size), t0, t1, out}); };
     for (i32 s = 0; s < ns; ++s) {
@@ -177,7 +184,7 @@ int64_t plan_rank_memory(const Symbolic& S, const DistPlan* D, int rank, RankMem
                 req(rows * cols, L, L + 1, &R.blk_off[sp][jb]);
             }
         }
-        if (cbrank) req(mb * S.w(s), L, L + 1, &R.land_off[s]);
+        if (cbrank && D->pd[s] < 0) req(mb * S.w(s), L, L + 1, &R.land_off[s]);  // else its panel copy
     }
     R.work_total = place(reqs, &R.work_live_max);
     if (placed)

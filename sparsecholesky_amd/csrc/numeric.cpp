@@ -161,20 +161,25 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
     const bool multi = !N.owner.empty();
     const DistPlan* Dp = multi ? &D : nullptr;
     auto is_split = [&](int32_t s) { return multi && D.split[s] >= 0; };
+    auto is_dpanel = [&](int32_t s) { return multi && D.pd[s] >= 0; };
     std::vector<int32_t> hosted_of((size_t)std::max(N.nranks, 1), -1);  // rank -> index into N.R
     for (size_t v = 0; v < N.R.size(); ++v) hosted_of[N.R[v].rank] = (int32_t)v;
     std::vector<int32_t> init_step, slab_step0, early_step0, deliver_step((size_t)S.nlevels, -1);
+    std::vector<std::vector<int32_t>> slab_step;  // distributed panels: step of slab k, -1 = none
     std::vector<std::vector<int>> early_ev((size_t)S.ns);  // sender: event after each CB column group
     std::vector<int64_t> step_beg;
     std::vector<char> emitted;
     if (multi) {
         init_step.assign((size_t)S.ns, -1);
         slab_step0.assign((size_t)S.ns, -1);
+        slab_step.assign((size_t)S.ns, std::vector<int32_t>());
+        for (size_t q = 0; q < D.pd_s.size(); ++q) slab_step[D.pd_s[q]].assign(D.slab_rank[q].size(), -1);
         early_step0.assign((size_t)S.ns, -1);
         for (int32_t id = 0; id < (int32_t)D.steps.size(); ++id) {
             const DistStep& t = D.steps[id];
             if (t.kind == STEP_INIT) init_step[t.s] = id;
             if (t.kind == STEP_SLAB && t.k == 0) slab_step0[t.s] = id;
+            if (t.kind == STEP_SLAB && D.pd[t.s] >= 0) slab_step[t.s][t.k] = id;
             if (t.kind == STEP_DELIVER && t.s < 0) deliver_step[t.level] = id;
             if (t.kind == STEP_DELIVER && t.s >= 0 && t.k == 0) early_step0[t.s] = id;
         }
@@ -565,6 +570,163 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
             push_gemm_launch(L_CB, lev, cbt, big, fl);
         }
     };
+    // Distributed panel of front s (dist.cpp): every hosted rank of its holders.  Per
+    // slab k: its owner factors it (the 64-column POTRF / TRSM / inner-update chain
+    // on the main stream), the SLAB step moves it, then every rank that needs it
+    // updates its own next slab on the main stream (critical path) and its other
+    // later slabs and CB blocks on the lookahead stream.  A lookahead-stream update
+    // of slab j (from slab k <= j - 2) is waited for before the main stream touches
+    // slab j (event after the lookahead launch of step j - 2, covering all earlier
+    // ones: the stream is in order).
+    auto emit_dist_front = [&](int32_t lev, int32_t s) {
+        const int q = D.pd[s];
+        const std::vector<int32_t>& sr = D.slab_rank[q];
+        const int w = S.w(s), m = S.sn_m[s], mb = m - w, nsl = (int)sr.size();
+        const int own = D.owner[s];
+        std::vector<int> vs;  // hosted holders
+        for (int32_t r : D.holders[q])
+            if (hosted_of[r] >= 0) vs.push_back(hosted_of[r]);
+        if (hosted_of[own] >= 0 && std::find(vs.begin(), vs.end(), hosted_of[own]) == vs.end())
+            vs.push_back(hosted_of[own]);
+        if (vs.empty()) return;
+        auto pan_of = [&](int v) { return N.R[v].P.panel_pool + N.R[v].panel_off[s]; };
+        auto slab_c0 = [&](int k) { return k * D.nbo; };
+        auto slab_c1 = [&](int k) { return std::min(w, (k + 1) * D.nbo); };
+        const int vo = hosted_of[own];
+        if (vo >= 0) {  // the owner assembles the whole front (tiled or column-streaming)
+            const int tile_min_m = S.opt.asm_tile_min_m > 0 ? S.opt.asm_tile_min_m : ASM_TILE_MIN_M;
+            Launch L {};
+            L.kind = L_ASM;
+            L.level = lev;
+            L.vr = vo;
+            L.big = m >= tile_min_m ? 1 : 0;
+            L.off = (int64_t)asmv.size();
+            for (int cb = 0; cb * ASM_COLS < m; ++cb) {
+                if (!L.big) {
+                    asmv.push_back(make_int2(s, cb));
+                    continue;
+                }
+                for (int kk = cb * ASM_COLS / ASM_ROWS; kk * ASM_ROWS < m; ++kk)
+                    asmv.push_back(make_int2(s, (kk << 16) | cb));
+            }
+            L.count = (int32_t)((int64_t)asmv.size() - L.off);
+            N.sched.push_back(L);
+        }
+        emit_step(init_step[s]);
+        std::vector<std::vector<int>> ev1((size_t)N.R.size(), std::vector<int>((size_t)nsl, -1));
+        auto last_ev1 = [&](int v, int kmax) {  // latest lookahead event of steps <= kmax
+            for (int k = std::min(kmax, nsl - 1); k >= 0; --k)
+                if (ev1[v][k] >= 0) return ev1[v][k];
+            return -1;
+        };
+        auto upd_task = [&](std::vector<GemmTask>& vec, double& fl, double* C, int64_t ldc, const double* A,
+                            int64_t lda, int M, int Nn, int K) {
+            if (M <= 0 || Nn <= 0 || K <= 0) return;
+            GemmTask t {};
+            t.C = C;
+            t.A = A;
+            t.ldc = ldc;
+            t.lda = lda;
+            t.M = M;
+            t.N = Nn;
+            t.K = K;
+            vec.push_back(t);
+            fl += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
+        };
+        for (int k = 0; k < nsl; ++k) {
+            const int k0s = slab_c0(k), k1s = slab_c1(k);
+            const int vk = hosted_of[sr[k]];
+            if (vk >= 0) {
+                // factor slab k: per 64 columns POTRF, TRSM of the rows below, and the
+                // update of the slab's next columns (recursive order, as emit_level)
+                const int e = last_ev1(vk, k - 2);
+                if (e >= 0) push_wait(0, e);
+                double* pan = pan_of(vk);
+                for (int k0 = k0s; k0 < k1s; k0 += PNB) {
+                    const int nb = std::min(PNB, k1s - k0), k1 = k0 + nb;
+                    Launch Lp {};
+                    Lp.kind = L_POTRF;
+                    Lp.level = lev;
+                    Lp.vr = vk;
+                    Lp.off = (int64_t)potrf.size();
+                    Lp.count = 1;
+                    potrf.push_back(make_int2(s, k0));
+                    N.sched.push_back(Lp);
+                    Launch Lt {};
+                    Lt.kind = L_TRSM;
+                    Lt.level = lev;
+                    Lt.vr = vk;
+                    Lt.off = (int64_t)trsm.size();
+                    Lt.big = nb < PNB ? 1 : 0;
+                    for (int r0 = k1; r0 < m; r0 += TRSM_ROWS) trsm.push_back(make_int4(s, k0, r0, 0));
+                    Lt.count = (int32_t)((int64_t)trsm.size() - Lt.off);
+                    if (Lt.count > 0) N.sched.push_back(Lt);
+                    if (k1 < k1s) {
+                        std::vector<GemmTask> upd;
+                        double fl = 0.0;
+                        if (S.opt.inner_order == 1) {
+                            const int b = (k0 - k0s) / PNB;
+                            const int span = PNB << __builtin_ctz((unsigned)(b + 1));
+                            const int c1 = std::min(k1s, k1 + span);
+                            upd_task(upd, fl, pan + (int64_t)k1 * m + k1, m, pan + (int64_t)(k1 - span) * m + k1, m,
+                                     m - k1, c1 - k1, span);
+                        } else {
+                            upd_task(upd, fl, pan + (int64_t)k1 * m + k1, m, pan + (int64_t)k0 * m + k1, m, m - k1,
+                                     k1s - k1, nb);
+                        }
+                        push_gemm_launch(L_PANEL, lev, upd, 0, fl);
+                    }
+                }
+            }
+            if (slab_step[s].size() > (size_t)k) emit_step(slab_step[s][k]);
+            // slab k's update on every hosted rank that needs it
+            for (int v : vs) {
+                const int r = N.R[v].rank;
+                if (D.need_row(S, s, k, r) >= m) continue;
+                double* pan = pan_of(v);
+                const double* Lk = pan + (int64_t)k0s * m;  // column k0s of the slab, row 0
+                const int K = k1s - k0s;
+                if (k + 1 < nsl && sr[k + 1] == r) {  // the next slab: critical path
+                    const int e = last_ev1(v, k - 1);
+                    if (e >= 0) push_wait(0, e);
+                    const int j0 = slab_c0(k + 1), j1 = slab_c1(k + 1);
+                    std::vector<GemmTask> t0;
+                    double fl = 0.0;
+                    upd_task(t0, fl, pan + (int64_t)j0 * m + j0, m, Lk + j0, m, m - j0, j1 - j0, K);
+                    push_gemm_launch(L_PANEL, lev, t0, 0, fl);
+                }
+                std::vector<GemmTask> t1;
+                double fl = 0.0;
+                for (int j = k + 2; j < nsl; ++j) {
+                    if (sr[j] != r) continue;
+                    const int j0 = slab_c0(j), j1 = slab_c1(j);
+                    upd_task(t1, fl, pan + (int64_t)j0 * m + j0, m, Lk + j0, m, m - j0, j1 - j0, K);
+                }
+                if (is_split(s) && r != own) {  // CB blocks: CB -= L21_k L21_k^T
+                    const std::vector<int32_t>& cbr = D.cb_rank[D.split[s]];
+                    for (int jb = 0; jb < (int)cbr.size(); ++jb) {
+                        if (cbr[jb] != r) continue;
+                        const int r0 = jb * D.cbb;
+                        int64_t ldc = 0;
+                        double* C = addr(v, R_CB, s, r0, r0, ldc);
+                        upd_task(t1, fl, C, ldc, Lk + w + r0, m, mb - r0, std::min(D.cbb, mb - r0), K);
+                    }
+                } else if (!is_split(s) && mb > 0 && r == own) {  // unsplit: the owner's whole CB
+                    int64_t ldc = 0;
+                    double* C = addr(v, R_CB, s, 0, 0, ldc);
+                    upd_task(t1, fl, C, ldc, Lk + w, m, mb, mb, K);
+                }
+                if (t1.empty()) continue;
+                push_wait(1, push_record(0));
+                push_gemm_launch(L_PANEL, lev, t1, 0, fl, 1);
+                ev1[v][k] = push_record(1);
+            }
+        }
+        for (int v : vs) {  // join the lookahead stream before the level's deliveries
+            const int e = last_ev1(v, nsl - 1);
+            if (e >= 0) push_wait(0, e);
+        }
+    };
     if (multi) push_wait(2, push_record(0));  // previous factorization's reads are done
     // multi-rank work-arena reuse guard (memplan.cpp): the comm steps of level L run
     // after the main stream has finished level L - 1, and the main stream starts level
@@ -583,14 +745,16 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
             }
             std::vector<int32_t> mine;
             for (int32_t s : by_level[lev])
-                if (D.owner[s] == N.R[v].rank) mine.push_back(s);
+                if (D.owner[s] == N.R[v].rank && !is_dpanel(s)) mine.push_back(s);
             if (!mine.empty()) emit_level(lev, mine, (int)v);
         }
         if (!multi) continue;
+        for (int32_t s : by_level[lev])
+            if (is_dpanel(s)) emit_dist_front(lev, s);
         // contribution-block ranks of this level's split fronts (emulated: after the
         // owners' panels, whose steps already moved the data)
         for (int32_t s : by_level[lev]) {
-            if (!is_split(s)) continue;
+            if (!is_split(s) || is_dpanel(s)) continue;
             const std::vector<int32_t>& cbr = D.cb_rank[D.split[s]];
             for (size_t v = 0; v < N.R.size(); ++v) {
                 const int who = N.R[v].rank;
@@ -629,20 +793,38 @@ int64_t numeric_create(const Symbolic& S, int device, Numeric*& out, std::string
     return SC_OK;
 }
 
-// Gathered panel layout: every rank's arena back to back (rank_base), each arena the
-// panels of the supernodes the rank owns in supernode order (plan_rank_memory).
-static void panel_layout(const Symbolic& S, const std::vector<int32_t>& owner, int nranks,
-                         std::vector<int64_t>& rank_base, std::vector<int64_t>& gpo) {
-    std::vector<int64_t> tot((size_t)nranks, 0);
-    gpo.assign((size_t)S.ns, 0);
+// Gathered panel layout: every rank's panel arena back to back (rank_base), each as
+// plan_rank_panels lays it out; a supernode's factor is its owner's copy (gpo).  The
+// slabs of a distributed panel that other ranks factored are copied into the owner's
+// copy after the exchange (fix).
+static void panel_layout(Numeric& N, const Symbolic& S, int nranks) {
+    const DistPlan* D = N.owner.empty() ? nullptr : &N.D;
+    std::vector<std::vector<int64_t>> po((size_t)nranks);
+    N.rank_base.assign((size_t)nranks + 1, 0);
+    for (int r = 0; r < nranks; ++r) N.rank_base[r + 1] = N.rank_base[r] + plan_rank_panels(S, D, r, po[r]);
+    N.gpo.assign((size_t)S.ns, 0);
     for (int32_t s = 0; s < S.ns; ++s) {
-        const int r = owner.empty() ? 0 : owner[s];
-        gpo[s] = tot[r];
-        tot[r] += (int64_t)S.sn_m[s] * S.w(s);
+        const int r = D ? D->owner[s] : 0;
+        N.gpo[s] = N.rank_base[r] + po[r][s];
     }
-    rank_base.assign((size_t)nranks + 1, 0);
-    for (int r = 0; r < nranks; ++r) rank_base[r + 1] = rank_base[r] + tot[r] + PNB;
-    for (int32_t s = 0; s < S.ns; ++s) gpo[s] += rank_base[owner.empty() ? 0 : owner[s]];
+    N.fix.clear();
+    if (!D) return;
+    for (size_t q = 0; q < D->pd_s.size(); ++q) {
+        const int32_t s = D->pd_s[q];
+        const int m = S.sn_m[s], w = S.w(s);
+        for (int k = 0; k < (int)D->slab_rank[q].size(); ++k) {
+            const int r = D->slab_rank[q][k];
+            if (r == D->owner[s]) continue;
+            const int k0 = k * D->nbo, k1 = std::min(w, k0 + D->nbo);
+            Numeric::SlabFix f {};
+            f.src = N.rank_base[r] + po[r][s] + (int64_t)k0 * m + k0;
+            f.dst = N.gpo[s] + (int64_t)k0 * m + k0;
+            f.ld = m;
+            f.rows = m - k0;
+            f.cols = k1 - k0;
+            N.fix.push_back(f);
+        }
+    }
 }
 
 int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
@@ -702,7 +884,7 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
         const int r = (multi && N.emulated) ? (int)v : (multi ? N.rank : 0);
         plan_rank_memory(S, multi ? &N.D : nullptr, r, N.R[v]);
     }
-    panel_layout(S, N.owner, multi ? N.nranks : 1, N.rank_base, N.gpo);
+    panel_layout(N, S, multi ? N.nranks : 1);
     // ---- shared plan arrays ----
     DevPlan P0 {};
     int32_t *d_sn_start, *d_sn_m, *d_child_ptr, *d_child_list, *d_relind, *d_apos, *d_relbnd;
@@ -1039,10 +1221,16 @@ int64_t numeric_gather(Numeric& N) {
     if (!N.factored) return SC_ERR_STATE;
     const int64_t st = numeric_status(N);
     if (st < 0) return st;
-    if (N.owner.empty() || N.emulated) return SC_OK;  // the arenas are the gathered layout
+    if (N.owner.empty()) return SC_OK;  // single device: the arena is the factor
     if (N.gather_gen == N.factor_gen) return SC_OK;
-    const int64_t rc = dist_gather_panels(N);
-    if (rc != SC_OK) return rc;
+    // emulated handles: the hosted arenas, back to back, are the gathered layout
+    if (!N.emulated) TRY(dist_gather_panels(N));
+    // slabs of distributed panels into their owners' copies
+    for (const Numeric::SlabFix& f : N.fix)
+        HIP_TRY(hipMemcpy2DAsync(N.gpanel + f.dst, (size_t)f.ld * sizeof(double), N.gpanel + f.src,
+                                 (size_t)f.ld * sizeof(double), (size_t)f.rows * sizeof(double), (size_t)f.cols,
+                                 hipMemcpyDeviceToDevice, N.stream));
+    HIP_TRY(hipStreamSynchronize(N.stream));
     N.gather_gen = N.factor_gen;
     return SC_OK;
 }

@@ -69,6 +69,18 @@ struct DistPlan {
     std::vector<int32_t> split;    // index into split_s / cb_rank, or -1
     std::vector<int32_t> split_s;
     std::vector<std::vector<int32_t>> cb_rank;  // per split front: rank of CB column block jb
+    // distributed panels (dist_panel): a shared front wider than one slab has panel slab
+    // k (columns [k nbo, (k+1) nbo)) factored by slab_rank[pd[s]][k] (slab 0 on the
+    // owner, the rest cyclic over the group); every rank in holders[pd[s]] (slab owners
+    // and CB ranks, ascending) keeps a full m x w panel copy
+    std::vector<int32_t> pd;       // per supernode: index into pd_s / slab_rank / holders, or -1
+    std::vector<int32_t> pd_s;
+    std::vector<std::vector<int32_t>> slab_rank;
+    std::vector<std::vector<int32_t>> holders;
+    // first front row rank r needs of final slab k of distributed front s: the start of
+    // its first own slab after k, or w for a CB rank; m = not needed
+    int need_row(const Symbolic& S, int32_t s, int k, int r) const;
+    bool holds(int32_t s, int r) const;  // r keeps a panel copy of s (owner included)
     // early delivery: a large, unsplit child whose parent runs on another rank has its
     // CB SYRK in column groups of early_gw, each group sent as soon as it is computed
     int early_gw = 4096;
@@ -103,6 +115,9 @@ struct PlacedRegion {
 };
 int64_t plan_rank_memory(const Symbolic& S, const DistPlan* D, int rank, RankMem& R,
                          std::vector<PlacedRegion>* placed = nullptr);
+// Panel arena of `rank` alone: panel_off per supernode (-1 = no copy here); returns
+// the arena size in doubles (incl. the PNB tail the TRSM reads past)
+int64_t plan_rank_panels(const Symbolic& S, const DistPlan* D, int rank, std::vector<int64_t>& panel_off);
 int64_t plan_check(const Symbolic& S, int nranks);
 // Physical location of logical element (row, col) of region (kind, s) on R: arena
 // (0 panel, 1 work), offset in doubles and leading dimension.  false: not on R.
@@ -213,6 +228,11 @@ struct Numeric {
     int64_t gather_gen = -1;         // factor_gen the gathered copy belongs to
     std::vector<int64_t> gpo;        // per supernode: offset in gpanel
     int64_t* d_gpo = nullptr;
+    struct SlabFix {                 // gathered copy of a slab another rank factored
+        int64_t src, dst, ld;        // doubles into gpanel
+        int32_t rows, cols;
+    };
+    std::vector<SlabFix> fix;
 
     // triangular solves (built at the first solve)
     struct SolveStep {

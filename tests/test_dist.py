@@ -65,7 +65,9 @@ def _worker(rank, world, port, k, opts, out):
 
 @pytest.mark.parametrize("world,k,opts", [(2, 16, {}), (4, 20, {}),
                                           (4, 20, dict(panel_nb_outer=128, dist_cbb=64, small_front_max=32)),
-                                          (3, 24, dict(dist_cbb=128)), (4, 20, dict(dist_split=0))])
+                                          (3, 24, dict(dist_cbb=128)), (4, 20, dict(dist_split=0)),
+                                          (8, 24, dict(panel_nb_outer=128, dist_cbb=64)),
+                                          (4, 20, dict(panel_nb_outer=128, dist_panel=0))])
 def test_message_schedule_matches_across_ranks(world, k, opts):
     import random
 
@@ -97,3 +99,23 @@ def test_split_front_plan(k, nranks):
             assert g[v] <= g[par[v]]
     s0 = sc.Symbolic(sc.laplacian3d(k), panel_nb_outer=128, dist_cbb=64, small_front_max=32, dist_split=0)
     assert (s0.dist_plan_info(nranks)["split_cb_ranks"] == 0).all()
+
+
+@pytest.mark.parametrize("k,nranks", [(20, 4), (24, 8), (24, 3)])
+def test_distributed_panel_plan(k, nranks):
+    # shared fronts wider than one slab (the root included) have their slabs factored
+    # slab-cyclic over the whole group; narrower or unshared fronts stay on one rank
+    s = sc.Symbolic(sc.laplacian3d(k), panel_nb_outer=128, dist_cbb=64, small_front_max=32)
+    info = s.dist_plan_info(nranks)
+    sn = s.supernodes()
+    g, slr = info["gsize"], info["slab_ranks"]
+    root = int(np.nonzero(sn["parent"] < 0)[0][-1])
+    assert slr[root] == min(g[root], -(-int(sn["w"][root]) // 128))
+    for v in range(len(g)):
+        nsl = -(-int(sn["w"][v]) // 128)
+        if g[v] > 1 and nsl > 1:
+            assert slr[v] == min(g[v], nsl)
+        else:
+            assert slr[v] == 0
+    s0 = sc.Symbolic(sc.laplacian3d(k), panel_nb_outer=128, dist_cbb=64, small_front_max=32, dist_panel=0)
+    assert (s0.dist_plan_info(nranks)["slab_ranks"] == 0).all()

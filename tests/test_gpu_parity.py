@@ -341,7 +341,7 @@ def test_partitioned_schedule_bitwise_equal(gpu, nranks):
     # emulated in one process with its own memory and every contribution block moved
     # by the message plan, must reproduce the single-GPU factor bitwise
     A = sc.laplacian3d(20)
-    s = sc.Symbolic(A, dist_split=0)
+    s = sc.Symbolic(A, dist_split=0, dist_panel=0)
     ref = sc.Numeric(s)
     assert ref.factor(A.x) == 0
     _, L0 = ref.export()
@@ -353,18 +353,24 @@ def test_partitioned_schedule_bitwise_equal(gpu, nranks):
     assert rel_fro(L1.x, Lx) < TOL
 
 
-@pytest.mark.parametrize("nranks,rccl", [(2, False), (3, False), (4, False), (8, False),
-                                         (2, True), (4, True), (8, True)])
-def test_partitioned_split_fronts_emulated(gpu, nranks, rccl):
-    # split top fronts (panel on the owner, CB column blocks updated per slab by the
-    # other ranks of the group): every rank in one process with private memory, the
-    # messages moved as device copies or (rccl=True) as ncclSend/ncclRecv to self in
-    # one group per comm step on a 1-rank RCCL communicator (dist.cpp transfer_group).
-    # A missing or misplaced message leaves a rank with stale data: parity catches it.
+@pytest.mark.parametrize("nranks,rccl,opts", [
+    (2, False, {}), (3, False, {}), (4, False, {}), (8, False, {}), (2, True, {}), (4, True, {}), (8, True, {}),
+    (4, False, dict(dist_panel=0)), (3, False, dict(dist_split=0)), (8, True, dict(dist_split=0)),
+    (4, False, dict(lookahead=0, inner_order=0))])
+def test_partitioned_split_fronts_emulated(gpu, nranks, rccl, opts):
+    # split top fronts (CB column blocks updated per slab by the ranks of the group)
+    # and distributed panels (slabs factored 1D slab-cyclic over the group, the root
+    # included): every rank in one process with private memory, the messages moved as
+    # device copies or (rccl=True) as ncclSend/ncclRecv to self in one group per comm
+    # step on a 1-rank RCCL communicator (dist.cpp transfer_group).  A missing or
+    # misplaced message leaves a rank with stale data: parity catches it.
     A = sc.laplacian3d(20)
-    s = sc.Symbolic(A, panel_nb_outer=128, dist_cbb=64, small_front_max=32)
+    s = sc.Symbolic(A, panel_nb_outer=128, dist_cbb=64, small_front_max=32, **opts)
     info = s.dist_plan_info(nranks)
-    assert nranks == 2 or (info["split_cb_ranks"] > 0).any()
+    if opts.get("dist_split", 1):
+        assert nranks == 2 or (info["split_cb_ranks"] > 0).any()
+    if opts.get("dist_panel", 1):
+        assert (info["slab_ranks"] >= min(nranks, 2)).any()
     v = sc.Numeric(s, nranks=nranks, virtual=True, rccl_self=rccl)
     for _ in range(2):  # refactor through the same handle: arenas reused
         assert v.factor(A.x) == 0
