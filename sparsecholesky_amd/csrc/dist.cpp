@@ -167,7 +167,10 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
         const int mb = S.mb(s), w = S.w(s);
         const bool split = S.opt.dist_split != 0 && S.fclass[s] == FRONT_LARGE && mb > 0;
         const bool dpanel = S.opt.dist_panel != 0 && S.fclass[s] == FRONT_LARGE && w > D.nbo;
-        if (dpanel) {  // slab k on group rank (owner + k) mod g
+        if (dpanel) {
+            // slab k on group rank (owner + k) mod g: the whole group is free at a
+            // shared front (its subtrees are done), so the slabs go round the group
+            // rather than to the ranks with the least total work
             const int g = hi - lo, nsl = (w + D.nbo - 1) / D.nbo;
             std::vector<i32> sr((size_t)nsl);
             for (int k = 0; k < nsl; ++k) {
@@ -190,9 +193,9 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
         std::vector<i32> cbr((size_t)nblk, -1);
         for (int b : ord) {
             const double rows = mb - (double)b * D.cbb, cols = std::min<double>(D.cbb, rows);
-            int best = -1;
+            int best = -1;  // a distributed panel's owner is free after slab 0: it may take blocks
             for (int r = lo; r < hi; ++r)
-                if (r != own && (best < 0 || D.work[r] < D.work[best])) best = r;
+                if ((r != own || dpanel) && (best < 0 || D.work[r] < D.work[best])) best = r;
             cbr[b] = best;
             D.work[best] += w * (2.0 * rows * cols - cols * cols + cols);
         }
@@ -263,6 +266,7 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
             if (D.split[s] >= 0) {
                 const std::vector<i32>& cbr = D.cb_rank[D.split[s]];
                 for (int jb = 0; jb < (int)cbr.size(); ++jb) {
+                    if (cbr[jb] == own) continue;  // computed in place in the owner's CB
                     DistMsg g {};
                     g.step = id;
                     g.src = own;

@@ -702,7 +702,7 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     const int j0 = slab_c0(j), j1 = slab_c1(j);
                     upd_task(t1, fl, pan + (int64_t)j0 * m + j0, m, Lk + j0, m, m - j0, j1 - j0, K);
                 }
-                if (is_split(s) && r != own) {  // CB blocks: CB -= L21_k L21_k^T
+                if (is_split(s)) {  // CB blocks: CB -= L21_k L21_k^T
                     const std::vector<int32_t>& cbr = D.cb_rank[D.split[s]];
                     for (int jb = 0; jb < (int)cbr.size(); ++jb) {
                         if (cbr[jb] != r) continue;

@@ -91,7 +91,7 @@ def test_split_front_plan(k, nranks):
     assert (cbr > 0).any()
     for v in np.nonzero(cbr)[0]:
         assert g[v] > 1
-        assert 1 <= cbr[v] <= g[v] - 1
+        assert 1 <= cbr[v] <= g[v]  # the owner too when its panel is distributed
         assert sn["m"][v] > sn["w"][v]  # has a contribution block
     par = sn["parent"]
     for v in range(len(g)):  # groups only shrink going down the tree
