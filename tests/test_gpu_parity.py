@@ -272,8 +272,10 @@ def test_lap128_closed_blocks_parity_and_solve(gpu):
     n = A.size()
     num = sc.Numeric(sc.Symbolic(A))
     assert num.factor(A.x) == 0
-    # leading 65536 block: F = 2.06e10 (two 32^3-scale subtrees and their separator)
-    for a, J in ((0, 65536), (_closed_block_start(A, 32768, n // 2), 32768)):
+    # leading 131072 block: F = 8.32e10, its separators up to 2079 wide (factored in the
+    # full matrix as fronts with K = w >= 2048 CB updates on 128 x 128 tiles); a 32768
+    # block past n / 2
+    for a, J in ((0, 131072), (_closed_block_start(A, 32768, n // 2), 32768)):
         b = a + J
         cp, ri, rx = num.export_cols(a, b)
         col = np.repeat(np.arange(J), np.diff(cp))
@@ -293,6 +295,31 @@ def test_lap128_closed_blocks_parity_and_solve(gpu):
     be = _backward_error(A, x, bvec)
     print(f"lap128 solve backward error {be:.3e}")
     assert be < 1e-14
+
+
+@pytest.fixture(scope="module")
+def lap48_oracle():
+    A = sc.laplacian3d(48)
+    st, Lp, Li, Lx = oracle.chol(A)
+    assert st == 0
+    return A, Lp, Li, Lx
+
+
+@pytest.mark.parametrize("opts", [{}, dict(asm_tile_min_m=1024)], ids=["default", "tiled_asm"])
+def test_lap48_full_parity(gpu, lap48_oracle, opts):
+    # the whole 48^3 factor (n = 110592, F = 7.07e10: a 2304-wide root, CB SYRK with K
+    # up to 1152 on 128 x 128 tiles) against the oracle, exact pattern and rel-Fro;
+    # tiled_asm: every front with m >= 1024 assembled by the write-once tile kernel
+    A, Lp, Li, Lx = lap48_oracle
+    s = sc.Symbolic(A, **opts)
+    assert s.stats()["max_front_w"] >= 2048
+    num = sc.Numeric(s)
+    assert num.factor(A.x) == 0
+    _, L = num.export()
+    assert np.array_equal(L.p, Lp) and np.array_equal(L.i, Li)
+    err = rel_fro(L.x, Lx)
+    print(f"lap48 {opts}: rel-Fro {err:.3e}")
+    assert err < TOL
 
 
 def test_solve_after_failed_factor(gpu):
