@@ -301,6 +301,10 @@ int64_t sc_numeric_create_dist_dry(const sc_symbolic* sym, int32_t device, int32
  * pointers, column-major) through the fp64 MFMA SYRK kernel. */
 int64_t sc_debug_syrk(double* dC, int32_t ldc, const double* dA, int32_t lda, int32_t M, int32_t N,
                       int32_t K);
+/* Chain launches (runs of single small-front levels): enable = 1 makes the next
+ * eager factorizations record 8 shader-clock stamps per chained front (phase
+ * boundaries); enable = 0 copies up to cap of them to out.  Returns the count. */
+int64_t sc_debug_chain_stamps(sc_numeric* num, int32_t enable, uint64_t* out, int64_t cap);
 /* Microbenchmarks: which=0 register-only fp64 MFMA probe (TFLOP/s; M blocks of
  * 4 waves, K iterations, arg accumulators); which=1/5 the SYRK kernel on an M x M
  * triangle with depth K, tile arg (64/128), with / without the XCD tile order

@@ -145,6 +145,7 @@ _SIGS = [
     ("sc_debug_syrk", _I64, [_P, _I32, _P, _I32, _I32, _I32, _I32]),
     ("sc_debug_bench", _I64, [_I32, _I32, _I32, _I32, _I32, C.POINTER(_D)]),
     ("sc_device_count", _I64, []),
+    ("sc_debug_chain_stamps", _I64, [_P, _I32, _P, _I64]),
 ]
 
 _lib: Optional[C.CDLL] = None

@@ -285,6 +285,11 @@ int64_t sc_numeric_syrk_stats(sc_numeric* num, int32_t wmin, double* flops, doub
     return sc::numeric_syrk_stats(*num->N, wmin, flops, ms, launches);
 }
 
+int64_t sc_debug_chain_stamps(sc_numeric* num, int32_t enable, uint64_t* out, int64_t cap) {
+    if (!num || !num->N) return SC_ERR_ARG;
+    return sc::numeric_chain_stamps(*num->N, enable, out, cap);
+}
+
 void sc_free_numeric(sc_numeric* num) {
     if (!num) return;
     sc::numeric_free(num->N);

@@ -217,127 +217,384 @@ __device__ __forceinline__ void trsm_steps(double (&r)[PNB], const double* Lc, c
 }
 
 // ---------------------------------------------------------------------------
-// Small fronts (m <= 128): the whole front in LDS, one 256-thread workgroup per
-// front, the lower triangle packed by columns (column j holds rows j..m-1 at
-// j m - j (j - 1) / 2): 64.5 KB at m = 128, two workgroups per CU.
-//   1. assemble: zero, A entries of the pivot columns, the children's CBs
-//      (extend-add, one wave per child column, children in a fixed order:
-//      deterministic, no atomics);
-//   2. POTRF of the w x w diagonal block by one wave in registers (w <= 64);
-//   3. TRSM: one thread per row of L21 (independent rows);
-//   4. the panel and CB = F22 - L21 L21^T (the SYRK, one wave per CB column,
-//      w-long dot products from LDS) written straight to HBM.
-// Fronts wider than 64 take a right-looking loop over the panel columns instead.
+// Small fronts (m <= 128).  The front is assembled in LDS (lower triangle packed by
+// columns: column j holds rows j..m-1 at j m - j (j - 1) / 2) -- zero, the A entries
+// of the pivot columns, then the children's CBs in a fixed order (extend-add,
+// deterministic, no atomics) -- and then factored in REGISTERS: the 256 threads
+// hold 4 x 4 tiles of the lower front (KT tiles each), and the w pivot steps run
+// right-looking over the whole front at once, so POTRF, TRSM and the CB update
+// (the reference's dpotrf_ / cblas_dtrsm / cblas_dsyrk, chol.hpp:1263-1322) are
+// one loop.  Step J: the owners of column J publish it to LDS (double-buffered,
+// one barrier per step), every thread takes the pivot's 1/sqrt and updates its
+// tiles right of J.  The panel (columns < w) and the CB leave straight from the
+// registers: to HBM, or -- chain launches -- added into the parent's LDS front.
 // ---------------------------------------------------------------------------
+// 1/sqrt(d): v_rsq_f64 seed plus two Newton steps (~1 ulp; NaN/inf for d <= 0,
+// which the callers flag separately).
+__device__ __forceinline__ double rsqrt_f64(double d) {
+    double y = __builtin_amdgcn_rsq(d);
+    const double h = 0.5 * d;
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    return y;
+}
+
 __device__ __forceinline__ int pk_col(int m, int j) { return j * m - ((j * (j - 1)) >> 1); }
 
-__device__ __forceinline__ void small_front(const DevPlan& P, const int s, const double* __restrict__ Ax,
-                                            double* F, double* colj) {
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int c0 = P.sn_start[s];
-    const int w = P.sn_start[s + 1] - c0;
-    const int m = P.sn_m[s];
-    const int mb = m - w;
-    const int tot = (m * (m + 1)) >> 1;
-    for (int idx = tid; idx < tot; idx += 256) F[idx] = 0.0;
-    __syncthreads();
-    for (int lc = wid; lc < w; lc += 4) {
-        const int64_t a0 = P.a_ptr[c0 + lc], a1 = P.a_ptr[c0 + lc + 1];
-        double* Fc = F + pk_col(m, lc) - lc;
-        for (int64_t q = a0 + lane; q < a1; q += 64) Fc[P.a_pos[q]] = Ax[P.a_src[q]];
-    }
-    __syncthreads();
-    for (int ci = P.child_ptr[s]; ci < P.child_ptr[s + 1]; ++ci) {
-        const int c = P.child_list[ci];
-        const int mbc = P.sn_m[c] - (P.sn_start[c + 1] - P.sn_start[c]);
-        const int32_t* __restrict__ rel = P.relind + P.rel_ptr[c];
-        const double* __restrict__ cb = P.cb_pool + P.cb_off[c];
-        for (int jc = wid; jc < mbc; jc += 4) {
-            const int pj = rel[jc];
-            double* Fc = F + pk_col(m, pj) - pj;
-            const double* __restrict__ src = cb + (int64_t)jc * mbc;
-            for (int ic = jc + lane; ic < mbc; ic += 64) Fc[rel[ic]] += src[ic];
+// Workgroup barrier for LDS traffic only: waits for this wave's LDS operations, not
+// for its global stores (the panel / CB stores stay in flight across it).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Tile q -> (bi, bj), bi >= bj, for T tile rows of which the first WT tile columns
+// hold pivot columns: the WT * T - WT (WT - 1) / 2 panel tiles first, column by
+// column (neighbouring threads share a tile column, so the masked pivot-column work
+// stays wave-coherent), then the CB tiles row by row.
+__device__ __forceinline__ void tile_map(int q, int T, int WT, int& bi, int& bj) {
+    const int np = WT * T - WT * (WT - 1) / 2;
+    if (q < np) {
+        int c = 0, rem = q;
+        while (rem >= T - c) {
+            rem -= T - c;
+            ++c;
         }
-        __syncthreads();
+        bi = c + rem;
+        bj = c;
+        return;
     }
-    if (w <= PNB) {
-        if (wid == 0) {  // 2. POTRF, lane = row of the diagonal block
-            const bool live = lane < w;
-            double r[PNB];
+    const int r = q - np;
+    int b = (int)((sqrtf(8.0f * (float)r + 1.0f) - 1.0f) * 0.5f);
+    while (b * (b + 1) / 2 > r) --b;
+    while ((b + 1) * (b + 2) / 2 <= r) ++b;
+    bi = WT + b;
+    bj = WT + r - b * (b + 1) / 2;
+}
+
+constexpr int COLB = 132;  // column buffer stride (128 rows + a tile of slack)
+
+template <int KT>
+struct SmallRegs {
+    double v[KT][16];  // v[k][r * 4 + c] = F(4 bi_k + r, 4 bj_k + c)
+    int bi[KT], bj[KT];  // bi < 0: no tile
+};
+
+template <int KT, int NT = 256>
+__device__ __forceinline__ void small_tiles(SmallRegs<KT>& R, int m, int w) {
+    const int T = (m + 3) >> 2, WT = (w + 3) >> 2, ntile = T * (T + 1) / 2;
 #pragma unroll
-            for (int c = 0; c < PNB; ++c) r[c] = (live && c <= lane && c < w) ? F[pk_col(m, c) + lane - c] : 0.0;
-            potrf_steps<0>(r, colj, lane, w, P.info, c0);
-            if (live) {
+    for (int k = 0; k < KT; ++k) {
+        const int q = threadIdx.x + NT * k;
+        int bi = -1, bj = -1;
+        if (q < ntile) tile_map(q, T, WT, bi, bj);
+        R.bi[k] = bi;
+        R.bj[k] = bj;
+    }
+}
+
+// Load the tiles of the assembled packed front F (entries above the diagonal or
+// past m read as 0; they are never stored).
+template <int KT>
+__device__ __forceinline__ void small_load(SmallRegs<KT>& R, const double* F, int m) {
 #pragma unroll
-                for (int c = 0; c < PNB; ++c)
-                    if (c < w && c <= lane) F[pk_col(m, c) + lane - c] = r[c];
+    for (int k = 0; k < KT; ++k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int i = 4 * R.bi[k] + r, j = 4 * R.bj[k] + c;
+                R.v[k][r * 4 + c] = (R.bi[k] >= 0 && i < m && i >= j) ? F[pk_col(m, j) + i - j] : 0.0;
             }
-        }
-        __syncthreads();
-        if (tid < mb) {  // 3. TRSM, thread = row w + tid: x_j = (F_ij - sum_t<j x_t L_jt) / L_jj
-            const int i = w + tid;
-            int oj = 0;  // pk_col(m, j)
-            for (int j = 0; j < w; ++j) {
-                double acc = F[oj + i - j];
-                int ot = 0;
-                for (int t = 0; t < j; ++t) {
-                    acc -= F[ot + i - t] * F[ot + j - t];
-                    ot += m - t;
+}
+
+// The w pivot steps, right-looking over the whole front, four pivots (one tile
+// column) per step.  Step b (pivots J = 4b .. J + nb - 1, nb = min(4, w - J)): the
+// owners of tile column b publish its four columns (colbuf row-major, [row][4],
+// double-buffered: one barrier per step); every thread factors the 4 x 4 diagonal
+// block D itself (L_D), solves its rows i against it (l_i = c_i L_D^-T, l_i = L(i,
+// J..J+3)) and updates its tiles right of the block with the rank-nb product; tiles
+// in column b take l_i in the pivot columns (and the update in any CB column).
+// colbuf: 2 x 4 * COLB doubles.
+template <int KT>
+__device__ __forceinline__ void small_steps(SmallRegs<KT>& R, double* colbuf, int w, int32_t* info, int c0) {
+    for (int J = 0, b = 0; J < w; J += 4, ++b) {
+        double* cb = colbuf + (b & 1) * 4 * COLB;
+        const int nb = min(4, w - J);
+#pragma unroll
+        for (int k = 0; k < KT; ++k)  // publish tile column b
+            if (R.bj[k] == b) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    double* row = cb + 4 * (4 * R.bi[k] + r);
+                    *reinterpret_cast<double2*>(row) = make_double2(R.v[k][r * 4], R.v[k][r * 4 + 1]);
+                    *reinterpret_cast<double2*>(row + 2) = make_double2(R.v[k][r * 4 + 2], R.v[k][r * 4 + 3]);
                 }
-                F[oj + i - j] = acc / F[oj];
-                oj += m - j;
+            }
+        lds_barrier();
+        // L_D = chol(D), D = rows J..J+3 of the published columns; rc[k] = 1 / L_D(k, k)
+        double D[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const double2 x01 = *reinterpret_cast<const double2*>(cb + 4 * (J + r));
+            const double2 x23 = *reinterpret_cast<const double2*>(cb + 4 * (J + r) + 2);
+            D[r][0] = x01.x;
+            D[r][1] = x01.y;
+            D[r][2] = x23.x;
+            D[r][3] = x23.y;
+        }
+        double Ld[4][4], rc[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            double dd = D[c][c];
+#pragma unroll
+            for (int t = 0; t < c; ++t) dd = fma(-Ld[c][t], Ld[c][t], dd);
+            if (c < nb && threadIdx.x == 0 && !(dd > 0.0)) report_fail(info, c0 + J + c);
+            rc[c] = c < nb ? rsqrt_f64(dd) : 0.0;
+            Ld[c][c] = dd * rc[c];
+#pragma unroll
+            for (int r = c + 1; r < 4; ++r) {
+                double x = D[r][c];
+#pragma unroll
+                for (int t = 0; t < c; ++t) x = fma(-Ld[r][t], Ld[c][t], x);
+                Ld[r][c] = x * rc[c];
             }
         }
-    } else {
-        for (int k = 0; k < w; ++k) {  // right-looking over the panel columns
-            double* Fk = F + pk_col(m, k) - k;
-            if (tid == 0) {
-                const double d = Fk[k];
-                if (!(d > 0.0)) report_fail(P.info, c0 + k);
-                Fk[k] = sqrt(d);
+        // l of one row: l[k] = (c[k] - sum_t<k l[t] L_D(k, t)) / L_D(k, k) (0 past nb)
+        auto solve_row = [&](int row, double (&l)[4]) {
+            const double2 x01 = *reinterpret_cast<const double2*>(cb + 4 * row);
+            const double2 x23 = *reinterpret_cast<const double2*>(cb + 4 * row + 2);
+            const double cr[4] = {x01.x, x01.y, x23.x, x23.y};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                double x = cr[k];
+#pragma unroll
+                for (int t = 0; t < k; ++t) x = fma(-l[t], Ld[k][t], x);
+                l[k] = x * rc[k];
             }
-            __syncthreads();
-            const double inv = 1.0 / Fk[k];
-            for (int r = k + 1 + tid; r < m; r += 256) Fk[r] *= inv;
-            __syncthreads();
-            for (int j = k + 1 + wid; j < w; j += 4) {
-                double* Fj = F + pk_col(m, j) - j;
-                const double ljk = Fk[j];
-                for (int r = j + lane; r < m; r += 64) Fj[r] -= Fk[r] * ljk;
-            }
-            __syncthreads();
-        }
-    }
-    __syncthreads();
-    double* panel = P.panel_pool + P.panel_off[s];
-    for (int j = wid; j < w; j += 4) {
-        const double* Fj = F + pk_col(m, j) - j;
-        for (int i = j + lane; i < m; i += 64) panel[(int64_t)j * m + i] = Fj[i];
-    }
-    if (mb > 0) {  // 4. CB(ic, jc) = F22(ic, jc) - sum_t L21(ic, t) L21(jc, t)
-        double* cb = P.cb_pool + P.cb_off[s];
-        for (int jc = wid; jc < mb; jc += 4) {
-            const int jj = w + jc;
-            for (int ic = jc + lane; ic < mb; ic += 64) {
-                const int ii = w + ic;
-                double v = F[pk_col(m, jj) + ii - jj];
-                int ot = 0;
-                for (int t = 0; t < w; ++t) {
-                    v -= F[ot + ii - t] * F[ot + jj - t];
-                    ot += m - t;
+        };
+#pragma unroll
+        for (int k = 0; k < KT; ++k) {
+            const int bi = R.bi[k], bj = R.bj[k];
+            if (bi < 0 || bj < b) continue;  // no tile, or left of the block
+            double lj[4][4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) solve_row(4 * bj + c, lj[c]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                double li[4];
+                solve_row(4 * bi + r, li);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    double x = R.v[k][r * 4 + c];
+                    if (bj == b && c < nb) {  // tile column b: the pivot columns take l
+                        x = li[c];
+                    } else {
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) x = fma(-li[t], lj[c][t], x);
+                    }
+                    R.v[k][r * 4 + c] = x;
                 }
-                cb[(int64_t)jc * mb + ic] = v;
             }
         }
     }
 }
 
-// maxm: LDS edge of the launch (the packed front plus the POTRF column buffer)
+// The panel (columns < w, rows >= the column) to HBM.
+template <int KT>
+__device__ __forceinline__ void small_store_panel(const SmallRegs<KT>& R, double* __restrict__ panel, int m, int w) {
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+        if (R.bi[k] < 0 || 4 * R.bj[k] >= w) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int i = 4 * R.bi[k] + r, j = 4 * R.bj[k] + c;
+                if (j < w && i >= j && i < m) panel[(int64_t)j * m + i] = R.v[k][r * 4 + c];
+            }
+    }
+}
+
+// The CB (rows / cols >= w) to HBM, column-major, ld = mb.
+template <int KT>
+__device__ __forceinline__ void small_store_cb(const SmallRegs<KT>& R, double* __restrict__ cb, int m, int w) {
+    const int mb = m - w;
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+        if (R.bi[k] < 0 || 4 * R.bi[k] + 3 < w) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int i = 4 * R.bi[k] + r, j = 4 * R.bj[k] + c;
+                if (j >= w && i >= j && i < m) cb[(int64_t)(j - w) * mb + (i - w)] = R.v[k][r * 4 + c];
+            }
+    }
+}
+
+// Zero, A entries, children's CBs from HBM (children in child-list order; skip: a
+// child left out, the chain child of a chained front).
+__device__ __forceinline__ void small_assemble(const DevPlan& P, int s, int c0, int w, int m,
+                                               const double* __restrict__ Ax, double* F, int skip = -1) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tot = (m * (m + 1)) >> 1;
+    for (int idx = tid; idx < tot; idx += 256) F[idx] = 0.0;
+    lds_barrier();
+    for (int lc = wid; lc < w; lc += 4) {
+        const int64_t a0 = P.a_ptr[c0 + lc], a1 = P.a_ptr[c0 + lc + 1];
+        double* Fcol = F + pk_col(m, lc) - lc;
+        for (int64_t q = a0 + lane; q < a1; q += 64) Fcol[P.a_pos[q]] = Ax[P.a_src[q]];
+    }
+    lds_barrier();
+    for (int ci = P.child_ptr[s]; ci < P.child_ptr[s + 1]; ++ci) {
+        const int c = P.child_list[ci];
+        if (c == skip) continue;
+        const int mbc = P.sn_m[c] - (P.sn_start[c + 1] - P.sn_start[c]);
+        const int32_t* __restrict__ rel = P.relind + P.rel_ptr[c];
+        const double* __restrict__ cb = P.cb_pool + P.cb_off[c];
+        for (int jc = wid; jc < mbc; jc += 4) {
+            const int pj = rel[jc];
+            double* Fcol = F + pk_col(m, pj) - pj;
+            const double* __restrict__ src = cb + (int64_t)jc * mbc;
+            for (int ic = jc + lane; ic < mbc; ic += 64) Fcol[rel[ic]] += src[ic];
+        }
+        lds_barrier();
+    }
+}
+
+// Level launch: one workgroup per front; LDS = the packed front (maxm) + colbuf.
+template <int KT>
 __global__ __launch_bounds__(256) void front_small_kernel(DevPlan P, const int32_t* __restrict__ nodes,
                                                            const double* __restrict__ Ax) {
     extern __shared__ double F[];
-    __shared__ double colj[PNB];
-    small_front(P, nodes[blockIdx.x], Ax, F, colj);
+    __shared__ __attribute__((aligned(16))) double colbuf[2 * 4 * COLB];
+    const int s = nodes[blockIdx.x];
+    const int c0 = P.sn_start[s];
+    const int w = P.sn_start[s + 1] - c0;
+    const int m = P.sn_m[s];
+    SmallRegs<KT> R;
+    small_tiles<KT>(R, m, w);
+    small_assemble(P, s, c0, w, m, Ax, F);
+    small_load<KT>(R, F, m);
+    small_steps<KT>(R, colbuf, w, P.info, c0);
+    small_store_panel<KT>(R, P.panel_pool + P.panel_off[s], m, w);
+    if (m > w) small_store_cb<KT>(R, P.cb_pool + P.cb_off[s], m, w);
+}
+
+// Chain, part 1 (one workgroup per chained front, all in parallel): the packed image
+// of A entries and the children other than the chain child, to HBM.
+__global__ __launch_bounds__(256) void chain_init_kernel(DevPlan P, ChainPlan C, int first,
+                                                          const double* __restrict__ Ax) {
+    extern __shared__ double F[];
+    const ChainDesc d = C.desc[first + blockIdx.x];
+    small_assemble(P, d.s, d.c0, d.w, d.m, Ax, F, d.sp);
+    const int tot = (d.m * (d.m + 1)) >> 1;
+    double* out = C.init + d.init_off;
+    for (int idx = threadIdx.x; idx < tot; idx += 256) out[idx] = F[idx];
+}
+
+// Chain, part 2 (one workgroup of CHAIN_NT threads, one tile each): iteration i loads
+// front i's tiles from the LDS front buffer, writes front i + 1's image (held in
+// registers since iteration i - 1) into the buffer, issues the loads of front i + 2's
+// image and CB relind, factors front i, stores its panel, and adds its CB into the
+// buffer at the parent's positions (the last front's CB goes to HBM).
+constexpr int CHAIN_IMG = (128 * 129 / 2 + CHAIN_NT - 1) / CHAIN_NT;  // image doubles per thread
+__global__ __launch_bounds__(CHAIN_NT) void front_chain_kernel(DevPlan P, ChainPlan C, int first, int count) {
+    extern __shared__ double F[];
+    __shared__ __attribute__((aligned(16))) double colbuf[2 * 4 * COLB];
+    __shared__ ChainDesc ds[CHAIN_MAXF];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < count; i += CHAIN_NT) ds[i] = C.desc[first + i];
+    lds_barrier();
+    // the next front's prefetched image slice, tile and its CB relind (rows, cols;
+    // four 8-bit parent rows packed per word: relind < m <= 128)
+    double img[CHAIN_IMG];
+    int nbi, nbj;
+    uint32_t nrr, nrc;
+    auto prefetch = [&](int f) {
+        const ChainDesc& d = ds[f];
+        const int tot = (d.m * (d.m + 1)) >> 1;
+        const double* src = C.init + d.init_off;
+#pragma unroll
+        for (int q = 0; q < CHAIN_IMG; ++q) {
+            const int idx = tid + CHAIN_NT * q;
+            img[q] = idx < tot ? src[idx] : 0.0;
+        }
+        const int T = (d.m + 3) >> 2;
+        nbi = nbj = -1;
+        if (tid < T * (T + 1) / 2) tile_map(tid, T, (d.w + 3) >> 2, nbi, nbj);
+        const bool has_parent = f + 1 < count;
+        const int32_t* rel = P.relind + d.rel_off;
+        nrr = nrc = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int i4 = 4 * nbi + t, j4 = 4 * nbj + t;
+            const uint32_t a = (has_parent && nbi >= 0 && i4 >= d.w && i4 < d.m) ? (uint32_t)rel[i4 - d.w] : 0u;
+            const uint32_t b = (has_parent && nbi >= 0 && j4 >= d.w && j4 < d.m) ? (uint32_t)rel[j4 - d.w] : 0u;
+            nrr |= a << (8 * t);
+            nrc |= b << (8 * t);
+        }
+    };
+    auto put = [&](int f) {  // image slice -> the LDS buffer
+        const int tot = (ds[f].m * (ds[f].m + 1)) >> 1;
+#pragma unroll
+        for (int q = 0; q < CHAIN_IMG; ++q) {
+            const int idx = tid + CHAIN_NT * q;
+            if (idx < tot) F[idx] = img[q];
+        }
+    };
+    int cbi, cbj;
+    uint32_t crr, crc;
+    auto take = [&]() {
+        cbi = nbi;
+        cbj = nbj;
+        crr = nrr;
+        crc = nrc;
+    };
+    prefetch(0);
+    put(0);
+    take();
+    if (count > 1) prefetch(1);
+    lds_barrier();
+    for (int i = 0; i < count; ++i) {
+        uint64_t* stamp = C.stamps ? C.stamps + 8 * (first + i) : nullptr;
+        if (stamp && tid == 0) stamp[0] = __builtin_amdgcn_s_memtime();
+        const ChainDesc d = ds[i];
+        const int m = d.m, w = d.w;
+        SmallRegs<1> R;
+        R.bi[0] = cbi;
+        R.bj[0] = cbj;
+        const uint32_t rr = crr, rc = crc;
+        small_load<1>(R, F, m);
+        lds_barrier();  // every thread has its tile: the buffer is free
+        if (stamp && tid == 0) stamp[1] = __builtin_amdgcn_s_memtime();
+        const bool has_parent = i + 1 < count;
+        if (has_parent) {
+            put(i + 1);  // ordered before the CB adds below by the steps' barriers
+            take();
+            if (i + 2 < count) prefetch(i + 2);
+        }
+        if (stamp && tid == 0) stamp[2] = __builtin_amdgcn_s_memtime();
+        small_steps<1>(R, colbuf, w, P.info, d.c0);
+        if (w == 0) lds_barrier();
+        if (stamp && tid == 0) stamp[3] = __builtin_amdgcn_s_memtime();
+        small_store_panel<1>(R, P.panel_pool + d.panel_off, m, w);
+        if (m > w && R.bi[0] >= 0 && 4 * R.bi[0] + 3 >= w) {
+            if (!has_parent) {
+                small_store_cb<1>(R, P.cb_pool + d.cb_off, m, w);
+            } else {  // CB entries into the parent's front (relind injective: no collisions)
+                const int mp = ds[i + 1].m;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const int ii = 4 * R.bi[0] + r, jj = 4 * R.bj[0] + c;
+                        const int pr = (rr >> (8 * r)) & 255, pc = (rc >> (8 * c)) & 255;
+                        if (jj >= w && ii >= jj && ii < m) F[pk_col(mp, pc) + pr - pc] += R.v[0][r * 4 + c];
+                    }
+            }
+        }
+        lds_barrier();
+        if (stamp && tid == 0) stamp[4] = __builtin_amdgcn_s_memtime();
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -360,15 +617,6 @@ __device__ __forceinline__ void buf_st(double v, __amdgpu_buffer_rsrc_t rs, int 
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0)), v), rs, voff, soff, 0);
 }
 
-// 1/sqrt(d): v_rsq_f64 seed plus two Newton steps (~1 ulp; NaN/inf for d <= 0,
-// which the callers flag separately).
-__device__ __forceinline__ double rsqrt_f64(double d) {
-    double y = __builtin_amdgcn_rsq(d);
-    const double h = 0.5 * d;
-    y = y * fma(-h * y, y, 1.5);
-    y = y * fma(-h * y, y, 1.5);
-    return y;
-}
 
 #include "panel_gen.inc"
 
@@ -599,11 +847,35 @@ __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask*
 // ---------------------------------------------------------------------------
 // Launch wrappers
 // ---------------------------------------------------------------------------
-hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count, int maxm, const double* Ax,
-                              hipStream_t st) {
+// KT: 4 x 4 register tiles per thread for fronts up to maxm (ceil(tiles / 256))
+static int small_kt(int maxm) {
+    const int T = (maxm + 3) / 4;
+    return (T * (T + 1) / 2 + 255) / 256;
+}
+
+hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count, int maxm, int wb, int chain,
+                              const double* Ax, hipStream_t st) {
     if (count <= 0) return hipSuccess;
+    (void)wb;
+    (void)chain;
     const size_t lds = (size_t)maxm * (maxm + 1) / 2 * sizeof(double);
-    hipLaunchKernelGGL(front_small_kernel, dim3(count), dim3(256), lds, st, P, nodes, Ax);
+    const int kt = small_kt(maxm);
+    if (kt <= 1)
+        hipLaunchKernelGGL(front_small_kernel<1>, dim3(count), dim3(256), lds, st, P, nodes, Ax);
+    else if (kt == 2)
+        hipLaunchKernelGGL(front_small_kernel<2>, dim3(count), dim3(256), lds, st, P, nodes, Ax);
+    else
+        hipLaunchKernelGGL(front_small_kernel<3>, dim3(count), dim3(256), lds, st, P, nodes, Ax);
+    return hipGetLastError();
+}
+
+hipError_t launch_front_chain(const DevPlan& P, const ChainPlan& C, int first, int count, int maxm,
+                              const double* Ax, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    if (count > CHAIN_MAXF || maxm > 128) return hipErrorInvalidValue;  // the host splits longer chains
+    const size_t lds = (size_t)maxm * (maxm + 1) / 2 * sizeof(double);
+    hipLaunchKernelGGL(chain_init_kernel, dim3(count), dim3(256), lds, st, P, C, first, Ax);
+    hipLaunchKernelGGL(front_chain_kernel, dim3(1), dim3(CHAIN_NT), lds, st, P, C, first, count);
     return hipGetLastError();
 }
 

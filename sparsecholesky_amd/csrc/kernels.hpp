@@ -91,8 +91,34 @@ hipError_t launch_solve_fwd(const SolvePlan& P, const int4* tasks, int count, hi
 hipError_t launch_permute(double* dst, const double* src, const int32_t* perm, int64_t n, bool scatter,
                           hipStream_t st);
 
-hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count, int maxm, const double* Ax,
-                              hipStream_t st);
+// Small fronts (m <= maxm <= 128): one workgroup per front, factored in registers
+// (4 x 4 tiles per thread; wb and chain unused).
+hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count, int maxm, int wb, int chain,
+                              const double* Ax, hipStream_t st);
+
+// Chain launches (a run of >= 2 single-front levels; each front the parent of the one
+// before).  chain_init_kernel assembles every chained front's A entries and its
+// children other than the chain child (all computed by earlier launches) into a
+// packed image in HBM, all fronts in parallel; front_chain_kernel (one workgroup)
+// then runs the chain, front i + 1's image streaming into registers while front i
+// is factored and front i's CB added into front i + 1 straight from registers.
+struct ChainDesc {
+    int32_t s, c0, w, m;
+    int32_t sp;      // the chain child (previous chained front), -1 for the first
+    int32_t pad;
+    int64_t panel_off, cb_off;
+    int64_t init_off;  // doubles into ChainPlan::init (packed image, m (m + 1) / 2)
+    int64_t rel_off;   // S.rel_ptr[s]: relind of s's CB rows in its parent
+};
+struct ChainPlan {
+    const ChainDesc* desc;
+    double* init;
+    uint64_t* stamps;  // debug: per front 5 shader-clock stamps (thread 0; stride 8), or null
+};
+constexpr int CHAIN_NT = 768;        // threads of the chain workgroup (>= 528 tiles of m = 128; 3 waves per SIMD)
+constexpr int CHAIN_MAXF = 256;      // chained fronts whose descriptors are staged in LDS
+hipError_t launch_front_chain(const DevPlan& P, const ChainPlan& C, int first, int count, int maxm,
+                              const double* Ax, hipStream_t st);
 // tiled: tasks are (front, (row tile << 16) | 16-column block) for the write-once
 // tile kernel (fronts with m >= ASM_TILE_MIN_M), else (front, column block)
 hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count, const double* Ax,

@@ -73,6 +73,14 @@ static int bucket_of(int m) {
     return 128;
 }
 
+// register width of the small-front POTRF / TRSM (w > 64: right-looking path)
+static int wbucket_of(int w) {
+    if (w <= 16) return 16;
+    if (w <= 32) return 32;
+    if (w <= 64) return 64;
+    return 128;
+}
+
 // Build the static launch schedule (host).  Task pointers into the pools are
 // final device addresses, so the schedule can be replayed or graph-captured.
 void append_tiles(std::vector<int2>& out, int task, int M, int N, int bt, int G) {
@@ -136,6 +144,8 @@ struct CommBuild {
 };
 
 struct SchedBuild {
+    std::vector<ChainDesc> cdesc;
+    int64_t chain_init = 0;  // doubles of the chained fronts' packed images
     std::vector<int32_t> small;
     std::vector<int2> asmv, potrf;
     std::vector<int4> trsm;
@@ -393,8 +403,12 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
             L.vr = v;
             L.off = (int64_t)small.size();
             L.maxm = b;
+            L.bt = 16;
             for (int32_t s : nodes)
-                if (S.fclass[s] == FRONT_SMALL && (nsmall <= 256 || bucket_of(S.sn_m[s]) == b)) small.push_back(s);
+                if (S.fclass[s] == FRONT_SMALL && (nsmall <= 256 || bucket_of(S.sn_m[s]) == b)) {
+                    small.push_back(s);
+                    L.bt = std::max(L.bt, wbucket_of(S.w(s)));
+                }
             L.count = (int32_t)((int64_t)small.size() - L.off);
             if (L.count > 0) N.sched.push_back(L);
         }
@@ -733,7 +747,43 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
     // L + 2 only after the comm steps of level L, so a region a step of level L touches
     // is never reused before level L + 2
     std::vector<int> comm_done((size_t)S.nlevels, -1);
+    // single device: a run of >= 2 levels holding one small front each (a chain: each
+    // front the parent of the one before) runs as one single-workgroup launch
+    auto chain_front = [&](int32_t lev) {
+        return !multi && by_level[lev].size() == 1 && S.fclass[by_level[lev][0]] == FRONT_SMALL;
+    };
     for (int32_t lev = 0; lev < S.nlevels; ++lev) {
+        if (chain_front(lev) && lev + 1 < S.nlevels && chain_front(lev + 1)) {
+            Launch L {};
+            L.kind = L_SMALL;
+            L.level = lev;
+            L.off = (int64_t)B.cdesc.size();
+            L.maxm = 32;
+            L.big = 1;  // chain
+            int32_t sp = -1;
+            for (; lev < S.nlevels && chain_front(lev) && (int64_t)B.cdesc.size() - L.off < CHAIN_MAXF; ++lev) {
+                const int32_t s = by_level[lev][0];
+                const int w = S.w(s), m = S.sn_m[s];
+                L.maxm = std::max(L.maxm, bucket_of(m));
+                ChainDesc d {};
+                d.s = s;
+                d.c0 = S.sn_start[s];
+                d.w = w;
+                d.m = m;
+                d.sp = sp;
+                d.panel_off = N.R[0].panel_off[s];
+                d.cb_off = N.R[0].cb_off[s] < 0 ? 0 : N.R[0].cb_off[s];
+                d.init_off = B.chain_init;
+                d.rel_off = S.rel_ptr[s];
+                B.chain_init += ((int64_t)m * (m + 1) / 2 + 63) / 64 * 64;
+                B.cdesc.push_back(d);
+                sp = s;
+            }
+            L.count = (int32_t)((int64_t)B.cdesc.size() - L.off);
+            N.sched.push_back(L);
+            --lev;
+            continue;
+        }
         if (multi) {
             if (lev >= 2 && comm_done[lev - 2] >= 0) push_wait(0, comm_done[lev - 2]);
             push_wait(2, push_record(0));
@@ -966,6 +1016,14 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
             N.err = "hipEventCreate failed";
             return fail(SC_ERR_HIP);
         }
+    {
+        ChainDesc* dd = nullptr;
+        if ((rc = upload(N, B.cdesc, dd))) return fail(rc);
+        N.CP.desc = dd;
+        N.n_chain = (int64_t)B.cdesc.size();
+        if ((rc = dalloc(N, (size_t)std::max<int64_t>(B.chain_init, 1) * sizeof(double), p))) return fail(rc);
+        N.CP.init = (double*)p;
+    }
     if ((rc = upload(N, B.small, N.d_small)) || (rc = upload(N, B.asmv, N.d_asm)) ||
         (rc = upload(N, B.potrf, N.d_potrf)) || (rc = upload(N, B.trsm, N.d_trsm)) ||
         (rc = upload(N, B.gemm, N.d_gemm)) || (rc = upload(N, B.tiles, N.d_tiles)))
@@ -990,7 +1048,8 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
         case L_WAIT:
             return hipStreamWaitEvent(st, N.sync_ev[L.count], 0);
         case L_SMALL:
-            return launch_front_small(N.R[L.vr].P, N.d_small + L.off, L.count, L.maxm, d_Ax, N.stream);
+            if (L.big) return launch_front_chain(N.R[L.vr].P, N.CP, (int)L.off, L.count, L.maxm, d_Ax, N.stream);
+            return launch_front_small(N.R[L.vr].P, N.d_small + L.off, L.count, L.maxm, L.bt, 0, d_Ax, N.stream);
         case L_ASM:
             return launch_assemble_large(N.R[L.vr].P, N.d_asm + L.off, L.count, d_Ax, N.stream, L.big != 0);
         case L_POTRF:
@@ -1457,6 +1516,23 @@ void numeric_free(Numeric* Np) {
     if (N.stream2) (void)hipStreamDestroy(N.stream2);
     if (N.stream3) (void)hipStreamDestroy(N.stream3);
     delete Np;
+}
+
+int64_t numeric_chain_stamps(Numeric& N, int enable, uint64_t* out, int64_t cap) {
+    const int64_t cnt = 8 * N.n_chain;
+    if (enable) {
+        if (!N.CP.stamps && cnt > 0) {
+            void* p = nullptr;
+            TRY(dalloc(N, (size_t)cnt * sizeof(uint64_t), p));
+            N.CP.stamps = (uint64_t*)p;
+        }
+        return cnt;
+    }
+    if (!N.CP.stamps) return 0;
+    HIP_TRY(hipStreamSynchronize(N.stream));
+    if (out && cap > 0)
+        HIP_TRY(hipMemcpy(out, N.CP.stamps, (size_t)std::min(cap, cnt) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return cnt;
 }
 
 int64_t debug_syrk(double* dC, int ldc, const double* dA, int lda, int M, int Nn, int K) {

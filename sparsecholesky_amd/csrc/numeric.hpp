@@ -175,6 +175,8 @@ struct Numeric {
     int64_t dev_bytes = 0;           // device memory held (pools, plan, staging)
     std::vector<Launch> sched;
     int32_t* d_small = nullptr;
+    ChainPlan CP {};                 // chain launches (runs of single small-front levels)
+    int64_t n_chain = 0;             // chained fronts (descriptors)
     int2* d_asm = nullptr;
     int2* d_potrf = nullptr;
     int4* d_trsm = nullptr;
@@ -279,6 +281,7 @@ void numeric_free(Numeric* N);
 int64_t numeric_solve_device(Numeric& N, const double* d_b, double* d_x);
 int64_t numeric_solve_host(Numeric& N, const double* b, double* x);
 int64_t debug_syrk(double* dC, int ldc, const double* dA, int lda, int M, int N, int K);
+int64_t numeric_chain_stamps(Numeric& N, int enable, uint64_t* out, int64_t cap);
 int64_t debug_bench(int which, int M, int K, int reps, int arg, double* tflops);
 
 }  // namespace sc
