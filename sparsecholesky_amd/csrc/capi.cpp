@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <new>
 #include <string>
@@ -211,6 +212,23 @@ int64_t sc_factor_device(sc_numeric* num, const double* d_Ax, int32_t sync) {
     int64_t rc = sc::numeric_factor(*num->N, d_Ax, sync != 0);
     if (rc < 0) g_last_error = num->N->err;
     return rc;
+}
+
+int64_t sc_debug_time_factor(sc_numeric* num, const double* d_Ax, int32_t reps, double* best_ms) {
+    if (!num || !num->N || reps < 1 || !best_ms) return SC_ERR_ARG;
+    double best = 1e30;
+    for (int r = 0; r <= reps; ++r) {  // the first call captures / warms up
+        const auto t0 = std::chrono::steady_clock::now();
+        const int64_t rc = sc::numeric_factor(*num->N, d_Ax, true);
+        const auto t1 = std::chrono::steady_clock::now();
+        if (rc < 0) {
+            g_last_error = num->N->err;
+            return rc;
+        }
+        if (r > 0) best = std::min(best, std::chrono::duration<double, std::milli>(t1 - t0).count());
+    }
+    *best_ms = best;
+    return SC_OK;
 }
 
 int64_t sc_factor(sc_numeric* num, const double* Ax) {

@@ -461,22 +461,83 @@ __device__ __forceinline__ void small_assemble(const DevPlan& P, int s, int c0, 
 }
 
 // Level launch: one workgroup per front; LDS = the packed front (maxm) + colbuf.
+// seq > 0: one workgroup runs nodes[0 .. seq) in order (a whole small tree in
+// postorder): each front's children were stored by earlier iterations, and the
+// workgroup barrier between fronts makes those CB stores visible (one CU, one L1).
 template <int KT>
 __global__ __launch_bounds__(256) void front_small_kernel(DevPlan P, const int32_t* __restrict__ nodes,
-                                                           const double* __restrict__ Ax) {
+                                                           const double* __restrict__ Ax, int seq) {
     extern __shared__ double F[];
     __shared__ __attribute__((aligned(16))) double colbuf[2 * 4 * COLB];
-    const int s = nodes[blockIdx.x];
-    const int c0 = P.sn_start[s];
-    const int w = P.sn_start[s + 1] - c0;
-    const int m = P.sn_m[s];
-    SmallRegs<KT> R;
-    small_tiles<KT>(R, m, w);
-    small_assemble(P, s, c0, w, m, Ax, F);
-    small_load<KT>(R, F, m);
-    small_steps<KT>(R, colbuf, w, P.info, c0);
-    small_store_panel<KT>(R, P.panel_pool + P.panel_off[s], m, w);
-    if (m > w) small_store_cb<KT>(R, P.cb_pool + P.cb_off[s], m, w);
+    const int n = seq > 0 ? seq : 1;
+    for (int f = 0; f < n; ++f) {
+        const int s = nodes[seq > 0 ? f : blockIdx.x];
+        const int c0 = P.sn_start[s];
+        const int w = P.sn_start[s + 1] - c0;
+        const int m = P.sn_m[s];
+        SmallRegs<KT> R;
+        small_tiles<KT>(R, m, w);
+        small_assemble(P, s, c0, w, m, Ax, F);
+        small_load<KT>(R, F, m);
+        small_steps<KT>(R, colbuf, w, P.info, c0);
+        small_store_panel<KT>(R, P.panel_pool + P.panel_off[s], m, w);
+        if (m > w) small_store_cb<KT>(R, P.cb_pool + P.cb_off[s], m, w);
+        if (seq > 0) __syncthreads();  // global CB stores visible to the next front's loads
+    }
+}
+
+// Tiny tree: one workgroup, every image and CB in LDS (see TinyPlan).  The A stores
+// of all fronts go in parallel first; then per front (postorder): its children's
+// CB entries (one phase per child), the register factorization, the panel to HBM and
+// the CB (packed lower, column j - w at pk_col(mb, j - w)) to LDS.
+__global__ __launch_bounds__(256) void tiny_tree_kernel(DevPlan P, TinyPlan T, const double* __restrict__ Ax) {
+    extern __shared__ double Lm[];
+    __shared__ __attribute__((aligned(16))) double colbuf[2 * 4 * COLB];
+    __shared__ TinyFront fr[TINY_MAX_FRONTS];
+    const int tid = threadIdx.x;
+    if (tid < T.nf) fr[tid] = T.fr[tid];
+    for (int i = tid; i < T.lds; i += 256) Lm[i] = 0.0;
+    lds_barrier();
+    for (int e = tid; e < T.na; e += 256) {
+        const int2 a = T.a[e];
+        Lm[a.y] = Ax[a.x];
+    }
+    lds_barrier();
+    for (int f = 0; f < T.nf; ++f) {
+        const TinyFront d = fr[f];
+        for (int p = 0; p < d.np; ++p) {
+            const int2 q = T.ph[d.e0 + p];
+            for (int e = q.x + tid; e < q.y; e += 256) {
+                const int2 pr = T.pr[e];
+                Lm[pr.y] += Lm[pr.x];
+            }
+            lds_barrier();
+        }
+        SmallRegs<1> R;
+        small_tiles<1>(R, d.m, d.w);
+        small_load<1>(R, Lm + d.img, d.m);
+        small_steps<1>(R, colbuf, d.w, P.info, d.c0);
+        small_store_panel<1>(R, P.panel_pool + d.panel_off, d.m, d.w);
+        if (d.m > d.w && R.bi[0] >= 0) {
+            const int mb = d.m - d.w;
+            double* cb = Lm + d.cb;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int i = 4 * R.bi[0] + r - d.w, j = 4 * R.bj[0] + c - d.w;
+                    if (j >= 0 && i >= j && i < mb) cb[pk_col(mb, j) + i - j] = R.v[0][r * 4 + c];
+                }
+        }
+        lds_barrier();
+    }
+}
+
+hipError_t launch_tiny_tree(const DevPlan& P, const TinyPlan& T, int maxm, const double* Ax, hipStream_t st) {
+    if (T.nf <= 0) return hipSuccess;
+    if (T.nf > TINY_MAX_FRONTS || T.lds > TINY_MAX_LDS || maxm > 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(tiny_tree_kernel, dim3(1), dim3(256), (size_t)T.lds * sizeof(double), st, P, T, Ax);
+    return hipGetLastError();
 }
 
 // Chain, part 1 (one workgroup per chained front, all in parallel): the packed image
@@ -521,17 +582,10 @@ __global__ __launch_bounds__(CHAIN_NT) void front_chain_kernel(DevPlan P, ChainP
         const int T = (d.m + 3) >> 2;
         nbi = nbj = -1;
         if (tid < T * (T + 1) / 2) tile_map(tid, T, (d.w + 3) >> 2, nbi, nbj);
-        const bool has_parent = f + 1 < count;
-        const int32_t* rel = P.relind + d.rel_off;
-        nrr = nrc = 0;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int i4 = 4 * nbi + t, j4 = 4 * nbj + t;
-            const uint32_t a = (has_parent && nbi >= 0 && i4 >= d.w && i4 < d.m) ? (uint32_t)rel[i4 - d.w] : 0u;
-            const uint32_t b = (has_parent && nbi >= 0 && j4 >= d.w && j4 < d.m) ? (uint32_t)rel[j4 - d.w] : 0u;
-            nrr |= a << (8 * t);
-            nrc |= b << (8 * t);
-        }
+        // parent rows of the tile's CB rows / columns: one packed word per tile row
+        // (host-built, 0 where the chain ends or rows are pivots)
+        nrr = nbi >= 0 ? C.relp[d.relp_off + nbi] : 0u;
+        nrc = nbi >= 0 ? C.relp[d.relp_off + nbj] : 0u;
     };
     auto put = [&](int f) {  // image slice -> the LDS buffer
         const int tot = (ds[f].m * (ds[f].m + 1)) >> 1;
@@ -853,19 +907,19 @@ static int small_kt(int maxm) {
     return (T * (T + 1) / 2 + 255) / 256;
 }
 
-hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count, int maxm, int wb, int chain,
+hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count, int maxm, bool seq,
                               const double* Ax, hipStream_t st) {
     if (count <= 0) return hipSuccess;
-    (void)wb;
-    (void)chain;
     const size_t lds = (size_t)maxm * (maxm + 1) / 2 * sizeof(double);
     const int kt = small_kt(maxm);
+    const dim3 grid(seq ? 1 : count);
+    const int sq = seq ? count : 0;
     if (kt <= 1)
-        hipLaunchKernelGGL(front_small_kernel<1>, dim3(count), dim3(256), lds, st, P, nodes, Ax);
+        hipLaunchKernelGGL(front_small_kernel<1>, grid, dim3(256), lds, st, P, nodes, Ax, sq);
     else if (kt == 2)
-        hipLaunchKernelGGL(front_small_kernel<2>, dim3(count), dim3(256), lds, st, P, nodes, Ax);
+        hipLaunchKernelGGL(front_small_kernel<2>, grid, dim3(256), lds, st, P, nodes, Ax, sq);
     else
-        hipLaunchKernelGGL(front_small_kernel<3>, dim3(count), dim3(256), lds, st, P, nodes, Ax);
+        hipLaunchKernelGGL(front_small_kernel<3>, grid, dim3(256), lds, st, P, nodes, Ax, sq);
     return hipGetLastError();
 }
 

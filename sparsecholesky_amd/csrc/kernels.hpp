@@ -92,8 +92,9 @@ hipError_t launch_permute(double* dst, const double* src, const int32_t* perm, i
                           hipStream_t st);
 
 // Small fronts (m <= maxm <= 128): one workgroup per front, factored in registers
-// (4 x 4 tiles per thread; wb and chain unused).
-hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count, int maxm, int wb, int chain,
+// (4 x 4 tiles per thread); seq: one workgroup runs the fronts in order (a whole
+// small tree in postorder, CBs through HBM).
+hipError_t launch_front_small(const DevPlan& P, const int32_t* nodes, int count, int maxm, bool seq,
                               const double* Ax, hipStream_t st);
 
 // Chain launches (a run of >= 2 single-front levels; each front the parent of the one
@@ -108,15 +109,38 @@ struct ChainDesc {
     int32_t pad;
     int64_t panel_off, cb_off;
     int64_t init_off;  // doubles into ChainPlan::init (packed image, m (m + 1) / 2)
-    int64_t rel_off;   // S.rel_ptr[s]: relind of s's CB rows in its parent
+    int64_t relp_off;  // words into ChainPlan::relp: per tile row, the parent rows of its 4 rows
 };
 struct ChainPlan {
     const ChainDesc* desc;
     double* init;
+    const uint32_t* relp;  // four 8-bit parent rows per word (relind < parent m <= 128)
     uint64_t* stamps;  // debug: per front 5 shader-clock stamps (thread 0; stride 8), or null
 };
 constexpr int CHAIN_NT = 768;        // threads of the chain workgroup (>= 528 tiles of m = 128; 3 waves per SIMD)
 constexpr int CHAIN_MAXF = 256;      // chained fronts whose descriptors are staged in LDS
+// Tiny trees (every front small, few of them, everything fits LDS): one workgroup
+// runs the whole factorization with every front image and contribution block in
+// LDS.  Host-built lists: the A stores (Ax index -> LDS), and per front and child the
+// extend-add pairs (LDS CB entry -> LDS image entry), child by child.
+struct TinyFront {
+    int32_t s, c0, w, m;
+    int32_t img, cb;  // LDS offsets (doubles) of the image (packed m x m lower) and the CB (packed)
+    int32_t e0, np;   // the front's extend-add phases: ph[e0 .. e0 + np)
+    int64_t panel_off;
+};
+struct TinyPlan {
+    const TinyFront* fr;
+    const int2* a;    // (Ax index, LDS image index)
+    const int2* ph;   // (first pair, end pair) per phase
+    const int2* pr;   // (LDS CB index, LDS image index)
+    int32_t nf, na, nph, npr;
+    int32_t lds;      // doubles of images + CBs
+};
+constexpr int TINY_MAX_FRONTS = 16;
+constexpr int TINY_MAX_LDS = 12288;  // doubles of images + CBs (96 KB)
+hipError_t launch_tiny_tree(const DevPlan& P, const TinyPlan& T, int maxm, const double* Ax, hipStream_t st);
+
 hipError_t launch_front_chain(const DevPlan& P, const ChainPlan& C, int first, int count, int maxm,
                               const double* Ax, hipStream_t st);
 // tiled: tasks are (front, (row tile << 16) | 16-column block) for the write-once

@@ -145,7 +145,11 @@ struct CommBuild {
 
 struct SchedBuild {
     std::vector<ChainDesc> cdesc;
+    std::vector<uint32_t> crelp;
     int64_t chain_init = 0;  // doubles of the chained fronts' packed images
+    std::vector<TinyFront> tfr;  // tiny-tree plan
+    std::vector<int2> ta, tph, tpr;
+    int32_t tiny_lds = 0;
     std::vector<int32_t> small;
     std::vector<int2> asmv, potrf;
     std::vector<int4> trsm;
@@ -752,7 +756,67 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
     auto chain_front = [&](int32_t lev) {
         return !multi && by_level[lev].size() == 1 && S.fclass[by_level[lev][0]] == FRONT_SMALL;
     };
-    for (int32_t lev = 0; lev < S.nlevels; ++lev) {
+    // single device, a tiny tree (at most TINY_MAX_FRONTS fronts, all small with m <= 64,
+    // every image and CB fitting LDS): the whole factorization as one single-workgroup
+    // launch, postorder (the internal numbering), everything in LDS
+    bool tiny = !multi && S.ns > 1 && S.ns <= TINY_MAX_FRONTS;
+    {
+        int64_t lds = 0;
+        for (int32_t s = 0; tiny && s < S.ns; ++s) {
+            const int64_t m = S.sn_m[s], mb = S.mb(s);
+            tiny = S.fclass[s] == FRONT_SMALL && m <= 64;
+            lds += m * (m + 1) / 2 + mb * (mb + 1) / 2;
+        }
+        tiny = tiny && lds <= TINY_MAX_LDS;
+    }
+    if (tiny) {
+        auto pk = [](int64_t m, int64_t j) { return j * m - j * (j - 1) / 2; };
+        std::vector<int32_t> img((size_t)S.ns), cbo((size_t)S.ns);
+        int32_t off = 0;
+        for (int32_t s = 0; s < S.ns; ++s) {
+            img[s] = off;
+            off += S.sn_m[s] * (S.sn_m[s] + 1) / 2;
+            cbo[s] = off;
+            off += S.mb(s) * (S.mb(s) + 1) / 2;
+        }
+        B.tiny_lds = off;
+        for (int32_t s = 0; s < S.ns; ++s) {
+            const int m = S.sn_m[s], w = S.w(s), c0 = S.sn_start[s];
+            TinyFront f {};
+            f.s = s;
+            f.c0 = c0;
+            f.w = w;
+            f.m = m;
+            f.img = img[s];
+            f.cb = cbo[s];
+            f.e0 = (int32_t)B.tph.size();
+            f.panel_off = N.R[0].panel_off[s];
+            for (int lc = 0; lc < w; ++lc)
+                for (int64_t q = S.a_ptr[c0 + lc]; q < S.a_ptr[c0 + lc + 1]; ++q)
+                    B.ta.push_back(make_int2((int32_t)S.a_src[q], img[s] + (int32_t)(pk(m, lc) + S.a_pos[q] - lc)));
+            for (int32_t ci = S.child_ptr[s]; ci < S.child_ptr[s + 1]; ++ci) {
+                const int32_t c = S.child_list[ci];
+                const int mbc = S.mb(c);
+                const int32_t* rel = S.relind.data() + S.rel_ptr[c];
+                const int32_t beg = (int32_t)B.tpr.size();
+                for (int jc = 0; jc < mbc; ++jc)
+                    for (int ic = jc; ic < mbc; ++ic)
+                        B.tpr.push_back(make_int2(cbo[c] + (int32_t)(pk(mbc, jc) + ic - jc),
+                                                  img[s] + (int32_t)(pk(m, rel[jc]) + rel[ic] - rel[jc])));
+                B.tph.push_back(make_int2(beg, (int32_t)B.tpr.size()));
+            }
+            f.np = (int32_t)B.tph.size() - f.e0;
+            B.tfr.push_back(f);
+        }
+        Launch L {};
+        L.kind = L_SMALL;
+        L.level = 0;
+        L.maxm = 64;
+        L.big = 2;  // tiny tree
+        L.count = 1;
+        N.sched.push_back(L);
+    }
+    for (int32_t lev = tiny ? S.nlevels : 0; lev < S.nlevels; ++lev) {
         if (chain_front(lev) && lev + 1 < S.nlevels && chain_front(lev + 1)) {
             Launch L {};
             L.kind = L_SMALL;
@@ -774,7 +838,16 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 d.panel_off = N.R[0].panel_off[s];
                 d.cb_off = N.R[0].cb_off[s] < 0 ? 0 : N.R[0].cb_off[s];
                 d.init_off = B.chain_init;
-                d.rel_off = S.rel_ptr[s];
+                d.relp_off = (int64_t)B.crelp.size();
+                for (int t0 = 0; t0 < m; t0 += 4) {  // parent rows of CB rows, packed per tile row
+                    uint32_t wd = 0;
+                    for (int t = 0; t < 4; ++t) {
+                        const int i = t0 + t;
+                        const int32_t pr = (i >= w && i < m) ? S.relind[(size_t)S.rel_ptr[s] + (i - w)] : 0;
+                        wd |= (uint32_t)(pr & 255) << (8 * t);
+                    }
+                    B.crelp.push_back(wd);
+                }
                 B.chain_init += ((int64_t)m * (m + 1) / 2 + 63) / 64 * 64;
                 B.cdesc.push_back(d);
                 sp = s;
@@ -1018,11 +1091,27 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
         }
     {
         ChainDesc* dd = nullptr;
-        if ((rc = upload(N, B.cdesc, dd))) return fail(rc);
+        uint32_t* dr = nullptr;
+        if ((rc = upload(N, B.cdesc, dd)) || (rc = upload(N, B.crelp, dr))) return fail(rc);
         N.CP.desc = dd;
+        N.CP.relp = dr;
         N.n_chain = (int64_t)B.cdesc.size();
         if ((rc = dalloc(N, (size_t)std::max<int64_t>(B.chain_init, 1) * sizeof(double), p))) return fail(rc);
         N.CP.init = (double*)p;
+        TinyFront* tf = nullptr;
+        int2 *t1 = nullptr, *t2 = nullptr, *t3 = nullptr;
+        if ((rc = upload(N, B.tfr, tf)) || (rc = upload(N, B.ta, t1)) || (rc = upload(N, B.tph, t2)) ||
+            (rc = upload(N, B.tpr, t3)))
+            return fail(rc);
+        N.TP.fr = tf;
+        N.TP.a = t1;
+        N.TP.ph = t2;
+        N.TP.pr = t3;
+        N.TP.nf = (int32_t)B.tfr.size();
+        N.TP.na = (int32_t)B.ta.size();
+        N.TP.nph = (int32_t)B.tph.size();
+        N.TP.npr = (int32_t)B.tpr.size();
+        N.TP.lds = B.tiny_lds;
     }
     if ((rc = upload(N, B.small, N.d_small)) || (rc = upload(N, B.asmv, N.d_asm)) ||
         (rc = upload(N, B.potrf, N.d_potrf)) || (rc = upload(N, B.trsm, N.d_trsm)) ||
@@ -1048,8 +1137,9 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
         case L_WAIT:
             return hipStreamWaitEvent(st, N.sync_ev[L.count], 0);
         case L_SMALL:
-            if (L.big) return launch_front_chain(N.R[L.vr].P, N.CP, (int)L.off, L.count, L.maxm, d_Ax, N.stream);
-            return launch_front_small(N.R[L.vr].P, N.d_small + L.off, L.count, L.maxm, L.bt, 0, d_Ax, N.stream);
+            if (L.big == 1) return launch_front_chain(N.R[L.vr].P, N.CP, (int)L.off, L.count, L.maxm, d_Ax, N.stream);
+            if (L.big == 2) return launch_tiny_tree(N.R[L.vr].P, N.TP, L.maxm, d_Ax, N.stream);
+            return launch_front_small(N.R[L.vr].P, N.d_small + L.off, L.count, L.maxm, false, d_Ax, N.stream);
         case L_ASM:
             return launch_assemble_large(N.R[L.vr].P, N.d_asm + L.off, L.count, d_Ax, N.stream, L.big != 0);
         case L_POTRF:

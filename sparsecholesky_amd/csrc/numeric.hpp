@@ -176,6 +176,7 @@ struct Numeric {
     std::vector<Launch> sched;
     int32_t* d_small = nullptr;
     ChainPlan CP {};                 // chain launches (runs of single small-front levels)
+    TinyPlan TP {};                  // tiny trees: the whole factorization in one workgroup
     int64_t n_chain = 0;             // chained fronts (descriptors)
     int2* d_asm = nullptr;
     int2* d_potrf = nullptr;
