@@ -304,6 +304,8 @@ int64_t sc_debug_syrk(double* dC, int32_t ldc, const double* dA, int32_t lda, in
 /* Best wall time (ms) of reps synchronous factorizations from device values
  * (sc_factor_device(num, d_Ax, 1): launch, run, status read-back), timed in C. */
 int64_t sc_debug_time_factor(sc_numeric* num, const double* d_Ax, int32_t reps, double* best_ms);
+/* Debug: eager = 1 launches the solve sweeps directly instead of replaying their graph. */
+int64_t sc_debug_solve_eager(sc_numeric* num, int32_t eager);
 /* Chain launches (runs of single small-front levels): enable = 1 makes the next
  * eager factorizations record 8 shader-clock stamps per chained front (phase
  * boundaries); enable = 0 copies up to cap of them to out.  Returns the count. */

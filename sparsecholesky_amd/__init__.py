@@ -147,6 +147,7 @@ _SIGS = [
     ("sc_device_count", _I64, []),
     ("sc_debug_chain_stamps", _I64, [_P, _I32, _P, _I64]),
     ("sc_debug_time_factor", _I64, [_P, C.c_void_p, _I32, C.POINTER(_D)]),
+    ("sc_debug_solve_eager", _I64, [_P, _I32]),
 ]
 
 _lib: Optional[C.CDLL] = None

@@ -231,6 +231,12 @@ int64_t sc_debug_time_factor(sc_numeric* num, const double* d_Ax, int32_t reps, 
     return SC_OK;
 }
 
+int64_t sc_debug_solve_eager(sc_numeric* num, int32_t eager) {
+    if (!num || !num->N) return SC_ERR_ARG;
+    num->N->solve_eager = eager != 0;
+    return SC_OK;
+}
+
 int64_t sc_factor(sc_numeric* num, const double* Ax) {
     if (!num || !num->N) return SC_ERR_ARG;
     sc::Numeric& N = *num->N;

@@ -707,7 +707,7 @@ __device__ __forceinline__ void trsm_partial(double* pan, int m, int k0, int nb,
     constexpr int LD = PNB + 2;
     const int tid = threadIdx.x;
     const double* blk = pan + (int64_t)k0 * m + k0;
-    for (int idx = tid; idx < PNB * PNB; idx += 256) {
+    for (int idx = tid; idx < PNB * PNB; idx += TRSM_ROWS) {
         const int q = idx % PNB, j = idx / PNB;
         const double v = (q < nb && j < nb && j <= q) ? blk[(int64_t)j * m + q] : 0.0;
         Lc[j * LD + q] = v;
@@ -730,7 +730,7 @@ __device__ __forceinline__ void trsm_partial(double* pan, int m, int k0, int nb,
 
 // Partial last blocks (nb < 64) of the panel TRSM, launched separately so the
 // full-block kernels keep their own register budgets.  Rows [r0, r0 + nrows).
-__global__ __launch_bounds__(256) void trsm_partial_kernel(DevPlan P, const int4* __restrict__ tasks, int nrows) {
+__global__ __launch_bounds__(TRSM_ROWS) void trsm_partial_kernel(DevPlan P, const int4* __restrict__ tasks, int nrows) {
     __shared__ double Lc[PNB * (PNB + 2)];
     __shared__ double invd[PNB];
     const int4 t = tasks[blockIdx.x];
@@ -741,9 +741,11 @@ __global__ __launch_bounds__(256) void trsm_partial_kernel(DevPlan P, const int4
     trsm_partial(P.panel_pool + P.panel_off[s], m, k0, min(PNB, w - k0), r0, nrows, Lc, invd);
 }
 
-// Panel TRSM, rows [r0, r0 + 256): L11 operands packed into an LDS stream in the
-// order the generated solve consumes them (1/L(J,J), then L(J+1..63, J)).
-__global__ __launch_bounds__(256) void trsm_panel_g_kernel(DevPlan P, const int4* __restrict__ tasks) {
+// Panel TRSM, rows [r0, r0 + TRSM_ROWS): L11 operands packed into an LDS stream in
+// the order the generated solve consumes them (1/L(J,J), then L(J+1..63, J)).  One
+// wave per workgroup: the stream's broadcast reads are the kernel's LDS-bound part,
+// so a CU serves one wave's worth of them (a 16k-row panel spreads over 256 CUs).
+__global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, const int4* __restrict__ tasks) {
     __shared__ double2 S[TRSM64_STREAM / 2];
     const int4 t = tasks[blockIdx.x];
     const int s = t.x, k0 = t.y, r0 = t.z;
@@ -760,11 +762,18 @@ __global__ __launch_bounds__(256) void trsm_panel_g_kernel(DevPlan P, const int4
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pan + (int64_t)k0 * m, (uint32_t)m * PNB * 8u);
     const int voff = row < m ? row * 8 : BUF_DEAD;
     double* Sd = reinterpret_cast<double*>(S);
-    for (int e = tid; e < PNB * PNB; e += 256) {
-        const int j = e / PNB, q = e % PNB;
-        if (q >= j) {
-            const double v = blk[(int64_t)j * m + q];
-            Sd[PNB * j - j * (j - 1) / 2 + (q - j)] = (q == j) ? 1.0 / v : v;
+    {  // stage L11: all loads in flight first (lane q of column j), then the stream
+        constexpr int PER = PNB * PNB / TRSM_ROWS;
+        double v[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int e = tid + TRSM_ROWS * k, j = e / PNB, q = e % PNB;
+            v[k] = q >= j ? blk[(int64_t)j * m + q] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int e = tid + TRSM_ROWS * k, j = e / PNB, q = e % PNB;
+            if (q >= j) Sd[PNB * j - j * (j - 1) / 2 + (q - j)] = (q == j) ? 1.0 / v[k] : v[k];
         }
     }
     __syncthreads();
@@ -952,7 +961,7 @@ hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hip
 hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st, bool partial) {
     if (count <= 0) return hipSuccess;
     if (partial)
-        hipLaunchKernelGGL(trsm_partial_kernel, dim3(count), dim3(256), 0, st, P, tasks, TRSM_ROWS);
+        hipLaunchKernelGGL(trsm_partial_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks, TRSM_ROWS);
     else
         hipLaunchKernelGGL(trsm_panel_g_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks);
     return hipGetLastError();

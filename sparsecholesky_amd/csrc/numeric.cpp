@@ -1537,9 +1537,7 @@ int64_t numeric_solve_device(Numeric& N, const double* d_b, double* d_x) {
     // the graph reads b from and writes x to the handle's own vector io = d_sbuf[0, n),
     // so it is captured once, whatever buffers the caller passes
     double* io = N.d_sbuf;
-    if (!N.solve_gexec) {
-        // ~700 dependent steps per sweep at 128^3: replayed as one hipGraph
-        HIP_TRY(hipStreamBeginCapture(s0, hipStreamCaptureModeThreadLocal));
+    auto sweeps = [&]() -> hipError_t {
         hipError_t e = launch_permute(N.SP.c, io, N.d_post, n, false, s0);
         // forward: one fused launch per step (y to SP.y), then y -> c
         for (size_t i = 0; e == hipSuccess && i < N.solve_steps.size(); ++i) {
@@ -1554,6 +1552,12 @@ int64_t numeric_solve_device(Numeric& N, const double* d_b, double* d_x) {
             if (e == hipSuccess) e = launch_solve_diag(N.SP, N.d_sdiag + t.doff, t.dcount, s0);
         }
         if (e == hipSuccess) e = launch_permute(io, N.SP.c, N.d_post, n, true, s0);
+        return e;
+    };
+    if (!N.solve_gexec && !N.solve_eager) {
+        // ~700 dependent steps per sweep at 128^3: replayed as one hipGraph
+        HIP_TRY(hipStreamBeginCapture(s0, hipStreamCaptureModeThreadLocal));
+        hipError_t e = sweeps();
         hipGraph_t g = nullptr;
         hipError_t e2 = hipStreamEndCapture(s0, &g);
         HIP_TRY(e);
@@ -1563,7 +1567,10 @@ int64_t numeric_solve_device(Numeric& N, const double* d_b, double* d_x) {
     }
     const size_t nb = (size_t)n * sizeof(double);
     if (d_b != io) HIP_TRY(hipMemcpyAsync(io, d_b, nb, hipMemcpyDeviceToDevice, s0));
-    HIP_TRY(hipGraphLaunch(N.solve_gexec, s0));
+    if (N.solve_eager)
+        HIP_TRY(sweeps());
+    else
+        HIP_TRY(hipGraphLaunch(N.solve_gexec, s0));
     if (d_x != io) HIP_TRY(hipMemcpyAsync(d_x, io, nb, hipMemcpyDeviceToDevice, s0));
     HIP_TRY(hipStreamSynchronize(s0));
     return SC_OK;

@@ -250,6 +250,7 @@ struct Numeric {
     int4* d_sfwd = nullptr;  // fused forward steps (s, k0, r0, writer)
     int32_t* d_post = nullptr;
     double* d_sbuf = nullptr;  // host-interface staging (b in, x out)
+    bool solve_eager = false;          // debug: launch the sweeps directly instead of the graph
     hipGraph_t solve_graph = nullptr;  // both sweeps captured once (b in / x out through d_sbuf)
     hipGraphExec_t solve_gexec = nullptr;
 
