@@ -1072,55 +1072,132 @@ hipError_t launch_mfma_peak(double* out, int blocks, int iters, int nacc, hipStr
 
 // ---------------------------------------------------------------------------
 // Triangular solves with the supernodal factor (the
-// reference has no solve).  Level-scheduled like the factorization.  Forward:
-// one fused launch per 64-column step (solve_fwd_kernel).  Backward, per step in
-// reverse: the transposed GEMV over the rows below each 64-column block
-// (solve_gemv_kernel), then the one-wave diagonal solve L11^T x = c
-// (solve_diag_kernel).  HBM-bound: L is read once per sweep.
+// reference has no solve).  Level-scheduled like the factorization, one launch per
+// 64-column step in each sweep.  Before the first solve of a factorization,
+// solve_inv_kernel stores X = inv(L11) of every 64 x 64 diagonal block in the
+// block's unused upper triangle (X(i, k), k < i, at panel row k, column i; the
+// diagonal 1 / L(i, i) is recomputed), so no step runs a serial substitution:
+//   forward  (solve_fwd_kernel): every workgroup of a block forms y = X c_blk (a
+//            64 x 64 product) and applies its rows, c[rows[r]] -= L(r, blk) y;
+//   backward (solve_gemv_kernel, then solve_diag_kernel): every workgroup adds its
+//            rows' share -L(rows, blk)^T x(rows) into c_blk, then one workgroup per
+//            block forms x_blk = X^T c_blk (a kernel boundary between them: a
+//            device-scope fence per workgroup would write back the XCD's L2).
+// HBM-bound in principle: L is read once per sweep.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void solve_diag_kernel(SolvePlan P, const int2* __restrict__ tasks) {
-    __shared__ double Lb[PNB * (PNB + 1)];  // Lb[j * (PNB + 1) + i] = L(k0 + i, k0 + j)
-    __shared__ double dinv[PNB];
+// One wave per diagonal block (s, k0): lane j solves e_j L11^-T (the panel TRSM's
+// row solve with the identity row), which is column j of X = inv(L11), and stores its
+// strict lower part transposed into the strict upper triangle.
+__global__ __launch_bounds__(64) void solve_inv_kernel(SolvePlan P, const int2* __restrict__ tasks) {
+    __shared__ double2 S[TRSM64_STREAM / 2];
+    __shared__ double Lc[PNB * (PNB + 2)];
+    __shared__ double invd[PNB];
     const int2 t = tasks[blockIdx.x];
     const int s = t.x, k0 = t.y;
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int lane = threadIdx.x;
     const int c0 = P.sn_start[s];
     const int w = P.sn_start[s + 1] - c0;
     const int m = P.sn_m[s];
     const int nb = min(PNB, w - k0);
-    const double* __restrict__ pan = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m + k0;
-    // stage the block: 16 independent loads per thread, one column per wave access
-#pragma unroll
-    for (int q = 0; q < PNB * PNB / 256; ++q) {
-        const int e = tid + 256 * q, j = e >> 6, i = e & 63;
-        Lb[j * (PNB + 1) + i] = (i < nb && j < nb) ? pan[(int64_t)j * m + i] : 0.0;
-    }
-    if (tid < PNB) dinv[tid] = 0.0;
-    __syncthreads();
-    if (tid < nb) dinv[tid] = 1.0 / Lb[tid * (PNB + 1) + tid];
-    __syncthreads();
-    if (tid >= 64) return;
-    // lane i keeps column i of the block (L(j, i)) in registers; all 64 steps run
-    // (zero padding past nb is inert), fully unrolled so the pivot and its
-    // reciprocal come from readlane, not LDS
+    double* blk = const_cast<double*>(P.panel_pool) + P.panel_off[s] + (int64_t)k0 * m + k0;
     double r[PNB];
+    {  // row `lane` of the block, all loads in flight first (lane = row: coalesced per column)
 #pragma unroll
-    for (int j = 0; j < PNB; ++j) r[j] = Lb[lane * (PNB + 1) + j];
-    const double d = dinv[lane];
-    double v = lane < nb ? P.c[c0 + k0 + lane] : 0.0;
-#pragma unroll
-    for (int j = PNB - 1; j >= 0; --j) {  // x_j = v_j / L_jj; v_i -= L_ji x_j (i < j)
-        const double xj = readlane_f64(v, j) * readlane_f64(d, j);
-        v = lane == j ? xj : (lane < j ? v - r[j] * xj : v);
+        for (int j = 0; j < PNB; ++j) r[j] = (j < nb && lane < nb && lane >= j) ? blk[(int64_t)j * m + lane] : 0.0;
     }
-    if (lane < nb) P.c[c0 + k0 + lane] = v;
+    if (nb == PNB) {
+        double* Sd = reinterpret_cast<double*>(S);
+#pragma unroll
+        for (int j = 0; j < PNB; ++j)  // the packed stream: 1 / L(j, j), then L(j+1..63, j)
+            if (lane >= j) Sd[PNB * j - j * (j - 1) / 2 + (lane - j)] = lane == j ? 1.0 / r[j] : r[j];
+    } else {
+        constexpr int LD = PNB + 2;
+#pragma unroll
+        for (int j = 0; j < PNB; ++j) {
+            Lc[j * LD + lane] = r[j];
+            if (lane == j) invd[j] = j < nb ? 1.0 / r[j] : 0.0;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < PNB; ++c) r[c] = c == lane ? 1.0 : 0.0;
+    if (nb == PNB)
+        trsm64_full(r, S);
+    else
+        trsm_steps<0>(r, Lc, invd, nb);
+#pragma unroll
+    for (int c = 0; c < PNB; ++c)
+        if (lane < c && c < nb) blk[(int64_t)c * m + lane] = r[c];
 }
 
-// c[blk] -= L[rows, blk]^T x[rows].  Per 64-row chunk: coalesced column loads into
-// LDS, then thread (column j, quarter g) sums 16 rows of column j.
+// y = X c_blk for the block at pan (column-major, ld m).  X is staged through LDS
+// with coalesced loads (column i of the panel block holds X(i, 0..i-1) in rows
+// 0..i-1: Xs[i][k]), the diagonal as 1 / L(i, i); then thread (row i = tid & 63,
+// quarter g) sums k in [16 g, 16 g + 16).  vb receives y.  256 threads.
+__device__ __forceinline__ void inv_apply(const double* __restrict__ pan, int64_t m, int nb, const double* cb,
+                                          double* vb, double (*part)[PNB], double (*Xs)[PNB + 1]) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < PNB * PNB / 256; ++q) {
+        const int e = tid + 256 * q, i = e >> 6, k = e & 63;  // lanes along k: coalesced in column i
+        double v = 0.0;
+        if (i < nb && k <= i) {
+            v = pan[(int64_t)i * m + k];
+            if (k == i) v = 1.0 / v;
+        }
+        Xs[i][k] = v;
+    }
+    __syncthreads();
+    const int i = tid & 63, g = tid >> 6;
+    double acc = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc = fma(Xs[i][g * 16 + q], cb[g * 16 + q], acc);
+    part[g][i] = acc;
+    __syncthreads();
+    if (tid < PNB) vb[tid] = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
+    __syncthreads();
+}
+
+// Forward step: every workgroup of block (s, k0) forms y = X c_blk and applies its
+// rows [r0, r0 + SOLVE_ROWS) below the block; the writer (t.w = 1) stores y to P.y
+// (not c, which the step's other workgroups still read).  r0 < 0: diagonal only.
+__global__ __launch_bounds__(SOLVE_ROWS) void solve_fwd_kernel(SolvePlan P, const int4* __restrict__ tasks) {
+    __shared__ double vb[PNB], cb[PNB];
+    __shared__ double part[4][PNB];
+    __shared__ double Xs[PNB][PNB + 1];
+    const int4 t = tasks[blockIdx.x];
+    const int s = t.x, k0 = t.y, r0 = t.z;
+    const int tid = threadIdx.x;
+    const int c0 = P.sn_start[s];
+    const int w = P.sn_start[s + 1] - c0;
+    const int m = P.sn_m[s];
+    const int nb = min(PNB, w - k0);
+    const double* __restrict__ pan = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m;
+    // this thread's row below the block: its 64 loads go out first, overlapping y = X c
+    const int r = r0 + tid;
+    const bool live = r0 >= 0 && r < m;
+    double v[PNB];
+#pragma unroll
+    for (int q = 0; q < PNB; ++q) v[q] = (live && q < nb) ? pan[(int64_t)q * m + r] : 0.0;
+    if (tid < PNB) cb[tid] = tid < nb ? P.c[c0 + k0 + tid] : 0.0;
+    __syncthreads();
+    inv_apply(pan + k0, m, nb, cb, vb, part, Xs);
+    if (t.w && tid < nb) P.y[c0 + k0 + tid] = vb[tid];
+    if (r0 < 0) return;
+    const int32_t* __restrict__ rows = P.rows + P.rows_ptr[s];
+    double acc = 0.0;
+#pragma unroll
+    for (int q = 0; q < PNB; ++q) acc = fma(v[q], vb[q], acc);
+    if (live) unsafeAtomicAdd(P.c + rows[r], -acc);
+}
+
+// Backward step, part 1: workgroup (s, k0, r0) adds -L(rows, blk)^T x(rows) into
+// c_blk for rows [r0, r0 + SOLVE_ROWS) below the block (fp64 atomics).  Thread t
+// owns row r0 + t: it loads its 64 entries (coalesced per column, all in flight),
+// scales them by x of its row and leaves them in LDS; then thread (column j, quarter
+// g) sums a quarter of column j.
 __global__ __launch_bounds__(SOLVE_ROWS) void solve_gemv_kernel(SolvePlan P, const int4* __restrict__ tasks) {
-    __shared__ double vb[SOLVE_ROWS];             // x of the rows
-    __shared__ double T[PNB * (PNB + 1)];         // 64-row chunk, T[j * (PNB + 1) + i]
+    __shared__ double T[PNB][SOLVE_ROWS + 1];     // T[j][row] = L(row, j) x(row)
     __shared__ double part[SOLVE_ROWS / 64][PNB];
     const int4 t = tasks[blockIdx.x];
     const int s = t.x, k0 = t.y, r0 = t.z;
@@ -1133,87 +1210,74 @@ __global__ __launch_bounds__(SOLVE_ROWS) void solve_gemv_kernel(SolvePlan P, con
     const int32_t* __restrict__ rows = P.rows + P.rows_ptr[s];
     const int r = r0 + tid;
     const bool live = r < m;
-    vb[tid] = live ? P.c[rows[r]] : 0.0;
-    const int j = tid & 63, g = tid >> 6;
-    double acc = 0.0;
-    for (int ch = 0; ch < SOLVE_ROWS && r0 + ch < m; ch += 64) {
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < PNB * 64 / SOLVE_ROWS; ++q) {
-            const int e = tid + SOLVE_ROWS * q, jj = e >> 6, ii = e & 63;
-            const int rr = r0 + ch + ii;
-            T[jj * (PNB + 1) + ii] = (rr < m && jj < nb) ? pan[(int64_t)jj * m + rr] : 0.0;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc += T[j * (PNB + 1) + g * 16 + q] * vb[ch + g * 16 + q];
-    }
-    part[g][j] = acc;
-    __syncthreads();
-    if (tid < nb) {
-        double a = 0.0;
-#pragma unroll
-        for (int q = 0; q < SOLVE_ROWS / 64; ++q) a += part[q][tid];
-        unsafeAtomicAdd(P.c + c0 + k0 + tid, -a);
-    }
-}
-
-// Fused forward step (one launch per 64-column step instead of two): every GEMV
-// workgroup of block (s, k0) solves L11 y = c_blk itself from the 64 x 64 block
-// (32 KB, L2-resident across the step's workgroups) and applies its rows.  The
-// block's writer (t.w = 1) stores y to P.y, not to c, which the step's other
-// workgroups still read.  r0 < 0: a block with no rows below (diagonal only).
-__global__ __launch_bounds__(SOLVE_ROWS) void solve_fwd_kernel(SolvePlan P, const int4* __restrict__ tasks) {
-    __shared__ double Lb[PNB * (PNB + 1)];  // Lb[j * (PNB + 1) + i] = L(k0 + i, k0 + j)
-    __shared__ double vb[PNB];
-    const int4 t = tasks[blockIdx.x];
-    const int s = t.x, k0 = t.y, r0 = t.z;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int c0 = P.sn_start[s];
-    const int w = P.sn_start[s + 1] - c0;
-    const int m = P.sn_m[s];
-    const int nb = min(PNB, w - k0);
-    const double* __restrict__ pan = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m;
-#pragma unroll
-    for (int q = 0; q < PNB * PNB / SOLVE_ROWS; ++q) {
-        const int e = tid + SOLVE_ROWS * q, j = e >> 6, i = e & 63;
-        Lb[j * (PNB + 1) + i] = (i < nb && j < nb) ? pan[(int64_t)j * m + k0 + i] : 0.0;
-    }
-    __syncthreads();
-    if (tid < 64) {
-        double r[PNB];
-#pragma unroll
-        for (int j = 0; j < PNB; ++j) r[j] = Lb[j * (PNB + 1) + lane];
-        const double d = lane < nb ? 1.0 / Lb[lane * (PNB + 1) + lane] : 0.0;
-        double v = lane < nb ? P.c[c0 + k0 + lane] : 0.0;
-#pragma unroll
-        for (int j = 0; j < PNB; ++j) {  // y_j = v_j / L_jj; v_i -= L_ij y_j (i > j)
-            const double yj = readlane_f64(v, j) * readlane_f64(d, j);
-            v = lane == j ? yj : (lane > j ? v - r[j] * yj : v);
-        }
-        vb[lane] = v;
-        if (t.w && lane < nb) P.y[c0 + k0 + lane] = v;
-    }
-    __syncthreads();
-    if (r0 < 0) return;
-    const int32_t* __restrict__ rows = P.rows + P.rows_ptr[s];
-    const int r = r0 + tid;
-    const bool live = r < m;
-    double acc = 0.0;
+    const double xr = live ? P.c[rows[r]] : 0.0;
 #pragma unroll
     for (int jc = 0; jc < PNB; jc += 16) {
         double v[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) v[q] = (live && jc + q < nb) ? pan[(int64_t)(jc + q) * m + r] : 0.0;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) acc += v[q] * vb[jc + q];
+        for (int q = 0; q < 16; ++q) T[jc + q][tid] = v[q] * xr;
     }
-    if (live) unsafeAtomicAdd(P.c + rows[r], -acc);
+    __syncthreads();
+    const int j = tid & 63, g = tid >> 6;
+    double acc = 0.0;
+#pragma unroll 8
+    for (int q = 0; q < SOLVE_ROWS / 4; ++q) acc += T[j][g * (SOLVE_ROWS / 4) + q];
+    part[g][j] = acc;
+    __syncthreads();
+    if (tid < nb) unsafeAtomicAdd(P.c + c0 + k0 + tid, -(part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid]));
+}
+
+// Backward step, part 2: x_blk = X^T c_blk for every block (s, k0) of the step:
+// thread (column k = tid & 63, quarter g) sums X(i, k) c_i over i in its quarter.
+__global__ __launch_bounds__(256) void solve_diag_kernel(SolvePlan P, const int2* __restrict__ tasks) {
+    __shared__ double cb[PNB];
+    __shared__ double part[4][PNB];
+    const int2 t = tasks[blockIdx.x];
+    const int s = t.x, k0 = t.y;
+    const int tid = threadIdx.x, k = tid & 63, g = tid >> 6;
+    const int c0 = P.sn_start[s];
+    const int w = P.sn_start[s + 1] - c0;
+    const int m = P.sn_m[s];
+    const int nb = min(PNB, w - k0);
+    const double* __restrict__ blk = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m + k0;
+    if (tid < PNB) cb[tid] = tid < nb ? P.c[c0 + k0 + tid] : 0.0;
+    __syncthreads();
+    double acc = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int i = g * 16 + q;
+        double xik = 0.0;  // X(i, k), i >= k: row k, column i of the block (lanes along k: coalesced)
+        if (i < nb && k <= i) xik = k < i ? blk[(int64_t)i * m + k] : 1.0 / blk[(int64_t)i * m + i];
+        acc = fma(xik, cb[i], acc);
+    }
+    part[g][k] = acc;
+    __syncthreads();
+    if (tid < nb) P.c[c0 + k0 + tid] = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
 }
 
 hipError_t launch_solve_fwd(const SolvePlan& P, const int4* tasks, int count, hipStream_t st) {
     if (count <= 0) return hipSuccess;
     hipLaunchKernelGGL(solve_fwd_kernel, dim3(count), dim3(SOLVE_ROWS), 0, st, P, tasks);
+    return hipGetLastError();
+}
+
+hipError_t launch_solve_gemv(const SolvePlan& P, const int4* tasks, int count, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(solve_gemv_kernel, dim3(count), dim3(SOLVE_ROWS), 0, st, P, tasks);
+    return hipGetLastError();
+}
+
+hipError_t launch_solve_diag(const SolvePlan& P, const int2* tasks, int count, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(solve_diag_kernel, dim3(count), dim3(256), 0, st, P, tasks);
+    return hipGetLastError();
+}
+
+hipError_t launch_solve_inv(const SolvePlan& P, const int2* tasks, int count, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(solve_inv_kernel, dim3(count), dim3(64), 0, st, P, tasks);
     return hipGetLastError();
 }
 
@@ -1225,18 +1289,6 @@ __global__ void permute_kernel(double* __restrict__ dst, const double* __restric
         dst[perm[i]] = src[i];
     else
         dst[i] = src[perm[i]];
-}
-
-hipError_t launch_solve_diag(const SolvePlan& P, const int2* tasks, int count, hipStream_t st) {
-    if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(solve_diag_kernel, dim3(count), dim3(256), 0, st, P, tasks);
-    return hipGetLastError();
-}
-
-hipError_t launch_solve_gemv(const SolvePlan& P, const int4* tasks, int count, hipStream_t st) {
-    if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(solve_gemv_kernel, dim3(count), dim3(SOLVE_ROWS), 0, st, P, tasks);
-    return hipGetLastError();
 }
 
 hipError_t launch_permute(double* dst, const double* src, const int32_t* perm, int64_t n, bool scatter,

@@ -77,16 +77,18 @@ struct SolvePlan {
     double* y;                // forward result (fused steps write here; copied to c after the sweep)
 };
 constexpr int SOLVE_ROWS = 256;  // front rows per GEMV workgroup
-// Backward sweep.  tasks (s, k0): the 64-column diagonal block of supernode s at
-// column k0, L11^T x = c in place in c
-hipError_t launch_solve_diag(const SolvePlan& P, const int2* tasks, int count, hipStream_t st);
-// tasks (s, k0, r0): front rows [r0, r0 + SOLVE_ROWS) below the block,
-// c[blk] -= L[r, blk]^T x[rows[r]] (fp64 atomics across the block's workgroups)
-hipError_t launch_solve_gemv(const SolvePlan& P, const int4* tasks, int count, hipStream_t st);
-// Forward sweep, one fused launch per step: tasks (s, k0, r0, writer); every
-// workgroup solves L11 y = c_blk itself and applies c[rows[r]] -= L[r, blk] y
-// (fp64 atomics: fronts of a level share ancestors); r0 < 0 = diagonal block only
+// X = inv(L11) of the 64 x 64 diagonal blocks (s, k0) into their strict upper
+// triangles (the factor's lower part is untouched); once per factorization, before
+// the first solve.
+hipError_t launch_solve_inv(const SolvePlan& P, const int2* tasks, int count, hipStream_t st);
+// Forward step: tasks (s, k0, r0, writer); every workgroup forms y = X c_blk and
+// applies c[rows[r]] -= L[r, blk] y for its SOLVE_ROWS rows (fp64 atomics: fronts of
+// a level share ancestors); r0 < 0 = the diagonal block only.
 hipError_t launch_solve_fwd(const SolvePlan& P, const int4* tasks, int count, hipStream_t st);
+// Backward step: tasks (s, k0, r0): c_blk -= L[rows, blk]^T x[rows] (fp64 atomics),
+// then tasks (s, k0): x_blk = X^T c_blk.
+hipError_t launch_solve_gemv(const SolvePlan& P, const int4* tasks, int count, hipStream_t st);
+hipError_t launch_solve_diag(const SolvePlan& P, const int2* tasks, int count, hipStream_t st);
 // c[i] = b[perm[i]] (gather) or x[perm[i]] = c[i] (scatter)
 hipError_t launch_permute(double* dst, const double* src, const int32_t* perm, int64_t n, bool scatter,
                           hipStream_t st);

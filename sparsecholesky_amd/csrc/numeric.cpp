@@ -1464,7 +1464,7 @@ static int64_t solve_build(Numeric& N) {
     std::vector<std::vector<int32_t>> by_level((size_t)S.nlevels);
     for (int32_t s = 0; s < S.ns; ++s) by_level[S.level[s]].push_back(s);
     std::vector<int2> diag;
-    std::vector<int4> gemv, fwd;
+    std::vector<int4> bwd, fwd;
     // internal index -> index in the caller's order (postorder, then the fill-reducing
     // permutation when one is in effect)
     std::vector<int32_t> solve_perm(S.post);
@@ -1476,21 +1476,23 @@ static int64_t solve_build(Numeric& N) {
         for (int k0 = 0; k0 < maxw; k0 += PNB) {
             Numeric::SolveStep st {};
             st.doff = (int64_t)diag.size();
-            st.goff = (int64_t)gemv.size();
+            st.goff = (int64_t)bwd.size();
             st.foff = (int64_t)fwd.size();
             for (int32_t s : by_level[lev]) {
                 const int w = S.w(s), m = S.sn_m[s];
                 if (w <= k0) continue;
+                const int slot = (int)diag.size();
                 diag.push_back(make_int2(s, k0));
                 const int rb = std::min(w, k0 + PNB);
+                (void)slot;
                 if (rb >= m) fwd.push_back(make_int4(s, k0, -1, 1));
                 for (int r0 = rb; r0 < m; r0 += SOLVE_ROWS) {
-                    gemv.push_back(make_int4(s, k0, r0, 0));
+                    bwd.push_back(make_int4(s, k0, r0, 0));
                     fwd.push_back(make_int4(s, k0, r0, r0 == rb ? 1 : 0));
                 }
             }
             st.dcount = (int32_t)((int64_t)diag.size() - st.doff);
-            st.gcount = (int32_t)((int64_t)gemv.size() - st.goff);
+            st.gcount = (int32_t)((int64_t)bwd.size() - st.goff);
             st.fcount = (int32_t)((int64_t)fwd.size() - st.foff);
             N.solve_steps.push_back(st);
         }
@@ -1498,7 +1500,8 @@ static int64_t solve_build(Numeric& N) {
     int64_t rc;
     int32_t* d_rows = nullptr;
     int64_t* d_rows_ptr = nullptr;
-    if ((rc = upload(N, diag, N.d_sdiag)) || (rc = upload(N, gemv, N.d_sgemv)) || (rc = upload(N, fwd, N.d_sfwd)) ||
+    N.n_sdiag = (int32_t)diag.size();
+    if ((rc = upload(N, diag, N.d_sdiag)) || (rc = upload(N, bwd, N.d_sgemv)) || (rc = upload(N, fwd, N.d_sfwd)) ||
         (rc = upload(N, S.rows, d_rows)) ||
         (rc = upload(N, S.rows_ptr, d_rows_ptr)) || (rc = upload(N, solve_perm, N.d_post)))
         return rc;
@@ -1564,6 +1567,10 @@ int64_t numeric_solve_device(Numeric& N, const double* d_b, double* d_x) {
         HIP_TRY(e2);
         N.solve_graph = g;
         HIP_TRY(hipGraphInstantiate(&N.solve_gexec, g, nullptr, nullptr, 0));
+    }
+    if (N.inv_gen != N.factor_gen) {  // inverses of the diagonal blocks, once per factorization
+        HIP_TRY(launch_solve_inv(N.SP, N.d_sdiag, N.n_sdiag, s0));
+        N.inv_gen = N.factor_gen;
     }
     const size_t nb = (size_t)n * sizeof(double);
     if (d_b != io) HIP_TRY(hipMemcpyAsync(io, d_b, nb, hipMemcpyDeviceToDevice, s0));

@@ -245,8 +245,10 @@ struct Numeric {
     std::vector<SolveStep> solve_steps;  // forward order (levels up, k0 up)
     bool solve_ready = false;
     SolvePlan SP {};
-    int2* d_sdiag = nullptr;
-    int4* d_sgemv = nullptr;
+    int2* d_sdiag = nullptr;         // diagonal blocks (s, k0): inverse preparation
+    int32_t n_sdiag = 0;
+    int64_t inv_gen = -1;            // factor_gen whose diagonal-block inverses are in place
+    int4* d_sgemv = nullptr;         // backward GEMV tasks (s, k0, r0)
     int4* d_sfwd = nullptr;  // fused forward steps (s, k0, r0, writer)
     int32_t* d_post = nullptr;
     double* d_sbuf = nullptr;  // host-interface staging (b in, x out)
