@@ -14,8 +14,9 @@ import torch  # noqa: E402
 import sparsecholesky_amd as sc  # noqa: E402
 
 k = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+opts = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in sys.argv[2:]}  # e.g. lookahead=0
 A = sc.laplacian3d(k)
-num = sc.Numeric(sc.Symbolic(A, use_graph=0))
+num = sc.Numeric(sc.Symbolic(A, use_graph=0, **opts))
 d = torch.from_numpy(A.x).to("cuda:0")
 num.set_profile(1)
 for _ in range(2):

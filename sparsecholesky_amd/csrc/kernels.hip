@@ -4,8 +4,8 @@
 // columns (the L panel, m x w, column-major, ld = m) become L and whose trailing
 // (m-w) x (m-w) lower block is the contribution block CB (ld = mb) handed to the
 // parent.  Replaces the reference's per-supernode dense calls:
-//   dpotrf_     include/chol.hpp:1263   -> front_small_kernel / potrf_diag_kernel
-//   cblas_dtrsm include/chol.hpp:1292   -> front_small_kernel / trsm_panel_kernel
+//   dpotrf_     include/chol.hpp:1263   -> front_small_kernel / trsm_panel_g_kernel (fused)
+//   cblas_dtrsm include/chol.hpp:1292   -> front_small_kernel / trsm_panel_g_kernel
 //   cblas_dsyrk include/chol.hpp:1322   -> front_small_kernel / syrk_mfma_kernel
 //   apply_update include/chol.hpp:1196  -> extend-add gather in front_small_kernel /
 //                                          assemble_large_kernel
@@ -77,8 +77,8 @@ __global__ __launch_bounds__(256) void assemble_cols_kernel(DevPlan P, const int
         const int mbc = P.sn_m[c] - (P.sn_start[c + 1] - P.sn_start[c]);
         const int32_t* __restrict__ rel = P.relind + P.rel_ptr[c];
         const double* __restrict__ cb = P.cb_pool + P.cb_off[c];
-        const int jlo = lower_bound_i32(rel, mbc, j0);
-        const int jhi = lower_bound_i32(rel, mbc, j1);
+        const int32_t* __restrict__ cbnd = P.col_bnd + P.cbk_ptr[c];  // j0 = t.y * ASM_COLS
+        const int jlo = cbnd[t.y], jhi = cbnd[t.y + 1];
         for (int jc = jlo + wid; jc < jhi; jc += 4) {
             const int pj = rel[jc];
             const double* __restrict__ src = cb + (int64_t)jc * mbc;
@@ -94,27 +94,41 @@ __global__ __launch_bounds__(256) void assemble_cols_kernel(DevPlan P, const int
 // tile is built in LDS (zero, A entries, then each child's rows that map into it,
 // children in fixed order; relative indices are injective and increasing, so a
 // child's rows for the tile are one contiguous run, precomputed on the host in
-// rel_bnd) and its lower part is stored once.  HBM traffic: one write per front
-// entry plus one read per child entry (zero-then-add paid 8 + 24 B).
+// rel_bnd / col_bnd) and its lower part is stored once.  HBM traffic: one write
+// per front entry plus one read per child entry (zero-then-add paid 8 + 24 B).
+// Wave w owns the tile columns j0 + w + 4q, so after one prologue that stages up
+// to ASM_CCH children's bounds in LDS the waves never synchronise: each child's
+// entries for a wave's columns (<= 4 columns x 256 rows) are loaded with all
+// loads in flight before the adds (the kernel is latency-bound otherwise).
+constexpr int ASM_CCH = 32;  // children staged per prologue
 __global__ __launch_bounds__(256) void assemble_tile_kernel(DevPlan P, const int2* __restrict__ tasks,
                                                              const double* __restrict__ Ax) {
     __shared__ double T[ASM_COLS * ASM_ROWS];  // T[(j - j0) * ASM_ROWS + (r - r0)]
+    __shared__ const double* s_src[ASM_CCH];
+    __shared__ const int32_t* s_rel[ASM_CCH];
+    __shared__ int s_mbc[ASM_CCH], s_ilo[ASM_CCH], s_ihi[ASM_CCH], s_jlo[ASM_CCH];
+    __shared__ int8_t s_pj[ASM_CCH][ASM_COLS];  // parent tile column of child column jlo + l, or -1
     const int2 t = tasks[blockIdx.x];
     const int s = t.x;
     const int k = t.y >> 16;
+    const int jb = t.y & 0xffff;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
     const int c0 = P.sn_start[s];
     const int w = P.sn_start[s + 1] - c0;
     const int m = P.sn_m[s];
     const int mb = m - w;
-    const int j0 = (t.y & 0xffff) * ASM_COLS;
+    const int j0 = jb * ASM_COLS;
     const int j1 = min(m, j0 + ASM_COLS);
     const int r0 = k * ASM_ROWS, r1 = min(m, r0 + ASM_ROWS);
     double* panel = P.panel_pool + P.panel_off[s];
     double* cbs = P.cb_pool + P.cb_off[s];
-    for (int idx = tid; idx < ASM_COLS * ASM_ROWS; idx += 256) T[idx] = 0.0;
-    __syncthreads();
+    const int cp0 = P.child_ptr[s], cp1 = P.child_ptr[s + 1];
+    // own columns: zero, then A entries (program order within the wave)
+#pragma unroll
+    for (int q = 0; q < ASM_COLS / 4; ++q)
+#pragma unroll
+        for (int r = lane; r < ASM_ROWS; r += 64) T[(wid + 4 * q) * ASM_ROWS + r] = 0.0;
     for (int j = j0 + wid; j < min(j1, w); j += 4) {
         const int64_t a0 = P.a_ptr[c0 + j], a1 = P.a_ptr[c0 + j + 1];
         for (int64_t q = a0 + lane; q < a1; q += 64) {
@@ -122,27 +136,66 @@ __global__ __launch_bounds__(256) void assemble_tile_kernel(DevPlan P, const int
             if (p >= r0 && p < r1) T[(j - j0) * ASM_ROWS + (p - r0)] = Ax[P.a_src[q]];
         }
     }
-    __syncthreads();
-    for (int ci = P.child_ptr[s]; ci < P.child_ptr[s + 1]; ++ci) {
-        const int c = P.child_list[ci];
-        const int mbc = P.sn_m[c] - (P.sn_start[c + 1] - P.sn_start[c]);
-        const int32_t* __restrict__ rel = P.relind + P.rel_ptr[c];
-        const int32_t* __restrict__ bnd = P.rel_bnd + P.rb_ptr[c];
-        const int ilo = bnd[k], ihi = bnd[k + 1];
-        if (ilo < ihi) {
-            // child columns landing in [j0, j1) lie in row tile j0 / ASM_ROWS
-            const int u0 = bnd[j0 / ASM_ROWS], u1 = bnd[j0 / ASM_ROWS + 1];
-            const int jlo = u0 + lower_bound_i32(rel + u0, u1 - u0, j0);
-            const int jhi = u0 + lower_bound_i32(rel + u0, u1 - u0, j1);
-            const double* __restrict__ cb = P.cb_pool + P.cb_off[c];
-            for (int jc = jlo + wid; jc < jhi; jc += 4) {
-                const double* __restrict__ src = cb + (int64_t)jc * mbc;
-                double* Tc = T + (rel[jc] - j0) * ASM_ROWS - r0;
-                for (int ic = max(jc, ilo) + lane; ic < ihi; ic += 64) Tc[rel[ic]] += src[ic];
-            }
+    for (int cb = cp0; cb < cp1; cb += ASM_CCH) {
+        const int nc = min(ASM_CCH, cp1 - cb);
+        if (cb > cp0) __syncthreads();  // previous chunk's staging fully read
+        if (tid < nc) {
+            const int c = P.child_list[cb + tid];
+            const int mbc = P.sn_m[c] - (P.sn_start[c + 1] - P.sn_start[c]);
+            const int32_t* rel = P.relind + P.rel_ptr[c];
+            const int32_t* bnd = P.rel_bnd + P.rb_ptr[c];
+            const int32_t* cbnd = P.col_bnd + P.cbk_ptr[c];
+            const int ilo = bnd[k], ihi = bnd[k + 1], jlo = cbnd[jb], jhi = cbnd[jb + 1];
+            int pj[ASM_COLS];
+#pragma unroll
+            for (int l = 0; l < ASM_COLS; ++l) pj[l] = (jlo + l < jhi && ilo < ihi) ? rel[jlo + l] - j0 : -1;
+#pragma unroll
+            for (int l = 0; l < ASM_COLS; ++l) s_pj[tid][l] = (int8_t)pj[l];
+            s_src[tid] = P.cb_pool + P.cb_off[c];
+            s_rel[tid] = rel;
+            s_mbc[tid] = mbc;
+            s_ilo[tid] = ilo;
+            s_ihi[tid] = ihi;
+            s_jlo[tid] = jlo;
         }
         __syncthreads();
+        for (int i = 0; i < nc; ++i) {
+            const int pjl = lane < ASM_COLS ? (int)s_pj[i][lane] : -1;
+            uint64_t mask = __ballot(pjl >= 0 && (pjl & 3) == wid);
+            if (!mask) continue;
+            const int mbc = s_mbc[i], ilo = s_ilo[i], ihi = s_ihi[i], jlo = s_jlo[i];
+            const double* __restrict__ src = s_src[i];
+            const int32_t* __restrict__ rel = s_rel[i];
+            // up to 4 child columns for this wave, each <= ASM_ROWS rows: all loads first
+            int jc[4], tc[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int b = mask ? __builtin_ctzll(mask) : -1;
+                jc[q] = b < 0 ? -1 : jlo + b;
+                tc[q] = b < 0 ? 0 : __shfl(pjl, b);
+                mask &= mask - 1;
+            }
+            double v[4][ASM_ROWS / 64];
+            int rr[4][ASM_ROWS / 64];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int lo = max(jc[q], ilo) + lane;
+#pragma unroll
+                for (int ch = 0; ch < ASM_ROWS / 64; ++ch) {
+                    const int ic = lo + 64 * ch;
+                    const bool ok = jc[q] >= 0 && ic < ihi;
+                    rr[q][ch] = ok ? rel[ic] : -1;
+                    v[q][ch] = ok ? src[(int64_t)jc[q] * mbc + ic] : 0.0;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int ch = 0; ch < ASM_ROWS / 64; ++ch)
+                    if (rr[q][ch] >= 0) T[tc[q] * ASM_ROWS + rr[q][ch] - r0] += v[q][ch];
+        }
     }
+    // own columns: store the lower part once
     for (int j = j0 + wid; j < j1; j += 4) {
         double* col = (j < w) ? panel + (int64_t)j * m : cbs + (int64_t)(j - w) * mb - w;
         const double* Tc = T + (j - j0) * ASM_ROWS - r0;
@@ -156,49 +209,6 @@ __device__ __forceinline__ double readlane_f64(double v, int src) {
     const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), src);
     const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-// Step J of the register-resident right-looking Cholesky of a <= 64 x 64 block
-// (lane = row).  Template recursion forces full unrolling so r[] keeps static
-// register indices (a rolled loop turns them into select chains).
-template <int J>
-__device__ __forceinline__ void potrf_steps(double (&r)[PNB], double* colj, int lane, int nb, int32_t* info,
-                                            int col0) {
-    if constexpr (J < PNB) {
-        if (J < nb) {
-            const double d = readlane_f64(r[J], J);
-            if (lane == 0 && !(d > 0.0)) report_fail(info, col0 + J);
-            const double piv = sqrt(d);
-            const double inv = 1.0 / piv;
-            const double rj = (lane == J) ? piv : r[J] * inv;
-            r[J] = rj;
-            colj[lane] = rj;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-            for (int q = J + 1; q < PNB; ++q) r[q] = fma(-rj, colj[q], r[q]);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            potrf_steps<J + 1>(r, colj, lane, nb, info, col0);
-        }
-    }
-}
-
-// One wave factors the nb x nb (nb <= 64) lower block at `blk` (ld) in place.
-__device__ __forceinline__ void potrf_block_wave(double* blk, int64_t ld, int nb, int lane, double* colj,
-                                                 int32_t* info, int col0) {
-    const bool live = lane < nb;
-    double r[PNB];
-#pragma unroll
-    for (int c = 0; c < PNB; ++c) r[c] = (live && c <= lane) ? blk[(int64_t)c * ld + lane] : 0.0;
-    potrf_steps<0>(r, colj, lane, nb, info, col0);
-    if (live) {
-#pragma unroll
-        for (int c = 0; c < PNB; ++c)
-            if (c < nb && c <= lane) blk[(int64_t)c * ld + lane] = r[c];
-    }
 }
 
 // Forward substitution steps of one row against L11 (column-major in LDS).
@@ -674,8 +684,11 @@ __device__ __forceinline__ void buf_st(double v, __amdgpu_buffer_rsrc_t rs, int 
 
 #include "panel_gen.inc"
 
-__global__ __launch_bounds__(64) void potrf_diag_g_kernel(DevPlan P, const int2* __restrict__ tasks) {
-    __shared__ double C[2 * PNB];
+// Diagonal block (nb <= 64) of a large front's panel: 256 threads hold its 4 x 4
+// tiles in registers (the small-front machinery with m = w = nb: 16 four-pivot
+// steps, one LDS barrier each) instead of one wave walking 64 pivots.
+__global__ __launch_bounds__(256) void potrf_tiles_kernel(DevPlan P, const int2* __restrict__ tasks) {
+    __shared__ __attribute__((aligned(16))) double colbuf[2 * 4 * COLB];
     const int2 t = tasks[blockIdx.x];
     const int s = t.x, k0 = t.y;
     const int c0 = P.sn_start[s];
@@ -683,20 +696,24 @@ __global__ __launch_bounds__(64) void potrf_diag_g_kernel(DevPlan P, const int2*
     const int m = P.sn_m[s];
     const int nb = min(PNB, w - k0);
     double* blk = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m + k0;
-    const int lane = threadIdx.x;
-    if (nb < PNB) {
-        potrf_block_wave(blk, m, nb, lane, C, P.info, c0 + k0);
-        return;
-    }
-    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(blk);
-    double r[PNB];
+    SmallRegs<1> R;
+    small_tiles<1>(R, nb, nb);
 #pragma unroll
-    for (int c = 0; c < PNB; ++c) r[c] = buf_ld(rs, lane * 8, c * m * 8);
-    const int bad = potrf64_full(r, C, lane);
-    if (bad >= 0 && lane == 0) report_fail(P.info, c0 + k0 + bad);
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int c = 0; c < PNB; ++c)
-        if (c <= lane) buf_st(r[c], rs, lane * 8, c * m * 8);
+        for (int c = 0; c < 4; ++c) {
+            const int i = 4 * R.bi[0] + r, j = 4 * R.bj[0] + c;
+            R.v[0][r * 4 + c] = (R.bi[0] >= 0 && i < nb && i >= j) ? blk[(int64_t)j * m + i] : 0.0;
+        }
+    small_steps<1>(R, colbuf, nb, P.info, c0 + k0);
+    if (R.bi[0] < 0) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int i = 4 * R.bi[0] + r, j = 4 * R.bj[0] + c;
+            if (i < nb && i >= j) blk[(int64_t)j * m + i] = R.v[0][r * 4 + c];
+        }
 }
 
 // Partial last block (nb < 64) of the panel TRSM: template path, kept out of
@@ -741,12 +758,21 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_partial_kernel(DevPlan P, cons
     trsm_partial(P.panel_pool + P.panel_off[s], m, k0, min(PNB, w - k0), r0, nrows, Lc, invd);
 }
 
-// Panel TRSM, rows [r0, r0 + TRSM_ROWS): L11 operands packed into an LDS stream in
-// the order the generated solve consumes them (1/L(J,J), then L(J+1..63, J)).  One
-// wave per workgroup: the stream's broadcast reads are the kernel's LDS-bound part,
-// so a CU serves one wave's worth of them (a 16k-row panel spreads over 256 CUs).
-__global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, const int4* __restrict__ tasks) {
+// Diagonal block POTRF fused with the panel TRSM, rows [r0, r0 + TRSM_ROWS): every
+// workgroup loads the 64 x 64 diagonal block, factors it in registers (4 x 4 tiles,
+// 16 four-pivot steps: a few microseconds) and packs L11 into an LDS stream in the
+// order the generated solve consumes it (1/L(J,J), then L(J+1..63, J)).  One launch
+// per 64-column step instead of two: on the panel chain every kernel boundary costs
+// more than this redundant factorization.  L11 overwrites the block in HBM only once
+// every workgroup of the block has read it: t.w - 1 indexes the block's arrival
+// counter, and the last workgroup to arrive stores L11 and rearms the counter.  A
+// block with no rows below gets one task with r0 >= m (factor and store only).
+__global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, const int4* __restrict__ tasks,
+                                                                 int32_t* __restrict__ arrive) {
+    static_assert(TRSM_ROWS == 256, "the fused POTRF maps 4 x 4 tiles onto 256 threads");
     __shared__ double2 S[TRSM64_STREAM / 2];
+    __shared__ __attribute__((aligned(16))) double colbuf[2 * 4 * COLB];
+    __shared__ int s_last;
     const int4 t = tasks[blockIdx.x];
     const int s = t.x, k0 = t.y, r0 = t.z;
     const int tid = threadIdx.x;
@@ -755,31 +781,53 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
     const int m = P.sn_m[s];
     const int nb = min(PNB, w - k0);
     double* pan = P.panel_pool + P.panel_off[s];
-    if (nb < PNB) return;  // partial blocks: trsm_partial_kernel
-    const double* blk = pan + (int64_t)k0 * m + k0;
+    if (nb < PNB) return;  // partial blocks: potrf_tiles_kernel + trsm_partial_kernel
+    double* blk = pan + (int64_t)k0 * m + k0;
+    double* Sd = reinterpret_cast<double*>(S);
+    SmallRegs<1> R;
+    small_tiles<1>(R, PNB, PNB);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int i = 4 * R.bi[0] + r, j = 4 * R.bj[0] + c;
+            R.v[0][r * 4 + c] = (R.bi[0] >= 0 && i >= j) ? blk[(int64_t)j * m + i] : 0.0;
+        }
+    small_steps<1>(R, colbuf, PNB, P.info, c0 + k0);  // every block load has returned
+    if (R.bi[0] >= 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int i = 4 * R.bi[0] + r, j = 4 * R.bj[0] + c;
+                if (i >= j) Sd[PNB * j - j * (j - 1) / 2 + (i - j)] = (i == j) ? 1.0 / R.v[0][r * 4 + c] : R.v[0][r * 4 + c];
+            }
+    }
     const int row = r0 + tid;
     // the 64 block columns, m rows each (< 2^31 bytes for m < 4M); dead lanes masked
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pan + (int64_t)k0 * m, (uint32_t)m * PNB * 8u);
     const int voff = row < m ? row * 8 : BUF_DEAD;
-    double* Sd = reinterpret_cast<double*>(S);
-    {  // stage L11: all loads in flight first (lane q of column j), then the stream
-        constexpr int PER = PNB * PNB / TRSM_ROWS;
-        double v[PER];
-#pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int e = tid + TRSM_ROWS * k, j = e / PNB, q = e % PNB;
-            v[k] = q >= j ? blk[(int64_t)j * m + q] : 0.0;
-        }
-#pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int e = tid + TRSM_ROWS * k, j = e / PNB, q = e % PNB;
-            if (q >= j) Sd[PNB * j - j * (j - 1) / 2 + (q - j)] = (q == j) ? 1.0 / v[k] : v[k];
-        }
-    }
-    __syncthreads();
     double r[PNB];
 #pragma unroll
     for (int c = 0; c < PNB; ++c) r[c] = buf_ld(rs, voff, c * m * 8);
+    __syncthreads();
+    if (tid == 0) {
+        const int k1 = k0 + PNB;
+        const int nwg = (max(m, k1 + 1) - k1 + TRSM_ROWS - 1) / TRSM_ROWS;
+        const int old = __hip_atomic_fetch_add(arrive + (t.w - 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == nwg - 1;
+        if (old == nwg - 1) __hip_atomic_store(arrive + (t.w - 1), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (s_last && R.bi[0] >= 0) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int i = 4 * R.bi[0] + rr, j = 4 * R.bj[0] + c;
+                if (i >= j) blk[(int64_t)j * m + i] = R.v[0][rr * 4 + c];
+            }
+    }
     trsm64_full(r, S);
 #pragma unroll
     for (int c = 0; c < PNB; ++c) buf_st(r[c], rs, voff, c * m * 8);
@@ -954,16 +1002,17 @@ hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count,
 
 hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hipStream_t st) {
     if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(potrf_diag_g_kernel, dim3(count), dim3(64), 0, st, P, tasks);
+    hipLaunchKernelGGL(potrf_tiles_kernel, dim3(count), dim3(256), 0, st, P, tasks);
     return hipGetLastError();
 }
 
-hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st, bool partial) {
+hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st, bool partial,
+                             int32_t* arrive) {
     if (count <= 0) return hipSuccess;
     if (partial)
         hipLaunchKernelGGL(trsm_partial_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks, TRSM_ROWS);
     else
-        hipLaunchKernelGGL(trsm_panel_g_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks);
+        hipLaunchKernelGGL(trsm_panel_g_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks, arrive);
     return hipGetLastError();
 }
 

@@ -15,7 +15,7 @@ constexpr int TRSM_ROWS = 256;
 // Columns owned by one assembly workgroup (one wave per column at a time).
 constexpr int ASM_COLS = 16;
 constexpr int ASM_ROWS = 256;  // rows per LDS tile of the write-once assembly
-constexpr int ASM_TILE_MIN_M = 8192;  // fronts at least this tall use the write-once tile kernel
+constexpr int ASM_TILE_MIN_M = 512;   // fronts at least this tall use the write-once tile kernel
 // Output tile edges of the MFMA SYRK kernel (per launch).
 constexpr int SYRK_BT_SMALL = 64;
 constexpr int SYRK_BT_LARGE = 128;
@@ -36,6 +36,8 @@ struct DevPlan {
     const int32_t* relind;
     const int64_t* rb_ptr;      // ns+1
     const int32_t* rel_bnd;     // per child: CB row bounds of the parent's ASM_ROWS row tiles
+    const int64_t* cbk_ptr;     // ns+1
+    const int32_t* col_bnd;     // per child: CB row bounds of the parent's ASM_COLS column blocks
     const int64_t* a_ptr;       // n+1 (internal columns)
     const int32_t* a_pos;       // row position in the column's front
     const int64_t* a_src;       // index into the input value array
@@ -153,7 +155,10 @@ hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count,
 // 64 x 64 diagonal POTRF (one wave per block) and the TRSM of the rows below it
 // (TRSM_ROWS rows per task).  partial: every task is a partial last block (nb < 64).
 hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hipStream_t st);
-hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st, bool partial = false);
+// partial: blocks with nb < 64; else full blocks with the POTRF fused (arrive: the
+// per-block arrival counters, zeroed; task .w - 1 indexes them)
+hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st, bool partial,
+                             int32_t* arrive);
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st);
 hipError_t launch_stamp(uint64_t* slot, hipStream_t st);
 hipError_t launch_fill_random(double* p, int64_t n, hipStream_t st);

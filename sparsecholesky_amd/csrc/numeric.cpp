@@ -488,9 +488,14 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 if (w <= k0) continue;
                 const int nb = std::min(PNB, w - k0);
                 const int k1 = k0 + nb;
-                potrf.push_back(make_int2(s, k0));
-                for (int r0 = k1; r0 < m; r0 += TRSM_ROWS)
-                    (nb < PNB ? trsm_part : trsm).push_back(make_int4(s, k0, r0, 0));
+                if (nb < PNB) {
+                    potrf.push_back(make_int2(s, k0));
+                    for (int r0 = k1; r0 < m; r0 += TRSM_ROWS) trsm_part.push_back(make_int4(s, k0, r0, 0));
+                } else {  // fused POTRF (one task if no rows below); .w - 1: arrival counter
+                    const int ctr = (int)trsm.size() + 1;
+                    for (int r0 = k1; r0 < std::max(m, k1 + 1); r0 += TRSM_ROWS)
+                        trsm.push_back(make_int4(s, k0, r0, ctr));
+                }
                 double* pan = panel_pool + poff[s];
                 const int slab0 = (k0 / NBO) * NBO;
                 const int slab1 = std::min(w, slab0 + NBO);
@@ -668,15 +673,19 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     Lp.vr = vk;
                     Lp.off = (int64_t)potrf.size();
                     Lp.count = 1;
-                    potrf.push_back(make_int2(s, k0));
-                    N.sched.push_back(Lp);
+                    if (nb < PNB) {  // full blocks: POTRF fused into the TRSM
+                        potrf.push_back(make_int2(s, k0));
+                        N.sched.push_back(Lp);
+                    }
                     Launch Lt {};
                     Lt.kind = L_TRSM;
                     Lt.level = lev;
                     Lt.vr = vk;
                     Lt.off = (int64_t)trsm.size();
                     Lt.big = nb < PNB ? 1 : 0;
-                    for (int r0 = k1; r0 < m; r0 += TRSM_ROWS) trsm.push_back(make_int4(s, k0, r0, 0));
+                    const int ctr = nb < PNB ? 0 : (int)trsm.size() + 1;  // fused POTRF: arrival counter
+                    for (int r0 = k1; r0 < (nb < PNB ? m : std::max(m, k1 + 1)); r0 += TRSM_ROWS)
+                        trsm.push_back(make_int4(s, k0, r0, ctr));
                     Lt.count = (int32_t)((int64_t)trsm.size() - Lt.off);
                     if (Lt.count > 0) N.sched.push_back(Lt);
                     if (k1 < k1s) {
@@ -989,6 +998,7 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     const int32_t ns = S.ns;
     int64_t rc;
     static_assert(ASM_ROWS == kAsmRows, "assembly row tile");
+    static_assert(ASM_COLS == kAsmCols, "assembly column block");
     for (int32_t s = 0; s < S.ns; ++s)
         if (S.sn_m[s] >= (1 << 20)) {  // assembly task encoding: 16-bit column block index
             N.err = "front with >= 2^20 rows is not supported";
@@ -1010,12 +1020,13 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     panel_layout(N, S, multi ? N.nranks : 1);
     // ---- shared plan arrays ----
     DevPlan P0 {};
-    int32_t *d_sn_start, *d_sn_m, *d_child_ptr, *d_child_list, *d_relind, *d_apos, *d_relbnd;
-    int64_t *d_rel_ptr, *d_aptr, *d_asrc, *d_rbptr;
+    int32_t *d_sn_start, *d_sn_m, *d_child_ptr, *d_child_list, *d_relind, *d_apos, *d_relbnd, *d_colbnd;
+    int64_t *d_rel_ptr, *d_aptr, *d_asrc, *d_rbptr, *d_cbkptr;
     if ((rc = upload(N, S.sn_start, d_sn_start)) || (rc = upload(N, S.sn_m, d_sn_m)) ||
         (rc = upload(N, S.child_ptr, d_child_ptr)) || (rc = upload(N, S.child_list, d_child_list)) ||
         (rc = upload(N, S.rel_ptr, d_rel_ptr)) || (rc = upload(N, S.relind, d_relind)) ||
         (rc = upload(N, S.rb_ptr, d_rbptr)) || (rc = upload(N, S.rel_bnd, d_relbnd)) ||
+        (rc = upload(N, S.cbk_ptr, d_cbkptr)) || (rc = upload(N, S.col_bnd, d_colbnd)) ||
         (rc = upload(N, S.a_ptr, d_aptr)) || (rc = upload(N, S.a_pos, d_apos)) ||
         (rc = upload(N, S.a_src, d_asrc)) || (rc = upload(N, N.gpo, N.d_gpo)))
         return fail(rc);
@@ -1027,6 +1038,8 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     P0.relind = d_relind;
     P0.rb_ptr = d_rbptr;
     P0.rel_bnd = d_relbnd;
+    P0.cbk_ptr = d_cbkptr;
+    P0.col_bnd = d_colbnd;
     P0.a_ptr = d_aptr;
     P0.a_pos = d_apos;
     P0.a_src = d_asrc;
@@ -1115,6 +1128,7 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     }
     if ((rc = upload(N, B.small, N.d_small)) || (rc = upload(N, B.asmv, N.d_asm)) ||
         (rc = upload(N, B.potrf, N.d_potrf)) || (rc = upload(N, B.trsm, N.d_trsm)) ||
+        (rc = upload(N, std::vector<int32_t>(B.trsm.size() + 1, 0), N.d_arrive)) ||
         (rc = upload(N, B.gemm, N.d_gemm)) || (rc = upload(N, B.tiles, N.d_tiles)))
         return fail(rc);
     (void)ns;
@@ -1145,7 +1159,7 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
         case L_POTRF:
             return launch_potrf_diag(N.R[L.vr].P, N.d_potrf + L.off, L.count, N.stream);
         case L_TRSM:
-            return launch_trsm_panel(N.R[L.vr].P, N.d_trsm + L.off, L.count, N.stream, L.big != 0);
+            return launch_trsm_panel(N.R[L.vr].P, N.d_trsm + L.off, L.count, N.stream, L.big != 0, N.d_arrive);
         case L_PANEL:
         case L_CB:
             return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st);
@@ -1670,7 +1684,7 @@ int64_t debug_syrk(double* dC, int ldc, const double* dA, int lda, int M, int Nn
 }
 
 // Panel-kernel microbenchmarks on one synthetic front (m = M rows, w = 64):
-// which 2 = POTRF (us per launch), 3 = TRSM (us per launch).
+// which 2 = POTRF (us per launch), 3 = TRSM with the fused POTRF (us per launch).
 static int64_t bench_panel(int which, int M, int reps, double* out) {
     const int w = PNB;
     if (M < w || reps < 1) return SC_ERR_ARG;
@@ -1688,16 +1702,17 @@ static int64_t bench_panel(int which, int M, int reps, double* out) {
     int32_t hs[2] = {0, w}, hm[1] = {M};
     int64_t ho[2] = {0, (int64_t)nel};
     std::vector<int4> tr;
-    for (int r0 = w; r0 < M; r0 += TRSM_ROWS) tr.push_back(make_int4(0, 0, r0, 0));
+    for (int r0 = w; r0 < M; r0 += TRSM_ROWS) tr.push_back(make_int4(0, 0, r0, 1));
     int2 pt = make_int2(0, 0);
     void *d_pan = nullptr, *d_ref = nullptr, *d_s = nullptr, *d_m = nullptr, *d_o = nullptr, *d_info = nullptr,
-         *d_pt = nullptr, *d_tr = nullptr;
+         *d_pt = nullptr, *d_tr = nullptr, *d_arr = nullptr;
     const size_t bytes = (nel + PNB) * sizeof(double);
     int64_t rc = SC_OK;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (hipMalloc(&d_pan, bytes) || hipMalloc(&d_ref, bytes) || hipMalloc(&d_s, 8) || hipMalloc(&d_m, 4) ||
         hipMalloc(&d_o, 16) || hipMalloc(&d_info, 4) || hipMalloc(&d_pt, 8) ||
-        hipMalloc(&d_tr, std::max<size_t>(1, tr.size()) * sizeof(int4)) || hipEventCreate(&e0) ||
+        hipMalloc(&d_tr, std::max<size_t>(1, tr.size()) * sizeof(int4)) || hipMalloc(&d_arr, 4) ||
+        hipMemset(d_arr, 0, 4) || hipEventCreate(&e0) ||
         hipEventCreate(&e1)) {
         rc = SC_ERR_DEVMEM;
     } else {
@@ -1724,7 +1739,7 @@ static int64_t bench_panel(int which, int M, int reps, double* out) {
             if (which == 2)
                 (void)launch_potrf_diag(P, (const int2*)d_pt, 1, nullptr);
             else
-                (void)launch_trsm_panel(P, (const int4*)d_tr, nt, nullptr);
+                (void)launch_trsm_panel(P, (const int4*)d_tr, nt, nullptr, false, (int32_t*)d_arr);
             (void)hipEventRecord(e1, nullptr);
             (void)hipEventSynchronize(e1);
             float ms = 0.f;
@@ -1734,7 +1749,7 @@ static int64_t bench_panel(int which, int M, int reps, double* out) {
         *out = 1e3 * tot / reps;
         if (hipGetLastError() != hipSuccess) rc = SC_ERR_HIP;
     }
-    for (void* p : {d_pan, d_ref, d_s, d_m, d_o, d_info, d_pt, d_tr})
+    for (void* p : {d_pan, d_ref, d_s, d_m, d_o, d_info, d_pt, d_tr, d_arr})
         if (p) (void)hipFree(p);
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);

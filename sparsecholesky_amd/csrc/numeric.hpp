@@ -181,6 +181,7 @@ struct Numeric {
     int2* d_asm = nullptr;
     int2* d_potrf = nullptr;
     int4* d_trsm = nullptr;
+    int32_t* d_arrive = nullptr;  // fused POTRF + TRSM: per-block arrival counters
     GemmTask* d_gemm = nullptr;
     int2* d_tiles = nullptr;
     int32_t* d_info = nullptr;       // shared by the hosted ranks' DevPlans

@@ -413,6 +413,21 @@ i64 analyze(i64 n, const i64* Ap, const i32* Ai, const sc_options& opt, Symbolic
         }
         S.rb_ptr[s + 1] = (i64)S.rel_bnd.size();
     }
+    // per child, the CB rows of each ASM_COLS-column block of its parent (the large-front
+    // assembly kernels read them instead of binary-searching relind)
+    S.cbk_ptr.assign((size_t)ns + 1, 0);
+    S.col_bnd.clear();
+    for (i32 s = 0; s < ns; ++s) {
+        const i32 p = S.sn_parent[s];
+        if (p >= 0) {
+            const i32 nb = (S.sn_m[p] + kAsmCols - 1) / kAsmCols;
+            const i32* rel = S.relind.data() + S.rel_ptr[s];
+            const i32 mbc = (i32)(S.rel_ptr[s + 1] - S.rel_ptr[s]);
+            for (i32 b = 0; b <= nb; ++b)
+                S.col_bnd.push_back((i32)(std::lower_bound(rel, rel + mbc, b * kAsmCols) - rel));
+        }
+        S.cbk_ptr[s + 1] = (i64)S.col_bnd.size();
+    }
     S.child_ptr.assign((size_t)ns + 1, 0);
     S.child_list.clear();
     for (i32 s = 0; s < ns; ++s) {

@@ -39,6 +39,7 @@ i64 etree_depth(i64 n, const i32* parent);
 enum FrontClass : int32_t { FRONT_SMALL = 0, FRONT_LARGE = 1 };
 
 constexpr int kAsmRows = 256;  // row tile of the large-front assembly (kernels.hpp ASM_ROWS)
+constexpr int kAsmCols = 16;   // column block of the large-front assembly (kernels.hpp ASM_COLS)
 
 struct Symbolic {
     sc_options opt {};
@@ -75,6 +76,8 @@ struct Symbolic {
     // k = 0 .. ceil(m_parent / kAsmRows) (the assembly's row tiles)
     std::vector<i64> rb_ptr;     // ns+1
     std::vector<i32> rel_bnd;
+    std::vector<i64> cbk_ptr;    // ns+1
+    std::vector<i32> col_bnd;    // per child: CB rows of the parent's kAsmCols-column blocks
     std::vector<i64> panel_off;  // ns+1 (doubles), L panel m x w, ld = m
     std::vector<i64> cb_off;     // ns+1 (doubles), CB mb x mb, ld = mb
     std::vector<i64> a_ptr;      // n+1: A entries grouped by internal column (lower part)
