@@ -71,7 +71,7 @@ def cb_syrk_traffic():
     """HBM bytes per CB SYRK launch from the committed PMC profile
     (scripts/gpu_pmc.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE
     doubled per the gfx950 note); None when the profile is absent."""
-    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01", "pmc_summary.json")
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r02", "pmc_summary.json")
     try:
         with open(p) as f:
             cb = json.load(f)["cb_syrk_128"]
@@ -79,7 +79,7 @@ def cb_syrk_traffic():
         return None, None
     b = cb["fetch_bytes_per_launch"] + cb["write_bytes_per_launch"]
     return round(b), ("bytes per syrk_mfma_kernel<128,2,4,1> launch (FETCH_SIZE x2 + WRITE_SIZE), "
-                      "profiles/r01/pmc_summary.json; L2-miss bytes incl. Infinity-Cache hits")
+                      "profiles/r02/pmc_summary.json; L2-miss bytes incl. Infinity-Cache hits")
 
 
 def cb_syrk_mfma_counters():
