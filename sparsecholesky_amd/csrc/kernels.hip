@@ -1179,39 +1179,100 @@ __global__ __launch_bounds__(64) void solve_inv_kernel(SolvePlan P, const int2* 
         if (lane < c && c < nb) blk[(int64_t)c * m + lane] = r[c];
 }
 
-// y = X c_blk for the block at pan (column-major, ld m).  X is staged through LDS
-// with coalesced loads (column i of the panel block holds X(i, 0..i-1) in rows
-// 0..i-1: Xs[i][k]), the diagonal as 1 / L(i, i); then thread (row i = tid & 63,
-// quarter g) sums k in [16 g, 16 g + 16).  vb receives y.  256 threads.
-__device__ __forceinline__ void inv_apply(const double* __restrict__ pan, int64_t m, int nb, const double* cb,
-                                          double* vb, double (*part)[PNB], double (*Xs)[PNB + 1]) {
+// Off-diagonal quadrant of the 128-column block inverse: for the block at blk
+// (columns k0 .. k0 + nb, 64 < nb <= 128), X128 = [Xa 0; E Xb] with Xa, Xb the 64-block
+// inverses (solve_inv_kernel) and E = -Xb B Xa, B = L(k0+64 .., k0 .. k0+64).  E(i, k)
+// goes to row k, column 64 + i of the block -- its unused upper triangle, like Xa and
+// Xb -- so X128(i, k) sits at (row k, column i) for every k < i.  256 threads, once per
+// factorization.
+__global__ __launch_bounds__(256) void solve_inv2_kernel(SolvePlan P, const int2* __restrict__ tasks) {
+    __shared__ double Xa[PNB][PNB + 1], Bm[PNB][PNB + 1], Xb[PNB][PNB + 1];
+    const int2 t = tasks[blockIdx.x];
+    const int s = t.x, k0 = t.y;
     const int tid = threadIdx.x;
+    const int c0 = P.sn_start[s];
+    const int w = P.sn_start[s + 1] - c0;
+    const int m = P.sn_m[s];
+    const int nbb = min(SOLVE_NB, w - k0) - PNB;  // > 0
+    double* blk = const_cast<double*>(P.panel_pool) + P.panel_off[s] + (int64_t)k0 * m + k0;
+    const double* blkb = blk + (int64_t)PNB * m + PNB;
 #pragma unroll
     for (int q = 0; q < PNB * PNB / 256; ++q) {
         const int e = tid + 256 * q, i = e >> 6, k = e & 63;  // lanes along k: coalesced in column i
-        double v = 0.0;
-        if (i < nb && k <= i) {
-            v = pan[(int64_t)i * m + k];
-            if (k == i) v = 1.0 / v;
-        }
-        Xs[i][k] = v;
+        Xa[i][k] = k < i ? blk[(int64_t)i * m + k] : (k == i ? 1.0 / blk[(int64_t)i * m + i] : 0.0);
+        Xb[i][k] = (i < nbb && k < i) ? blkb[(int64_t)i * m + k] : ((i < nbb && k == i) ? 1.0 / blkb[(int64_t)i * m + i] : 0.0);
+        Bm[k][i] = k < nbb ? blk[(int64_t)i * m + PNB + k] : 0.0;  // B(k, i) = L(k0 + 64 + k, k0 + i)
+    }
+    __syncthreads();
+    // thread: row i = tid >> 2, columns j = (tid & 3) + 4 q
+    const int i = tid >> 2, jg = tid & 3;
+    double acc[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.0;
+    for (int k = 0; k < PNB; ++k) {
+        const double bik = Bm[i][k];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] = fma(bik, Xa[k][jg + 4 * q], acc[q]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) Bm[i][jg + 4 * q] = acc[q];  // T = B Xa
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.0;
+    for (int k = 0; k <= i; ++k) {
+        const double xik = Xb[i][k];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] = fma(xik, Bm[k][jg + 4 * q], acc[q]);
+    }
+    if (i < nbb) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) blk[(int64_t)(PNB + i) * m + jg + 4 * q] = -acc[q];
+    }
+}
+
+// out[i] (+)= sum_k X128(64 I + i, 64 K + k) cb[64 K + k] for the block at blk (nb
+// columns): the quadrant is staged through LDS with coalesced loads (X128(gi, gk) at
+// row gk, column gi; the diagonal as 1 / L), then thread (row i = tid & 63, quarter
+// g) sums 16 k.  256 threads.
+__device__ __forceinline__ void quad_apply(const double* __restrict__ blk, int64_t m, int nb, int I, int K,
+                                           const double* cb, double* out, bool add, double (*part)[PNB],
+                                           double (*Xs)[PNB + 1]) {
+    const int tid = threadIdx.x;
+    // branch-free: dead elements read 0 through the buffer's range check, all loads in flight
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(blk, (uint32_t)(((int64_t)(nb - 1) * m + nb) * 8));
+    double v[PNB * PNB / 256];
+#pragma unroll
+    for (int q = 0; q < PNB * PNB / 256; ++q) {
+        const int e = tid + 256 * q, i = e >> 6, k = e & 63;  // lanes along k: coalesced in column gi
+        const int gi = PNB * I + i, gk = PNB * K + k;
+        v[q] = buf_ld(rs, (gi < nb && gk <= gi) ? (int)(((int64_t)gi * m + gk) * 8) : BUF_DEAD, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < PNB * PNB / 256; ++q) {
+        const int e = tid + 256 * q, i = e >> 6, k = e & 63;
+        Xs[i][k] = (PNB * I + i == PNB * K + k && PNB * I + i < nb) ? 1.0 / v[q] : v[q];  // dead: 0, not 1/0
     }
     __syncthreads();
     const int i = tid & 63, g = tid >> 6;
     double acc = 0.0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) acc = fma(Xs[i][g * 16 + q], cb[g * 16 + q], acc);
+    for (int q = 0; q < 16; ++q) acc = fma(Xs[i][g * 16 + q], cb[PNB * K + g * 16 + q], acc);
     part[g][i] = acc;
     __syncthreads();
-    if (tid < PNB) vb[tid] = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
+    if (tid < PNB) {
+        const double v = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
+        out[tid] = add ? out[tid] + v : v;
+    }
     __syncthreads();
 }
 
-// Forward step: every workgroup of block (s, k0) forms y = X c_blk and applies its
-// rows [r0, r0 + SOLVE_ROWS) below the block; the writer (t.w = 1) stores y to P.y
-// (not c, which the step's other workgroups still read).  r0 < 0: diagonal only.
+// Forward step (128-column blocks): every workgroup of block (s, k0) forms y = X128
+// c_blk (quadrants Xa, E, Xb) and applies its rows [r0, r0 + SOLVE_ROWS) below the
+// block, c[rows[r]] -= L(r, blk) y; the writer (t.w = 1) stores y to P.y (not c, which
+// the step's other workgroups still read).  r0 < 0: the diagonal block only.
 __global__ __launch_bounds__(SOLVE_ROWS) void solve_fwd_kernel(SolvePlan P, const int4* __restrict__ tasks) {
-    __shared__ double vb[PNB], cb[PNB];
+    __shared__ double vb[SOLVE_NB], cb[SOLVE_NB];
     __shared__ double part[4][PNB];
     __shared__ double Xs[PNB][PNB + 1];
     const int4 t = tasks[blockIdx.x];
@@ -1220,31 +1281,44 @@ __global__ __launch_bounds__(SOLVE_ROWS) void solve_fwd_kernel(SolvePlan P, cons
     const int c0 = P.sn_start[s];
     const int w = P.sn_start[s + 1] - c0;
     const int m = P.sn_m[s];
-    const int nb = min(PNB, w - k0);
+    const int nb = min(SOLVE_NB, w - k0);
     const double* __restrict__ pan = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m;
-    // this thread's row below the block: its 64 loads go out first, overlapping y = X c
+    // this thread's row below the block: its first 64 loads go out first, overlapping y
     const int r = r0 + tid;
     const bool live = r0 >= 0 && r < m;
+    // the block's columns; the whole offset in the VGPR so the range check masks dead
+    // rows and columns past nb
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pan, (uint32_t)((int64_t)nb * m * 8));
     double v[PNB];
 #pragma unroll
-    for (int q = 0; q < PNB; ++q) v[q] = (live && q < nb) ? pan[(int64_t)q * m + r] : 0.0;
-    if (tid < PNB) cb[tid] = tid < nb ? P.c[c0 + k0 + tid] : 0.0;
+    for (int q = 0; q < PNB; ++q) v[q] = buf_ld(rs, (live && q < nb) ? (q * m + r) * 8 : BUF_DEAD, 0);
+    if (tid < SOLVE_NB) cb[tid] = tid < nb ? P.c[c0 + k0 + tid] : 0.0;
     __syncthreads();
-    inv_apply(pan + k0, m, nb, cb, vb, part, Xs);
+    quad_apply(pan + k0, m, nb, 0, 0, cb, vb, false, part, Xs);
+    if (nb > PNB) {
+        quad_apply(pan + k0, m, nb, 1, 0, cb, vb + PNB, false, part, Xs);
+        quad_apply(pan + k0, m, nb, 1, 1, cb, vb + PNB, true, part, Xs);
+    }
     if (t.w && tid < nb) P.y[c0 + k0 + tid] = vb[tid];
     if (r0 < 0) return;
     const int32_t* __restrict__ rows = P.rows + P.rows_ptr[s];
     double acc = 0.0;
 #pragma unroll
     for (int q = 0; q < PNB; ++q) acc = fma(v[q], vb[q], acc);
+    if (nb > PNB) {
+#pragma unroll
+        for (int q = 0; q < PNB; ++q) v[q] = buf_ld(rs, (live && PNB + q < nb) ? ((PNB + q) * m + r) * 8 : BUF_DEAD, 0);
+#pragma unroll
+        for (int q = 0; q < PNB; ++q) acc = fma(v[q], vb[PNB + q], acc);
+    }
     if (live) unsafeAtomicAdd(P.c + rows[r], -acc);
 }
 
 // Backward step, part 1: workgroup (s, k0, r0) adds -L(rows, blk)^T x(rows) into
-// c_blk for rows [r0, r0 + SOLVE_ROWS) below the block (fp64 atomics).  Thread t
-// owns row r0 + t: it loads its 64 entries (coalesced per column, all in flight),
-// scales them by x of its row and leaves them in LDS; then thread (column j, quarter
-// g) sums a quarter of column j.
+// c_blk for rows [r0, r0 + SOLVE_ROWS) below the 128-column block (fp64 atomics), in
+// two 64-column halves.  Thread t owns row r0 + t: it loads its 64 entries of the half
+// (coalesced per column, all in flight), scales them by x of its row and leaves them
+// in LDS; then thread (column j, quarter g) sums a quarter of column j.
 __global__ __launch_bounds__(SOLVE_ROWS) void solve_gemv_kernel(SolvePlan P, const int4* __restrict__ tasks) {
     __shared__ double T[PNB][SOLVE_ROWS + 1];     // T[j][row] = L(row, j) x(row)
     __shared__ double part[SOLVE_ROWS / 64][PNB];
@@ -1254,56 +1328,69 @@ __global__ __launch_bounds__(SOLVE_ROWS) void solve_gemv_kernel(SolvePlan P, con
     const int c0 = P.sn_start[s];
     const int w = P.sn_start[s + 1] - c0;
     const int m = P.sn_m[s];
-    const int nb = min(PNB, w - k0);
+    const int nb = min(SOLVE_NB, w - k0);
     const double* __restrict__ pan = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m;
     const int32_t* __restrict__ rows = P.rows + P.rows_ptr[s];
     const int r = r0 + tid;
     const bool live = r < m;
     const double xr = live ? P.c[rows[r]] : 0.0;
+    // the block's columns; the whole offset in the VGPR (range check masks dead rows / columns)
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pan, (uint32_t)((int64_t)nb * m * 8));
+    for (int h = 0; h * PNB < nb; ++h) {
+        if (h) __syncthreads();  // the previous half's T fully read
+        double v[PNB];
 #pragma unroll
-    for (int jc = 0; jc < PNB; jc += 16) {
-        double v[16];
+        for (int q = 0; q < PNB; ++q) {
+            const int col = h * PNB + q;
+            v[q] = buf_ld(rs, (live && col < nb) ? (col * m + r) * 8 : BUF_DEAD, 0);
+        }
 #pragma unroll
-        for (int q = 0; q < 16; ++q) v[q] = (live && jc + q < nb) ? pan[(int64_t)(jc + q) * m + r] : 0.0;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) T[jc + q][tid] = v[q] * xr;
-    }
-    __syncthreads();
-    const int j = tid & 63, g = tid >> 6;
-    double acc = 0.0;
+        for (int q = 0; q < PNB; ++q) T[q][tid] = v[q] * xr;
+        __syncthreads();
+        const int j = tid & 63, g = tid >> 6;
+        double acc = 0.0;
 #pragma unroll 8
-    for (int q = 0; q < SOLVE_ROWS / 4; ++q) acc += T[j][g * (SOLVE_ROWS / 4) + q];
-    part[g][j] = acc;
-    __syncthreads();
-    if (tid < nb) unsafeAtomicAdd(P.c + c0 + k0 + tid, -(part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid]));
+        for (int q = 0; q < SOLVE_ROWS / 4; ++q) acc += T[j][g * (SOLVE_ROWS / 4) + q];
+        part[g][j] = acc;
+        __syncthreads();
+        if (tid < PNB && h * PNB + tid < nb)
+            unsafeAtomicAdd(P.c + c0 + k0 + h * PNB + tid, -(part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid]));
+    }
 }
 
-// Backward step, part 2: x_blk = X^T c_blk for every block (s, k0) of the step:
-// thread (column k = tid & 63, quarter g) sums X(i, k) c_i over i in its quarter.
+// Backward step, part 2: x_blk = X128^T c_blk for every block (s, k0) of the step:
+// thread (column k = tid & 127, half g) sums X128(i, k) c_i over i in its half
+// (X128(i, k) at row k, column i of the block: lanes along k read coalesced).
 __global__ __launch_bounds__(256) void solve_diag_kernel(SolvePlan P, const int2* __restrict__ tasks) {
-    __shared__ double cb[PNB];
-    __shared__ double part[4][PNB];
+    __shared__ double cb[SOLVE_NB];
+    __shared__ double part[2][SOLVE_NB];
     const int2 t = tasks[blockIdx.x];
     const int s = t.x, k0 = t.y;
-    const int tid = threadIdx.x, k = tid & 63, g = tid >> 6;
+    const int tid = threadIdx.x, k = tid & (SOLVE_NB - 1), g = tid >> 7;
     const int c0 = P.sn_start[s];
     const int w = P.sn_start[s + 1] - c0;
     const int m = P.sn_m[s];
-    const int nb = min(PNB, w - k0);
+    const int nb = min(SOLVE_NB, w - k0);
     const double* __restrict__ blk = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m + k0;
-    if (tid < PNB) cb[tid] = tid < nb ? P.c[c0 + k0 + tid] : 0.0;
+    if (tid < SOLVE_NB) cb[tid] = tid < nb ? P.c[c0 + k0 + tid] : 0.0;
     __syncthreads();
+    // branch-free: dead elements read 0 through the buffer's range check, all loads in flight
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(blk, (uint32_t)(((int64_t)(nb - 1) * m + nb) * 8));
+    double xv[PNB];
+#pragma unroll
+    for (int q = 0; q < PNB; ++q) {
+        const int i = g * PNB + q;
+        xv[q] = buf_ld(rs, (i < nb && k <= i) ? (int)(((int64_t)i * m + k) * 8) : BUF_DEAD, 0);
+    }
     double acc = 0.0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int i = g * 16 + q;
-        double xik = 0.0;  // X(i, k), i >= k: row k, column i of the block (lanes along k: coalesced)
-        if (i < nb && k <= i) xik = k < i ? blk[(int64_t)i * m + k] : 1.0 / blk[(int64_t)i * m + i];
-        acc = fma(xik, cb[i], acc);
+    for (int q = 0; q < PNB; ++q) {
+        const int i = g * PNB + q;
+        acc = fma((k == i && i < nb) ? 1.0 / xv[q] : xv[q], cb[i], acc);  // dead: 0, not 1/0
     }
     part[g][k] = acc;
     __syncthreads();
-    if (tid < nb) P.c[c0 + k0 + tid] = part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid];
+    if (tid < nb) P.c[c0 + k0 + tid] = part[0][tid] + part[1][tid];
 }
 
 hipError_t launch_solve_fwd(const SolvePlan& P, const int4* tasks, int count, hipStream_t st) {
@@ -1324,9 +1411,10 @@ hipError_t launch_solve_diag(const SolvePlan& P, const int2* tasks, int count, h
     return hipGetLastError();
 }
 
-hipError_t launch_solve_inv(const SolvePlan& P, const int2* tasks, int count, hipStream_t st) {
-    if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(solve_inv_kernel, dim3(count), dim3(64), 0, st, P, tasks);
+hipError_t launch_solve_inv(const SolvePlan& P, const int2* tasks, int count, const int2* tasks2, int count2,
+                            hipStream_t st) {
+    if (count > 0) hipLaunchKernelGGL(solve_inv_kernel, dim3(count), dim3(64), 0, st, P, tasks);
+    if (count2 > 0) hipLaunchKernelGGL(solve_inv2_kernel, dim3(count2), dim3(256), 0, st, P, tasks2);
     return hipGetLastError();
 }
 

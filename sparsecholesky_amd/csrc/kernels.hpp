@@ -79,16 +79,19 @@ struct SolvePlan {
     double* y;                // forward result (fused steps write here; copied to c after the sweep)
 };
 constexpr int SOLVE_ROWS = 256;  // front rows per GEMV workgroup
-// X = inv(L11) of the 64 x 64 diagonal blocks (s, k0) into their strict upper
-// triangles (the factor's lower part is untouched); once per factorization, before
-// the first solve.
-hipError_t launch_solve_inv(const SolvePlan& P, const int2* tasks, int count, hipStream_t st);
-// Forward step: tasks (s, k0, r0, writer); every workgroup forms y = X c_blk and
-// applies c[rows[r]] -= L[r, blk] y for its SOLVE_ROWS rows (fp64 atomics: fronts of
-// a level share ancestors); r0 < 0 = the diagonal block only.
+constexpr int SOLVE_NB = 128;    // columns per solve step (two 64-blocks)
+// X = inv(L11) of the 64 x 64 diagonal blocks (s, k0) (tasks) into their strict upper
+// triangles, then (tasks2: 128-column blocks wider than 64) the off-diagonal quadrant
+// E = -Xb B Xa of the 128-block inverse into the block's upper-right square; the
+// factor's lower part is untouched.  Once per factorization, before the first solve.
+hipError_t launch_solve_inv(const SolvePlan& P, const int2* tasks, int count, const int2* tasks2, int count2,
+                            hipStream_t st);
+// Forward step: tasks (s, k0, r0, writer) of 128-column blocks; every workgroup forms
+// y = X128 c_blk and applies c[rows[r]] -= L[r, blk] y for its SOLVE_ROWS rows (fp64
+// atomics: fronts of a level share ancestors); r0 < 0 = the diagonal block only.
 hipError_t launch_solve_fwd(const SolvePlan& P, const int4* tasks, int count, hipStream_t st);
 // Backward step: tasks (s, k0, r0): c_blk -= L[rows, blk]^T x[rows] (fp64 atomics),
-// then tasks (s, k0): x_blk = X^T c_blk.
+// then tasks (s, k0): x_blk = X128^T c_blk.
 hipError_t launch_solve_gemv(const SolvePlan& P, const int4* tasks, int count, hipStream_t st);
 hipError_t launch_solve_diag(const SolvePlan& P, const int2* tasks, int count, hipStream_t st);
 // c[i] = b[perm[i]] (gather) or x[perm[i]] = c[i] (scatter)

@@ -1477,7 +1477,7 @@ static int64_t solve_build(Numeric& N) {
     const Symbolic& S = *N.S;
     std::vector<std::vector<int32_t>> by_level((size_t)S.nlevels);
     for (int32_t s = 0; s < S.ns; ++s) by_level[S.level[s]].push_back(s);
-    std::vector<int2> diag;
+    std::vector<int2> diag, inv64, inv128;
     std::vector<int4> bwd, fwd;
     // internal index -> index in the caller's order (postorder, then the fill-reducing
     // permutation when one is in effect)
@@ -1487,7 +1487,7 @@ static int64_t solve_build(Numeric& N) {
     for (int32_t lev = 0; lev < S.nlevels; ++lev) {
         int maxw = 0;
         for (int32_t s : by_level[lev]) maxw = std::max(maxw, S.w(s));
-        for (int k0 = 0; k0 < maxw; k0 += PNB) {
+        for (int k0 = 0; k0 < maxw; k0 += SOLVE_NB) {
             Numeric::SolveStep st {};
             st.doff = (int64_t)diag.size();
             st.goff = (int64_t)bwd.size();
@@ -1495,10 +1495,13 @@ static int64_t solve_build(Numeric& N) {
             for (int32_t s : by_level[lev]) {
                 const int w = S.w(s), m = S.sn_m[s];
                 if (w <= k0) continue;
-                const int slot = (int)diag.size();
                 diag.push_back(make_int2(s, k0));
-                const int rb = std::min(w, k0 + PNB);
-                (void)slot;
+                inv64.push_back(make_int2(s, k0));
+                if (w > k0 + PNB) {
+                    inv64.push_back(make_int2(s, k0 + PNB));
+                    inv128.push_back(make_int2(s, k0));
+                }
+                const int rb = std::min(w, k0 + SOLVE_NB);
                 if (rb >= m) fwd.push_back(make_int4(s, k0, -1, 1));
                 for (int r0 = rb; r0 < m; r0 += SOLVE_ROWS) {
                     bwd.push_back(make_int4(s, k0, r0, 0));
@@ -1514,8 +1517,10 @@ static int64_t solve_build(Numeric& N) {
     int64_t rc;
     int32_t* d_rows = nullptr;
     int64_t* d_rows_ptr = nullptr;
-    N.n_sdiag = (int32_t)diag.size();
-    if ((rc = upload(N, diag, N.d_sdiag)) || (rc = upload(N, bwd, N.d_sgemv)) || (rc = upload(N, fwd, N.d_sfwd)) ||
+    N.n_sinv = (int32_t)inv64.size();
+    N.n_sinv2 = (int32_t)inv128.size();
+    if ((rc = upload(N, diag, N.d_sdiag)) || (rc = upload(N, inv64, N.d_sinv)) || (rc = upload(N, inv128, N.d_sinv2)) ||
+        (rc = upload(N, bwd, N.d_sgemv)) || (rc = upload(N, fwd, N.d_sfwd)) ||
         (rc = upload(N, S.rows, d_rows)) ||
         (rc = upload(N, S.rows_ptr, d_rows_ptr)) || (rc = upload(N, solve_perm, N.d_post)))
         return rc;
@@ -1583,7 +1588,7 @@ int64_t numeric_solve_device(Numeric& N, const double* d_b, double* d_x) {
         HIP_TRY(hipGraphInstantiate(&N.solve_gexec, g, nullptr, nullptr, 0));
     }
     if (N.inv_gen != N.factor_gen) {  // inverses of the diagonal blocks, once per factorization
-        HIP_TRY(launch_solve_inv(N.SP, N.d_sdiag, N.n_sdiag, s0));
+        HIP_TRY(launch_solve_inv(N.SP, N.d_sinv, N.n_sinv, N.d_sinv2, N.n_sinv2, s0));
         N.inv_gen = N.factor_gen;
     }
     const size_t nb = (size_t)n * sizeof(double);

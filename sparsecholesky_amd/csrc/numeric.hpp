@@ -246,8 +246,10 @@ struct Numeric {
     std::vector<SolveStep> solve_steps;  // forward order (levels up, k0 up)
     bool solve_ready = false;
     SolvePlan SP {};
-    int2* d_sdiag = nullptr;         // diagonal blocks (s, k0): inverse preparation
-    int32_t n_sdiag = 0;
+    int2* d_sdiag = nullptr;         // 128-column diagonal blocks (s, k0) of the steps
+    int2* d_sinv = nullptr;          // 64-column blocks (s, k0): inverse preparation
+    int2* d_sinv2 = nullptr;         // 128-column blocks wider than 64: off-diagonal inverse quadrant
+    int32_t n_sinv = 0, n_sinv2 = 0;
     int64_t inv_gen = -1;            // factor_gen whose diagonal-block inverses are in place
     int4* d_sgemv = nullptr;         // backward GEMV tasks (s, k0, r0)
     int4* d_sfwd = nullptr;  // fused forward steps (s, k0, r0, writer)
