@@ -1,0 +1,14 @@
+# Build copies of the package with extra compile flags for A/B runs on the GPU box:
+#   build_variants.sh NAME "FLAGS" [NAME "FLAGS" ...] -> gpurun_var/NAME/{bench.py,sparsecholesky_amd,profiles}
+set -e
+cd "$(dirname "$0")/.."
+while [ $# -ge 2 ]; do
+  name=$1; flags=$2; shift 2
+  d=gpurun_var/$name
+  rm -rf "$d"; mkdir -p "$d/profiles/r02"
+  cp bench.py "$d/"
+  cp profiles/r02/pmc_summary.json profiles/r02/mfma_util.json "$d/profiles/r02/"
+  mkdir -p "$d/sparsecholesky_amd"
+  cp sparsecholesky_amd/__init__.py "$d/sparsecholesky_amd/"
+  make -s -j8 -C sparsecholesky_amd/csrc OBJDIR=build_$name OUT="$PWD/$d/sparsecholesky_amd/libsparsecholesky_amd.so" OPT="-O3 $flags"
+done

@@ -863,6 +863,9 @@ __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask*
     const int lane = tid & 63;
     const int wid = tid >> 6;
     const int wr = wid / WN, wc = wid % WN;
+    // static priority for the second-dispatched half of the waves (the arbitration loser
+    // on every segment of two co-resident waves per SIMD): 547.8-548.5 -> 544.6-546.0 ms
+    if (wid >= WM * WN / 2) __builtin_amdgcn_s_setprio(1);
     const double* __restrict__ A = T.A;
     const int64_t lda = T.lda;
 
