@@ -93,7 +93,7 @@ def cb_syrk_mfma_counters():
     except (OSError, KeyError, ValueError):
         return None
     for name, v in ks.items():
-        if "syrk_mfma_kernel<128, 2, 4, 1>" in name:
+        if "syrk_mfma_kernel<128, 2, 4, 1>" in name or "syrk_mfma_kernel<128, 2, 4, 1, 0>" in name:
             return {"mfma_busy_frac": v["raw_mfma_ratio"], "clock_GHz": v["clock_GHz"],
                     "source": "profiles/r02/mfma_util.json (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE)"}
     return None
@@ -222,8 +222,9 @@ def main():
     phases = None
     if not args.graph:
         phases = [round(x, 3) for x in num.timing().tolist()]
-    # dominant kernel = the CB SYRK instance on 128 x 128 tiles (the dispatches the
-    # rocprofv3 kernel trace lists as syrk_mfma_kernel<128, 2, 4, 1>)
+    # dominant kernel = the CB SYRK instance on 128 x 128 tiles with the trickle epilogue
+    # (the dispatches the rocprofv3 kernel trace lists as syrk_mfma_kernel<128, 2, 4, 1, 0>;
+    # <128, 2, 4, 1> before the epilogue template parameter)
     fl, ms, nl = num.syrk_stats(-2)
     gfl, gms, gnl = num.syrk_stats(256)
     if ms > 0 and nl > 0:
@@ -232,7 +233,7 @@ def main():
         roof = {
             "bound": "mfma", "achieved": round(ach, 3), "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / FP64_MFMA_PEAK_TFLOPS, 4), "traffic": traffic, "traffic_note": tnote,
-            "kernel": "syrk_mfma_kernel<128,2,4,1> (CB update)" + (" on rank 0" if world > 1 else ""),
+            "kernel": "syrk_mfma_kernel<128,2,4,1,0> (CB update)" + (" on rank 0" if world > 1 else ""),
             "flops_per_step": fl, "kernel_ms_per_step": round(ms, 3), "launches_per_step": nl,
             "avg_launch_ms": round(ms / nl, 3),
         }

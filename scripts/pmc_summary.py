@@ -40,7 +40,8 @@ def main():
             "fetch_bytes_per_launch": 2.0 * 1024.0 * sum(f.values()) / nf,
             "write_bytes_per_launch": 1024.0 * sum(w.values()) / nw,
         }
-    cb = [v for k, v in out["kernels"].items() if k.startswith("void sc::syrk_mfma_kernel<128, 2, 4, 1")]
+    cb = [v for k, v in out["kernels"].items() if (k.startswith("void sc::syrk_mfma_kernel<128, 2, 4, 1>") or
+                                                    k.startswith("void sc::syrk_mfma_kernel<128, 2, 4, 1, 0>"))]
     if cb:
         out["cb_syrk_128"] = cb[0]
     print(json.dumps(out, indent=1))

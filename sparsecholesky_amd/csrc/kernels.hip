@@ -842,7 +842,7 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
 // (BK = 8 and 32, and a 4-wave 128 x 128 instance, were measured slower on every
 // shape: DESIGN.md section 5.)
 // ---------------------------------------------------------------------------
-template <int BT, int WM, int WN, int TAG>
+template <int BT, int WM, int WN, int TAG, int EPI>
 __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
                                                                   const int2* __restrict__ tiles) {
     constexpr int NT = 64 * WM * WN;
@@ -948,18 +948,42 @@ __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask*
     const int64_t ldc = T.ldc;
     const __amdgpu_buffer_rsrc_t rc =
         buf_rsrc(C + (int64_t)col0 * ldc, (uint32_t)(min(BT, T.N - col0) * ldc * 8));
+    // EPI = 0: element by element; the compiler may not move a C load above an earlier
+    // C store (same buffer), so each element waits one memory round trip -- a trickle
+    // that leaves the co-resident workgroup's MFMAs undisturbed (deep-K CB updates:
+    // 0.2-1.2 ms per level faster this way).  EPI = 1: two MFMA tile rows per chunk,
+    // every load of a chunk in flight before its stores (short-K launches, where the
+    // epilogue is most of a tile's life: 0.4-0.6 ms per level faster).
+    constexpr int EPI_A = EPI ? (RTM < 2 ? RTM : 2) : 1;
 #pragma unroll
-    for (int a = 0; a < RTM; ++a)
+    for (int a0 = 0; a0 < RTM; a0 += EPI_A) {
+        double cv[EPI_A][RTN][4];
+        int offs[EPI_A][RTN][4];
 #pragma unroll
-        for (int b = 0; b < RTN; ++b)
+        for (int a = 0; a < EPI_A; ++a)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int gi = row0 + wr * (BT / WM) + a * 16 + MFMA_F64_ROW(lane, r);
-                const int gj = col0 + wc * (BT / WN) + b * 16 + (lane & 15);
-                const bool live = gi < T.M && gi >= gj;
-                const int off = live ? (int)((gi + (int64_t)(gj - col0) * ldc) * 8) : BUF_DEAD;
-                buf_st(buf_ld(rc, off, 0) - acc[a][b][r], rc, off, 0);
-            }
+            for (int b = 0; b < RTN; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int gi = row0 + wr * (BT / WM) + (a0 + a) * 16 + MFMA_F64_ROW(lane, r);
+                    const int gj = col0 + wc * (BT / WN) + b * 16 + (lane & 15);
+                    const bool live = gi < T.M && gi >= gj;
+                    offs[a][b][r] = live ? (int)((gi + (int64_t)(gj - col0) * ldc) * 8) : BUF_DEAD;
+                    if constexpr (EPI) {
+                        cv[a][b][r] = buf_ld(rc, offs[a][b][r], 0);
+                    } else {
+                        buf_st(buf_ld(rc, offs[a][b][r], 0) - acc[a0 + a][b][r], rc, offs[a][b][r], 0);
+                    }
+                }
+        if constexpr (EPI) {
+#pragma unroll
+            for (int a = 0; a < EPI_A; ++a)
+#pragma unroll
+                for (int b = 0; b < RTN; ++b)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) buf_st(cv[a][b][r] - acc[a0 + a][b][r], rc, offs[a][b][r], 0);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1025,20 +1049,22 @@ hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hip
 
 // TAG only separates the launches in profiles: 0 = panel update, 1 = CB update.
 // bt = 64: 64x64 tiles on 4 waves (2x2); bt = 128: 128x128 tiles on 8 waves (2x4).
-template <int TAG>
+// epi: epilogue with its C loads in flight together (see the kernel).
+template <int TAG, int EPI>
 static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int bt, hipStream_t st) {
     if (bt == 128)
-        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG>), dim3(n), dim3(512), 0, st, tasks, tiles);
+        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, EPI>), dim3(n), dim3(512), 0, st, tasks, tiles);
     else
-        hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG>), dim3(n), dim3(256), 0, st, tasks, tiles);
+        hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG, EPI>), dim3(n), dim3(256), 0, st, tasks, tiles);
 }
 
-hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st) {
+hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
+                       int epi) {
     if (total_tiles <= 0) return hipSuccess;
     if (tag)
-        launch_syrk_t<1>(tasks, tiles, total_tiles, bt, st);
+        epi ? launch_syrk_t<1, 1>(tasks, tiles, total_tiles, bt, st) : launch_syrk_t<1, 0>(tasks, tiles, total_tiles, bt, st);
     else
-        launch_syrk_t<0>(tasks, tiles, total_tiles, bt, st);
+        epi ? launch_syrk_t<0, 1>(tasks, tiles, total_tiles, bt, st) : launch_syrk_t<0, 0>(tasks, tiles, total_tiles, bt, st);
     return hipGetLastError();
 }
 

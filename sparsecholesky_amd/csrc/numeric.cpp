@@ -16,6 +16,12 @@
 
 namespace sc {
 
+// CB launches with every K below this use the batched SYRK epilogue (measured per
+// level at 128^3: K <= 121 gains, K = 226 loses)
+#ifndef SC_EPI_KMAX
+#define SC_EPI_KMAX 192
+#endif
+
 #define HIP_TRY(x)                                                                \
     do {                                                                          \
         hipError_t e_ = (x);                                                      \
@@ -219,10 +225,17 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
         L.off = (int64_t)gemm.size();
         // 128x128 tiles on 8 waves when every task is at least 256 wide (random data,
         // 16384 x 4096: 61 vs 52 TF/s for 64x64); 64x64 on 4 waves for narrow updates
-        int minN = INT32_MAX;
-        for (auto& t : tasks) minN = std::min(minN, (int)t.N);
+        int minN = INT32_MAX, maxK = 0;
+        for (auto& t : tasks) {
+            minN = std::min(minN, (int)t.N);
+            maxK = std::max(maxK, (int)t.K);
+        }
         const bool wide = minN >= 256;
         L.bt = (S.opt.syrk_tile == 128 || (S.opt.syrk_tile == 0 && wide)) ? SYRK_BT_LARGE : SYRK_BT_SMALL;
+        // batched C epilogue on the critical path (main-stream panel updates) and where
+        // K is short enough that the epilogue dominates a tile (CB of levels 4-7 at
+        // 128^3); deep-K CB updates and the lookahead stream keep the trickle epilogue
+        L.epi = (kind == L_PANEL && strm == 0) || (kind == L_CB && maxK < SC_EPI_KMAX);
         L.toff = (int64_t)tiles.size();
         for (size_t q = 0; q < tasks.size(); ++q) {
             append_tiles(tiles, (int)q, tasks[q].M, tasks[q].N, L.bt);
@@ -1162,7 +1175,7 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
             return launch_trsm_panel(N.R[L.vr].P, N.d_trsm + L.off, L.count, N.stream, L.big != 0, N.d_arrive);
         case L_PANEL:
         case L_CB:
-            return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st);
+            return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st, L.epi);
         case L_COMM:
             return comm_launch(N, L);
     }
@@ -1353,8 +1366,9 @@ int64_t numeric_timing(Numeric& N, double* t, int nt) {
 
 int64_t numeric_syrk_stats(Numeric& N, int wmin, double* flops, double* ms, int64_t* launches) {
     // CB SYRK launches are split by w >= 256; wmin selects them (0: all CB launches,
-    // -1: the panel-update launches instead, -2: the CB launches on 128 x 128 tiles,
-    // i.e. exactly the syrk_mfma_kernel<128,2,4,1> dispatches a kernel trace lists)
+    // -1: the panel-update launches instead, -2: the CB launches on 128 x 128 tiles with
+    // the trickle epilogue, i.e. exactly the syrk_mfma_kernel<128,2,4,1,0> dispatches a
+    // kernel trace lists)
     double fl = 0.0, t = 0.0;
     int64_t cnt = 0;
     bool have_t = N.status_valid && N.profile != 0;
@@ -1363,7 +1377,7 @@ int64_t numeric_syrk_stats(Numeric& N, int wmin, double* flops, double* ms, int6
         const Launch& L = N.sched[i];
         if (L.kind != (wmin == -1 ? L_PANEL : L_CB)) continue;
         if (wmin >= 256 && !L.big) continue;
-        if (wmin == -2 && L.bt != SYRK_BT_LARGE) continue;
+        if (wmin == -2 && (L.bt != SYRK_BT_LARGE || L.epi)) continue;
         fl += L.flops;
         ++cnt;
         if (have_t) {
