@@ -129,6 +129,10 @@ def main():
                     help="extra sc_options field, key=value (lists comma-separated), e.g. nrelax=4,16,48")
     ap.add_argument("--tile", type=int, default=None, help="SYRK tile: 0 auto, 64, 128")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--transport", choices=["rccl", "host", "dry"], default="rccl",
+                    help="N > 1 data path: rccl (default, one GPU per rank); host: every transfer staged "
+                         "through host memory over gloo (rehearsal with several ranks on one GPU); dry: "
+                         "comm steps move nothing (per-rank compute only, the factor is not validated)")
     args = ap.parse_args()
 
     import torch
@@ -141,8 +145,9 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if args.gpus > 1 and world == 1:
         raise SystemExit("multi-GPU runs are launched with torch.distributed.run (one rank per GPU)")
-    torch.cuda.set_device(local_rank)
-    dev = local_rank
+    # rccl: one GPU per rank; host / dry rehearsals may put several ranks on one GPU
+    dev = local_rank if args.transport == "rccl" else local_rank % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -182,9 +187,13 @@ def main():
     t0 = time.perf_counter()
     work_share = None
     if world > 1:
-        uid = [sc.dist_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        num = sc.Numeric(symb, device=dev, rank=rank, nranks=world, uid=uid[0])
+        if args.transport == "rccl":
+            uid = [sc.dist_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            num = sc.Numeric(symb, device=dev, rank=rank, nranks=world, uid=uid[0])
+        else:
+            num = sc.Numeric(symb, device=dev, rank=rank, nranks=world,
+                             transport=sc.GlooHostTransport() if args.transport == "host" else "dry")
         _, wr = symb.owner_map(world)
         work_share = [round(float(x) / float(wr.sum()), 4) for x in wr]
     else:
@@ -254,14 +263,16 @@ def main():
     # ||A x - b||_inf / (||A||_inf ||x||_inf + ||b||_inf), with A from the upper CSC.
     # A wrong factor cannot pass: the bound is 1e-12 (measured 6.9e-16 at 128^3).
     solve = None
-    d_b = torch.ones(st["n"], dtype=torch.float64, device=f"cuda:{dev}")
-    d_x = torch.empty_like(d_b)
-    torch.cuda.synchronize()  # d_b complete before the library stream reads it
-    num.solve_device(d_b.data_ptr(), d_x.data_ptr())
-    x = d_x.cpu().numpy()
-    berr = backward_error(A, x, np.ones(st["n"]))
-    if not berr < 1e-12:
-        raise SystemExit(f"validation failed: backward error {berr:.3e} of the timed factor")
+    berr = None
+    if args.transport != "dry":
+        d_b = torch.ones(st["n"], dtype=torch.float64, device=f"cuda:{dev}")
+        d_x = torch.empty_like(d_b)
+        torch.cuda.synchronize()  # d_b complete before the library stream reads it
+        num.solve_device(d_b.data_ptr(), d_x.data_ptr())
+        x = d_x.cpu().numpy()
+        berr = backward_error(A, x, np.ones(st["n"]))
+        if not berr < 1e-12:
+            raise SystemExit(f"validation failed: backward error {berr:.3e} of the timed factor")
     if world == 1 and not args.no_solve:
         # solve timing: forward + backward sweep, each reads L once (8 * panel entries
         # bytes, relaxed zeros included)
@@ -294,7 +305,10 @@ def main():
             "supernodes": st["n_supernodes"], "levels": st["n_levels"], "max_front": st["max_front_m"],
             "flops_executed": st["flops_executed"],
             "parallelism": "single GPU" if world == 1 else
-            f"subtree partition over {world} GPUs, RCCL p2p of contribution blocks at merge fronts",
+            f"subtree partition over {world} GPUs, RCCL p2p of contribution blocks at merge fronts"
+            if args.transport == "rccl" else
+            f"subtree partition over {world} ranks on {torch.cuda.device_count()} GPU(s), transport "
+            f"{args.transport} (rehearsal of the N-GPU protocol; not an N-GPU measurement)",
             "work_share_per_rank": work_share,
             "options": {"relax_wmax": symb.opt.relax_wmax, "panel_nb_outer": symb.opt.panel_nb_outer,
                         "small_front_max": symb.opt.small_front_max, "use_graph": symb.opt.use_graph,
@@ -304,8 +318,10 @@ def main():
         "roofline": roof,
         "timing_s": {"generate": round(t_gen, 3), "analyze": round(t_an, 3), "numeric_create": round(t_alloc, 3)},
         "phase_ms": phases,
-        "validation": {"backward_error": float(f"{berr:.3e}"), "bound": 1e-12,
-                       "check": "GPU solve with the timed factor, ||Ax-b||/(||A|| ||x||+||b||), inf-norms"},
+        "validation": {"backward_error": float(f"{berr:.3e}") if berr is not None else None, "bound": 1e-12,
+                       "check": "GPU solve with the timed factor, ||Ax-b||/(||A|| ||x||+||b||), inf-norms"
+                       if berr is not None else "skipped: dry transport (no data moved, factor not valid)"},
+        "transport": args.transport if world > 1 else None,
         "device_memory_GB": {"total": round(mem["total"] / 1e9, 2), "panels_L": round(mem["panel"] / 1e9, 2),
                              "work_arena_CB": round(mem["work"] / 1e9, 2),
                              "note": "rank 0 of the handle, factorization only (solve buffers excluded)"},

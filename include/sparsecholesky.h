@@ -51,8 +51,12 @@ enum sc_status {
 typedef struct sc_symbolic sc_symbolic;
 typedef struct sc_numeric sc_numeric;
 
-/* Analysis options.  Defaults: sc_default_options(). */
+/* Analysis options.  Defaults: sc_default_options(), which also sets struct_size;
+ * sc_analyze rejects (SC_ERR_ARG) options whose struct_size is not this header's
+ * sizeof(sc_options), so a caller built against another layout fails loudly instead
+ * of misreading fields. */
 typedef struct sc_options {
+    int32_t struct_size;     /* sizeof(sc_options) of the caller's header (set by sc_default_options) */
     int32_t relax;           /* 1 = relaxed supernode amalgamation (CHOLMOD-style) */
     int32_t nrelax[3];       /* width thresholds for amalgamation */
     double zrelax[3];        /* zero-fraction thresholds for amalgamation */
@@ -80,6 +84,9 @@ typedef struct sc_options {
                                 factored 1D slab-cyclic over its rank group, each final slab sent to the ranks
                                 that update later slabs or its contribution block (1, default); 0: the panel
                                 on the front's owner */
+    int32_t cb_gather;       /* 1 (default): a large front's contribution block is not assembled; its CB SYRK
+                                gathers the children's entries into each output tile (C = sum - L21 L21^T,
+                                written once); 0: assembly writes the whole front, the SYRK updates it */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

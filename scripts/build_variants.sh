@@ -5,7 +5,7 @@ cd "$(dirname "$0")/.."
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   d=gpurun_var/$name
-  rm -rf "$d"; mkdir -p "$d/profiles/r02"
+  rm -rf "$d"; mkdir -p "$d/profiles/r02" "$d/oracle"
   cp bench.py "$d/"
   cp profiles/r02/pmc_summary.json profiles/r02/mfma_util.json "$d/profiles/r02/"
   mkdir -p "$d/sparsecholesky_amd"

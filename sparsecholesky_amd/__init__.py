@@ -64,12 +64,13 @@ class LibraryError(RuntimeError):
 
 class Options(C.Structure):
     _fields_ = [
-        ("relax", C.c_int32), ("nrelax", C.c_int32 * 3), ("zrelax", C.c_double * 3),
+        ("struct_size", C.c_int32), ("relax", C.c_int32), ("nrelax", C.c_int32 * 3), ("zrelax", C.c_double * 3),
         ("small_front_max", C.c_int32), ("panel_nb", C.c_int32), ("panel_nb_outer", C.c_int32),
         ("use_graph", C.c_int32), ("relax_wmax", C.c_int32), ("syrk_tile", C.c_int32),
         ("lookahead", C.c_int32), ("inner_order", C.c_int32),
         ("asm_tile_min_m", C.c_int32), ("dist_split", C.c_int32), ("dist_cbb", C.c_int32),
         ("ordering", C.c_int32), ("dist_early", C.c_int32), ("dist_panel", C.c_int32),
+        ("cb_gather", C.c_int32),
     ]
 
 

@@ -64,6 +64,7 @@ const char* sc_last_error(void) { return g_last_error.c_str(); }
 void sc_default_options(sc_options* opt) {
     if (!opt) return;
     std::memset(opt, 0, sizeof(*opt));
+    opt->struct_size = (int32_t)sizeof(sc_options);
     opt->relax = 1;
     opt->nrelax[0] = 4;
     opt->nrelax[1] = 16;
@@ -84,6 +85,7 @@ void sc_default_options(sc_options* opt) {
     opt->dist_cbb = 1024;
     opt->dist_early = 1;
     opt->dist_panel = 1;
+    opt->cb_gather = 1;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,
@@ -91,10 +93,16 @@ int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_opt
     if (!out) return SC_ERR_ARG;
     *out = nullptr;
     sc_options o;
-    if (opt)
+    if (opt) {
+        if (opt->struct_size != (int32_t)sizeof(sc_options)) {
+            g_last_error = "sc_options.struct_size does not match this library's sizeof(sc_options): "
+                           "initialise the options with sc_default_options() from the matching header";
+            return SC_ERR_ARG;
+        }
         o = *opt;
-    else
+    } else {
         sc_default_options(&o);
+    }
     if (o.small_front_max > 128) o.small_front_max = 128;
     if (o.small_front_max < 0) o.small_front_max = 0;
     sc_symbolic* h = new (std::nothrow) sc_symbolic();

@@ -773,6 +773,9 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
     __shared__ double2 S[TRSM64_STREAM / 2];
     __shared__ __attribute__((aligned(16))) double colbuf[2 * 4 * COLB];
     __shared__ int s_last;
+#if SC_CRIT_PRIO > 0
+    __builtin_amdgcn_s_setprio(SC_CRIT_PRIO);  // critical path: wins issue over co-resident SYRK waves
+#endif
     const int4 t = tasks[blockIdx.x];
     const int s = t.x, k0 = t.y, r0 = t.z;
     const int tid = threadIdx.x;
@@ -842,9 +845,120 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
 // (BK = 8 and 32, and a 4-wave 128 x 128 instance, were measured slower on every
 // shape: DESIGN.md section 5.)
 // ---------------------------------------------------------------------------
+// Extend-add fused into the CB update (fronts whose contribution block is not
+// assembled): C = sum over children of their CB entries that map into the tile, minus
+// the tile's A A^T.  Replaces the assembly's zero + add of the CB region and the
+// SYRK's read of it (two of the four HBM passes over every CB entry).  The tile is
+// built in LDS in 64-row chunks (G[col * GLD + row], GLD odd: the epilogue's 16
+// columns x 4 rows per load hit distinct banks); wave w owns the chunk's columns
+// c = w (mod waves), so children add in their fixed order with no atomics and no
+// barrier per child (deterministic).  A child's CB rows that land in a 64-row block
+// of the parent's CB are one contiguous run (relind is increasing): tile_bnd.
+__device__ __forceinline__ int tile_bnd_at(const int32_t* tb, int k, int mbc) {
+    const int klo = tb[0], khi = tb[1];
+    return k <= klo ? tb[2] : (k >= khi ? mbc : tb[3 + k - klo - 1]);
+}
+// wave-uniform values kept in SGPRs (the child loop is uniform; without this the
+// compiler keeps its counters in VGPRs and branches per lane)
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+template <class T>
+__device__ __forceinline__ T* uni_ptr(T* p) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
+}
+
+template <int BT, int WM, int WN>
+__device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const DevPlan& P, int row0, int col0,
+                                                     double4_t (&acc)[BT / WM / 16][BT / WN / 16], double* smem) {
+    constexpr int NW = WM * WN, NT = 64 * NW;
+    constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
+    constexpr int GR = 64, GLD = GR + 1;  // rows per chunk, LDS column stride (doubles)
+    constexpr int GQ = SC_GATHER_Q;       // child columns per batch of loads (VGPR budget: 4 waves / SIMD)
+    static_assert(BT * GLD * 8 <= 2 * 2 * 16 * (BT + 16) * 8, "gather chunk fits the operand LDS");
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wr = wid / WN, wc = wid % WN;
+    const int s = T.gs;
+    const int w = T.K;
+    const int mb = T.M;
+    const int cp0 = uni(P.child_ptr[s]), cp1 = uni(P.child_ptr[s + 1]);
+    double* G = smem;
+    double* __restrict__ C = T.C;
+    const int64_t ldc = T.ldc;
+    const __amdgpu_buffer_rsrc_t rc = buf_rsrc(C + (int64_t)col0 * ldc, (uint32_t)(min(BT, T.N - col0) * ldc * 8));
+#pragma unroll 1
+    for (int h = 0; h < BT / GR; ++h) {
+        const int r0 = row0 + h * GR;  // CB rows of this chunk: [r0, r0 + 64)
+        if (h) __syncthreads();        // previous chunk's G fully read
+        for (int e = tid; e < BT * GLD; e += NT) G[e] = 0.0;
+        __syncthreads();
+        if (r0 < mb) {
+            for (int ci = cp0; ci < cp1; ++ci) {
+                const int c = uni(P.child_list[ci]);
+                const int mbc = uni(P.sn_m[c] - (P.sn_start[c + 1] - P.sn_start[c]));
+                const int32_t* tb = uni_ptr(P.tile_bnd + P.tb_ptr[c]);
+                const int ilo = uni(tile_bnd_at(tb, r0 / GR, mbc)), ihi = uni(tile_bnd_at(tb, r0 / GR + 1, mbc));
+                const int jlo = uni(tile_bnd_at(tb, col0 / GR, mbc)), jhi = uni(tile_bnd_at(tb, (col0 + BT) / GR, mbc));
+                if (ilo >= ihi || jlo >= jhi) continue;
+                const int32_t* __restrict__ rel = uni_ptr(P.relind + P.rel_ptr[c]);
+                const double* __restrict__ cb = uni_ptr(P.cb_pool + P.cb_off[c]);
+                // this lane's row of the chunk (<= 64 child rows map into 64 parent rows)
+                const int ic = ilo + lane;
+                const int prow = ic < ihi ? rel[ic] - w - r0 : -1;
+                for (int jb = jlo; jb < jhi; jb += 64) {
+                    const int jl = jb + lane;
+                    const int pcl = jl < jhi ? rel[jl] - w - col0 : -1;
+                    uint64_t mask = __ballot(pcl >= 0 && pcl % NW == wid);
+                    while (mask) {  // up to GQ owned child columns (uniform), all loads in flight first
+                        int jc[GQ], pc[GQ];
+#pragma unroll
+                        for (int q = 0; q < GQ; ++q) {
+                            const int b = mask ? __builtin_ctzll(mask) : -1;
+                            jc[q] = b < 0 ? -1 : jb + b;
+                            pc[q] = b < 0 ? 0 : __builtin_amdgcn_readlane(pcl, b);
+                            mask &= mask - 1;
+                        }
+                        double v[GQ];
+                        bool ok[GQ];
+#pragma unroll
+                        for (int q = 0; q < GQ; ++q) {  // column jc of the child's CB, rows >= jc
+                            ok[q] = jc[q] >= 0 && prow >= 0 && ic >= jc[q];
+                            const __amdgpu_buffer_rsrc_t rs = buf_rsrc(cb + (int64_t)max(jc[q], 0) * mbc, (uint32_t)mbc * 8u);
+                            v[q] = buf_ld(rs, ok[q] ? ic * 8 : BUF_DEAD, 0);
+                        }
+#pragma unroll
+                        for (int q = 0; q < GQ; ++q)
+                            if (ok[q]) G[pc[q] * GLD + prow] += v[q];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // the waves whose MFMA rows lie in this chunk (a wave's BT / WM <= 64 rows sit in
+        // one chunk) store C = G - acc (no C read)
+        static_assert(GR % (BT / WM) == 0, "a wave's rows lie in one chunk");
+        if ((wr * (BT / WM)) / GR == h) {
+#pragma unroll
+            for (int a = 0; a < RTM; ++a)
+#pragma unroll
+                for (int b = 0; b < RTN; ++b)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int lr = wr * (BT / WM) + a * 16 + MFMA_F64_ROW(lane, r);
+                        const int lc = wc * (BT / WN) + b * 16 + (lane & 15);
+                        const int gi = row0 + lr, gj = col0 + lc;
+                        const bool live = gi < T.M && gi >= gj && gj < T.N;
+                        const double x = G[lc * GLD + (lr - h * GR)] - acc[a][b][r];
+                        buf_st(x, rc, live ? (int)((gi + (int64_t)(gj - col0) * ldc) * 8) : BUF_DEAD, 0);
+                    }
+        }
+    }
+    __syncthreads();  // G fully read before the workgroup's next tile stages operands
+}
+
 template <int BT, int WM, int WN, int TAG, int EPI>
-__global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
-                                                                  const int2* __restrict__ tiles) {
+__device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ tasks, const int2* __restrict__ tiles,
+                                               int bidx, const DevPlan* __restrict__ plans) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BK = 16;
     constexpr int LDT = BT + 16;  // +128 B row pad: the two k-rows read by a half-wave hit disjoint banks
@@ -854,7 +968,7 @@ __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask*
     double(*Bs)[BK * LDT] = reinterpret_cast<double(*)[BK * LDT]>(smem + 2 * BK * LDT);
 
     // host-ordered tile list: blocks sharing an XCD walk a contiguous, L2-blocked run of tiles
-    const int2 tl = tiles[blockIdx.x];
+    const int2 tl = tiles[bidx];
     const GemmTask T = tasks[tl.x];
     const int ti = tl.y >> 16, tj = tl.y & 0xffff;
     const int row0 = ti * BT, col0 = tj * BT;
@@ -865,6 +979,12 @@ __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask*
     const int wr = wid / WN, wc = wid % WN;
     // static priority for the second-dispatched half of the waves (the arbitration loser
     // on every segment of two co-resident waves per SIMD): 547.8-548.5 -> 544.6-546.0 ms
+#if SC_CRIT_PRIO > 0
+    // main-stream panel updates (TAG 0, EPI 1) are the critical path: above every co-resident SYRK wave
+    if (TAG == 0 && EPI == 1)
+        __builtin_amdgcn_s_setprio(SC_CRIT_PRIO - 1);
+    else
+#endif
     if (wid >= WM * WN / 2) __builtin_amdgcn_s_setprio(1);
     const double* __restrict__ A = T.A;
     const int64_t lda = T.lda;
@@ -941,6 +1061,12 @@ __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask*
         __syncthreads();
     }
 
+    if constexpr (TAG == 1) {
+        if (T.gs >= 0) {  // the front's CB is not assembled: gather the children's entries
+            syrk_gather_epilogue<BT, WM, WN>(T, plans[T.gv], row0, col0, acc, smem);
+            return;
+        }
+    }
     // epilogue: f64 16x16x4 C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg.
     // C read-modify-write through a buffer resource over the tile's columns (dead
     // elements -- above the diagonal, past M / N -- masked by range, no branches).
@@ -984,6 +1110,21 @@ __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask*
                     for (int r = 0; r < 4; ++r) buf_st(cv[a][b][r] - acc[a0 + a][b][r], rc, offs[a][b][r], 0);
         }
     }
+}
+
+template <int BT, int WM, int WN, int TAG, int EPI>
+__global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
+                                                                  const int2* __restrict__ tiles,
+                                                                  const DevPlan* __restrict__ plans) {
+    syrk_tile_body<BT, WM, WN, TAG, EPI>(tasks, tiles, blockIdx.x, plans);
+}
+
+// Capped grid (lookahead-stream updates): workgroup b takes tiles b, b + grid, ...
+// (grid a multiple of 8, so every tile keeps the XCD the host ordered it for).
+template <int BT, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_loop_kernel(const GemmTask* __restrict__ tasks,
+                                                                       const int2* __restrict__ tiles, int ntiles) {
+    for (int bt = blockIdx.x; bt < ntiles; bt += gridDim.x) syrk_tile_body<BT, WM, WN, 0, 0>(tasks, tiles, bt, nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -1051,20 +1192,33 @@ hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hip
 // bt = 64: 64x64 tiles on 4 waves (2x2); bt = 128: 128x128 tiles on 8 waves (2x4).
 // epi: epilogue with its C loads in flight together (see the kernel).
 template <int TAG, int EPI>
-static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int bt, hipStream_t st) {
+static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int grid, int bt, hipStream_t st,
+                          const DevPlan* plans) {
+    if (TAG == 0 && EPI == 0 && grid < n) {
+        if (bt == 128)
+            hipLaunchKernelGGL((syrk_mfma_loop_kernel<128, 2, 4>), dim3(grid), dim3(512), 0, st, tasks, tiles, n);
+        else
+            hipLaunchKernelGGL((syrk_mfma_loop_kernel<64, 2, 2>), dim3(grid), dim3(256), 0, st, tasks, tiles, n);
+        return;
+    }
     if (bt == 128)
-        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, EPI>), dim3(n), dim3(512), 0, st, tasks, tiles);
+        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, EPI>), dim3(n), dim3(512), 0, st, tasks, tiles, plans);
     else
-        hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG, EPI>), dim3(n), dim3(256), 0, st, tasks, tiles);
+        hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG, EPI>), dim3(n), dim3(256), 0, st, tasks, tiles, plans);
 }
 
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
-                       int epi) {
+                       int epi, int max_grid, const DevPlan* plans) {
     if (total_tiles <= 0) return hipSuccess;
+    // max_grid > 0 (a multiple of 8; panel updates without the batched epilogue): at
+    // most that many workgroups, each looping over tiles
+    const int grid = (max_grid > 0 && total_tiles > max_grid && !tag && !epi) ? max_grid : total_tiles;
     if (tag)
-        epi ? launch_syrk_t<1, 1>(tasks, tiles, total_tiles, bt, st) : launch_syrk_t<1, 0>(tasks, tiles, total_tiles, bt, st);
+        epi ? launch_syrk_t<1, 1>(tasks, tiles, total_tiles, grid, bt, st, plans)
+            : launch_syrk_t<1, 0>(tasks, tiles, total_tiles, grid, bt, st, plans);
     else
-        epi ? launch_syrk_t<0, 1>(tasks, tiles, total_tiles, bt, st) : launch_syrk_t<0, 0>(tasks, tiles, total_tiles, bt, st);
+        epi ? launch_syrk_t<0, 1>(tasks, tiles, total_tiles, grid, bt, st, plans)
+            : launch_syrk_t<0, 0>(tasks, tiles, total_tiles, grid, bt, st, plans);
     return hipGetLastError();
 }
 

@@ -24,6 +24,20 @@ constexpr int SYRK_BT_LARGE = 128;
 // section 3): col = lane & 15, row = (lane >> 4) + 4 * reg.
 #define MFMA_F64_ROW(lane, r) (((lane) >> 4) + 4 * (r))
 
+// s_setprio of the critical-path kernels (fused POTRF/TRSM: this value; main-stream
+// panel updates: one less); 0 = off
+#ifndef SC_CRIT_PRIO
+#define SC_CRIT_PRIO 0
+#endif
+// child columns per batch of loads in the CB SYRK's extend-add gather
+#ifndef SC_GATHER_Q
+#define SC_GATHER_Q 4
+#endif
+// workgroups of a lookahead-stream panel update (0 = one per tile)
+#ifndef SC_LA_GRID
+#define SC_LA_GRID 0
+#endif
+
 // All device arrays of the numeric plan (internal numbering).
 struct DevPlan {
     const int32_t* sn_start;    // ns+1
@@ -38,6 +52,8 @@ struct DevPlan {
     const int32_t* rel_bnd;     // per child: CB row bounds of the parent's ASM_ROWS row tiles
     const int64_t* cbk_ptr;     // ns+1
     const int32_t* col_bnd;     // per child: CB row bounds of the parent's ASM_COLS column blocks
+    const int64_t* tb_ptr;      // ns+1
+    const int32_t* tile_bnd;    // per child: CB row bounds of the parent's 64-row CB blocks (symbolic.hpp)
     const int64_t* a_ptr;       // n+1 (internal columns)
     const int32_t* a_pos;       // row position in the column's front
     const int64_t* a_src;       // index into the input value array
@@ -47,12 +63,17 @@ struct DevPlan {
 };
 
 // One lower-trapezoid SYRK update: C[i,j] -= sum_k A[i,k] A[j,k], j < N, j <= i < M.
+// gs >= 0 (CB updates only): C is front gs's whole contribution block and is not read;
+// the children's CB entries that fall into it are gathered instead (the extend-add of
+// the reference's apply_update, chol.hpp:1196) and C = sum(children) - A A^T is written.
+// gv: the hosted rank whose DevPlan (plans[gv]) holds the children.
 struct GemmTask {
     double* C;
     const double* A;
     int64_t ldc;
     int64_t lda;
     int32_t M, N, K;
+    int32_t gs = -1, gv = 0;
 };
 
 // Strided <-> packed copy of a rows x cols block (pack: a -> b; unpack: b -> a).
@@ -162,8 +183,9 @@ hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hip
 // per-block arrival counters, zeroed; task .w - 1 indexes them)
 hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st, bool partial,
                              int32_t* arrive);
+// max_grid > 0 (a multiple of 8): at most that many workgroups, each looping over tiles
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
-                       int epi = 0);
+                       int epi = 0, int max_grid = 0, const DevPlan* plans = nullptr);
 hipError_t launch_stamp(uint64_t* slot, hipStream_t st);
 hipError_t launch_fill_random(double* p, int64_t n, hipStream_t st);
 hipError_t launch_mfma_peak(double* out, int blocks, int iters, int nacc, hipStream_t st);

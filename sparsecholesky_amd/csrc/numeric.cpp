@@ -433,6 +433,9 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
         for (int32_t s : nodes)
             if (S.fclass[s] == FRONT_LARGE) large.push_back(s);
         if (large.empty()) return;
+        // fronts whose CB SYRK gathers the children's CB entries itself (one CB launch
+        // task covering the whole CB): their assembly stops at the panel columns
+        auto gather = [&](int32_t s) { return S.opt.cb_gather && S.mb(s) > 0 && !is_split(s) && !is_early_sender(s, v); };
         // assembly: fronts with m >= ASM_TILE_MIN_M one workgroup per (front, 16
         // columns, 256-row tile), write-once (big = 1); smaller fronts one workgroup per
         // (front, 16 columns) streaming child columns (measured faster below ~8k rows)
@@ -447,7 +450,8 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
             for (int32_t s : large) {
                 const int m = S.sn_m[s];
                 if ((m >= tile_min_m) != (tiled == 1)) continue;
-                for (int cb = 0; cb * ASM_COLS < m; ++cb) {
+                const int ncol = gather(s) ? S.w(s) : m;  // assembled columns
+                for (int cb = 0; cb * ASM_COLS < ncol; ++cb) {
                     if (!tiled) {
                         asmv.push_back(make_int2(s, cb));
                         continue;
@@ -600,6 +604,10 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 t.M = mb;
                 t.N = mb;
                 t.K = w;
+                if (gather(s)) {
+                    t.gs = s;
+                    t.gv = v;
+                }
                 cbt.push_back(t);
                 fl += (double)mb * (mb + 1.0) * t.K;
             }
@@ -1033,13 +1041,14 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     panel_layout(N, S, multi ? N.nranks : 1);
     // ---- shared plan arrays ----
     DevPlan P0 {};
-    int32_t *d_sn_start, *d_sn_m, *d_child_ptr, *d_child_list, *d_relind, *d_apos, *d_relbnd, *d_colbnd;
-    int64_t *d_rel_ptr, *d_aptr, *d_asrc, *d_rbptr, *d_cbkptr;
+    int32_t *d_sn_start, *d_sn_m, *d_child_ptr, *d_child_list, *d_relind, *d_apos, *d_relbnd, *d_colbnd, *d_tilebnd;
+    int64_t *d_rel_ptr, *d_aptr, *d_asrc, *d_rbptr, *d_cbkptr, *d_tbptr;
     if ((rc = upload(N, S.sn_start, d_sn_start)) || (rc = upload(N, S.sn_m, d_sn_m)) ||
         (rc = upload(N, S.child_ptr, d_child_ptr)) || (rc = upload(N, S.child_list, d_child_list)) ||
         (rc = upload(N, S.rel_ptr, d_rel_ptr)) || (rc = upload(N, S.relind, d_relind)) ||
         (rc = upload(N, S.rb_ptr, d_rbptr)) || (rc = upload(N, S.rel_bnd, d_relbnd)) ||
         (rc = upload(N, S.cbk_ptr, d_cbkptr)) || (rc = upload(N, S.col_bnd, d_colbnd)) ||
+        (rc = upload(N, S.tb_ptr, d_tbptr)) || (rc = upload(N, S.tile_bnd, d_tilebnd)) ||
         (rc = upload(N, S.a_ptr, d_aptr)) || (rc = upload(N, S.a_pos, d_apos)) ||
         (rc = upload(N, S.a_src, d_asrc)) || (rc = upload(N, N.gpo, N.d_gpo)))
         return fail(rc);
@@ -1053,6 +1062,8 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     P0.rel_bnd = d_relbnd;
     P0.cbk_ptr = d_cbkptr;
     P0.col_bnd = d_colbnd;
+    P0.tb_ptr = d_tbptr;
+    P0.tile_bnd = d_tilebnd;
     P0.a_ptr = d_aptr;
     P0.a_pos = d_apos;
     P0.a_src = d_asrc;
@@ -1089,6 +1100,11 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
         R.P.cb_off = dp;
     }
     if (!multi || N.emulated) N.gpanel = pbase;  // gathered layout == the arenas
+    {
+        std::vector<DevPlan> plans;
+        for (const RankMem& R : N.R) plans.push_back(R.P);
+        if ((rc = upload(N, plans, N.d_plans))) return fail(rc);
+    }
 
     SchedBuild B;
     if ((rc = build_schedule(N, B))) return fail(rc);
@@ -1175,7 +1191,8 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
             return launch_trsm_panel(N.R[L.vr].P, N.d_trsm + L.off, L.count, N.stream, L.big != 0, N.d_arrive);
         case L_PANEL:
         case L_CB:
-            return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st, L.epi);
+            return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st, L.epi,
+                               (L.kind == L_PANEL && L.strm == 1) ? SC_LA_GRID : 0, N.d_plans);
         case L_COMM:
             return comm_launch(N, L);
     }

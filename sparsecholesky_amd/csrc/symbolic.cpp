@@ -428,6 +428,25 @@ i64 analyze(i64 n, const i64* Ap, const i32* Ai, const sc_options& opt, Symbolic
         }
         S.cbk_ptr[s + 1] = (i64)S.col_bnd.size();
     }
+    S.tb_ptr.assign((size_t)ns + 1, 0);
+    S.tile_bnd.clear();
+    for (i32 s = 0; s < ns; ++s) {
+        const i32 p = S.sn_parent[s];
+        if (p >= 0) {
+            const i32 wp = S.w(p);
+            const i32* rel = S.relind.data() + S.rel_ptr[s];
+            const i32 mbc = (i32)(S.rel_ptr[s + 1] - S.rel_ptr[s]);
+            const i32 j0 = (i32)(std::lower_bound(rel, rel + mbc, wp) - rel);
+            const i32 klo = j0 < mbc ? (rel[j0] - wp) / 64 : 0;
+            const i32 khi = j0 < mbc ? (rel[mbc - 1] - wp) / 64 + 1 : 0;
+            S.tile_bnd.push_back(klo);
+            S.tile_bnd.push_back(khi);
+            S.tile_bnd.push_back(j0);
+            for (i32 k = klo + 1; k < khi; ++k)
+                S.tile_bnd.push_back((i32)(std::lower_bound(rel, rel + mbc, wp + 64 * k) - rel));
+        }
+        S.tb_ptr[s + 1] = (i64)S.tile_bnd.size();
+    }
     S.child_ptr.assign((size_t)ns + 1, 0);
     S.child_list.clear();
     for (i32 s = 0; s < ns; ++s) {

@@ -78,6 +78,12 @@ struct Symbolic {
     std::vector<i32> rel_bnd;
     std::vector<i64> cbk_ptr;    // ns+1
     std::vector<i32> col_bnd;    // per child: CB rows of the parent's kAsmCols-column blocks
+    // per child: its CB rows in the parent's contribution block, by 64-row blocks of the
+    // parent's CB (the CB SYRK's extend-add gather, kernels.hip syrk_gather): g(k) = first
+    // CB row whose parent position is >= w_parent + 64 k, stored compactly as
+    // [k_lo, k_hi, g(k_lo), g(k_lo + 1) .. g(k_hi - 1)] (g = g(k_lo) below k_lo, mbc from k_hi)
+    std::vector<i64> tb_ptr;     // ns+1
+    std::vector<i32> tile_bnd;
     std::vector<i64> panel_off;  // ns+1 (doubles), L panel m x w, ld = m
     std::vector<i64> cb_off;     // ns+1 (doubles), CB mb x mb, ld = mb
     std::vector<i64> a_ptr;      // n+1: A entries grouped by internal column (lower part)

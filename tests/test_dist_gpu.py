@@ -69,6 +69,8 @@ def _sym_full(A):
 
 @pytest.mark.parametrize("world,k,opts", [
     (2, 16, {}),
+    (2, 32, {}),  # default options (NBO 1024, dist_cbb 1024): the 1024-wide root slabs distributed
+    (4, 32, {}),  # defaults with split fronts (1024-wide CB blocks)
     (2, 20, dict(dist_cbb=64, small_front_max=32)),
     (3, 20, dict(dist_cbb=64, dist_early=0)),
     (4, 20, dict(panel_nb_outer=128, dist_cbb=64, small_front_max=32)),
@@ -83,6 +85,15 @@ def test_multiprocess_host_transport(gpu, world, k, opts):
     out = mgr.dict()
     mp.spawn(_rank_main, args=(world, port, k, opts, out), nprocs=world, join=True)
     ok_pat, same, err, be, sts, exp_st, errs, mems = out["res"]
+    if not opts:  # the default plan must exercise the distributed paths
+        import sparsecholesky_amd as sc
+
+        info = sc.Symbolic(sc.laplacian3d(k)).dist_plan_info(world)
+        if k >= 32:
+            assert info["slab_ranks"].max() >= 2
+        if k >= 32 and world >= 4:
+            assert info["split_cb_ranks"].max() > 0
+    print(f"world {world}, k {k}, {opts}: rel-Fro {err:.3e}, backward error {be:.3e}")
     assert all(e is None for e in errs), errs
     assert all(s == [0, 0] for s in sts), sts
     assert all(s == 0 for s in exp_st), exp_st

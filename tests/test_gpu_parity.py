@@ -322,6 +322,34 @@ def test_lap48_full_parity(gpu, lap48_oracle, opts):
     assert err < TOL
 
 
+@pytest.mark.parametrize("nranks,rccl", [(2, False), (4, False), (8, False), (2, True), (4, True), (8, True)])
+def test_partitioned_defaults_lap48(gpu, lap48_oracle, nranks, rccl):
+    # the distributed plan at the DEFAULT options the N-GPU bench runs (panel_nb_outer
+    # 1024, dist_cbb 1024, small_front_max 128): the 2327-wide root factored 1D
+    # slab-cyclic in three 1024-column slabs, split fronts with 1024-wide CB blocks;
+    # every rank emulated with private memory, messages as device copies or RCCL
+    # send/recv to self (dist.cpp transfer_group)
+    A, Lp, Li, Lx = lap48_oracle
+    s = sc.Symbolic(A)
+    assert s.opt.panel_nb_outer == 1024 and s.opt.dist_cbb == 1024
+    info = s.dist_plan_info(nranks)
+    assert info["slab_ranks"].max() >= 2
+    if nranks >= 4:
+        assert info["split_cb_ranks"].max() > 0
+    v = sc.Numeric(s, nranks=nranks, virtual=True, rccl_self=rccl)
+    for _ in range(2):
+        assert v.factor(A.x) == 0
+    _, L = v.export()
+    assert np.array_equal(L.p, Lp) and np.array_equal(L.i, Li)
+    err = rel_fro(L.x, Lx)
+    print(f"lap48 defaults, {nranks} emulated ranks, rccl={rccl}: rel-Fro {err:.3e}, "
+          f"{info['n_steps']} comm steps, {info['n_msgs']} messages")
+    assert err < TOL
+    b = np.random.default_rng(6).standard_normal(A.size())
+    x = v.solve(b)
+    assert _backward_error(A, x, b) < 1e-14
+
+
 def test_solve_after_failed_factor(gpu):
     A = sc.laplacian3d(6)
     A.x[A.p[5]:A.p[6]][-1] = -10.0  # diagonal of column 5 (last entry of an upper column)
