@@ -209,7 +209,8 @@ def main():
     num.set_profile(2 if args.graph else 1)
     for _ in range(max(args.warmup, 1 if args.graph else 0)):
         rc = num.factor_device(d_Ax.data_ptr(), sync=True)
-        assert rc == 0, f"factorization failed: {rc}"
+        # dry transport: received blocks hold stale values, a pivot may fail (not a factor)
+        assert rc == 0 or args.transport == "dry", f"factorization failed: {rc}"
 
     barrier()
     t0 = time.perf_counter()
@@ -219,7 +220,7 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     barrier()
-    assert rc == 0, f"factorization failed: {rc}"
+    assert rc == 0 or args.transport == "dry", f"factorization failed: {rc}"
     if dist is not None:
         tt = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)

@@ -45,7 +45,8 @@ enum sc_status {
     SC_ERR_STATE = -5,    /* call out of order (e.g. export before factor) */
     SC_ERR_COMM = -6,     /* RCCL / transport error */
     SC_ERR_NOTIMPL = -7,
-    SC_ERR_NOTSYM = -8    /* MatrixMarket input that is not symmetric (general / skew-symmetric) */
+    SC_ERR_NOTSYM = -8,   /* MatrixMarket input that is not symmetric (general / skew-symmetric) */
+    SC_ERR_IO = -9        /* file could not be opened */
 };
 
 typedef struct sc_symbolic sc_symbolic;
@@ -156,6 +157,14 @@ int64_t sc_factor(sc_numeric* num, const double* Ax);
 /* Factor with device-resident values d_Ax (HBM).  Asynchronous on the library
  * stream unless sync != 0; sc_numeric_status() syncs and returns the status. */
 int64_t sc_factor_device(sc_numeric* num, const double* d_Ax, int32_t sync);
+/* Status of the last factorization: 0, or the 1-based natural column of the failing
+ * pivot (not positive definite).  COLLECTIVE on a one-rank-per-process handle
+ * (sc_numeric_create_dist / _dist_host): the first call after each factorization
+ * reduces the minimum failing column over all ranks, so every rank must make it, in
+ * the same order relative to the handle's other collective calls -- and so must
+ * sc_factor, sc_factor_device(sync != 0), sc_export_L, sc_export_L_cols(rx != NULL)
+ * and the solves, which read the status.  A rank that skips it leaves the others
+ * waiting.  Later calls before the next factorization are local. */
 int64_t sc_numeric_status(sc_numeric* num);
 /* Export L in the reference CSC layout (chol() output, chol.hpp:749-863):
  * Lp[n+1], Li[nnz_L], Lx[nnz_L]; any of the three may be NULL.  On a multi-rank

@@ -267,7 +267,8 @@ csc_matrix<T, sym::upper> load_matrix_market_to_csc(const std::string& filename)
     int64_t nnz = sc_read_mtx(filename.c_str(), &n, nullptr, nullptr, nullptr);
     if (nnz == SC_ERR_NOTSYM) throw std::runtime_error("Matrix in " + filename + " is not symmetric");
     if (nnz == SC_ERR_NOTIMPL) throw std::runtime_error("Unsupported MatrixMarket format in " + filename);
-    if (nnz < 0) throw std::runtime_error("Could not open file " + filename);
+    if (nnz == SC_ERR_IO) throw std::runtime_error("Could not open file " + filename);
+    if (nnz < 0) throw std::runtime_error("Malformed MatrixMarket file " + filename);
     csc_matrix<T, sym::upper> A(static_cast<std::size_t>(n), static_cast<std::size_t>(n),
                                 static_cast<std::size_t>(nnz));
     std::vector<double> Ax(static_cast<std::size_t>(nnz));

@@ -54,7 +54,7 @@ SC_OK = 0
 _STATUS = {
     -1: "invalid argument", -2: "host allocation failed", -3: "HIP runtime error",
     -4: "device allocation failed", -5: "call out of order", -6: "communication error",
-    -7: "not implemented", -8: "matrix is not symmetric",
+    -7: "not implemented", -8: "matrix is not symmetric", -9: "file could not be opened",
 }
 
 

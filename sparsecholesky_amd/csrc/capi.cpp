@@ -55,6 +55,7 @@ const char* sc_status_string(int64_t st) {
         case SC_ERR_COMM: return "communication error";
         case SC_ERR_NOTIMPL: return "not implemented";
         case SC_ERR_NOTSYM: return "matrix is not symmetric";
+        case SC_ERR_IO: return "file could not be opened";
     }
     return "unknown status";
 }

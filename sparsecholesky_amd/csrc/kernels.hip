@@ -23,6 +23,13 @@ __device__ __forceinline__ void report_fail(int32_t* info, int32_t col_internal)
     atomicMin(info, col_internal + 1);
 }
 
+// g(k) of a child's compact block bounds (symbolic.cpp bounds()): [k_lo, k_hi, g(k_lo),
+// g(k_lo + 1) .. g(k_hi - 1)]; g = g(k_lo) at or below k_lo, mbc at or above k_hi
+__device__ __forceinline__ int bnd_at(const int32_t* b, int k, int mbc) {
+    const int klo = b[0], khi = b[1];
+    return k <= klo ? b[2] : (k >= khi ? mbc : b[2 + k - klo]);
+}
+
 // ---------------------------------------------------------------------------
 // Large fronts, assembly: one workgroup per (front, 64-column block).  Zeroes its
 // panel / CB columns, stores the A entries, then adds every child's CB entries
@@ -78,7 +85,7 @@ __global__ __launch_bounds__(256) void assemble_cols_kernel(DevPlan P, const int
         const int32_t* __restrict__ rel = P.relind + P.rel_ptr[c];
         const double* __restrict__ cb = P.cb_pool + P.cb_off[c];
         const int32_t* __restrict__ cbnd = P.col_bnd + P.cbk_ptr[c];  // j0 = t.y * ASM_COLS
-        const int jlo = cbnd[t.y], jhi = cbnd[t.y + 1];
+        const int jlo = bnd_at(cbnd, t.y, mbc), jhi = bnd_at(cbnd, t.y + 1, mbc);
         for (int jc = jlo + wid; jc < jhi; jc += 4) {
             const int pj = rel[jc];
             const double* __restrict__ src = cb + (int64_t)jc * mbc;
@@ -145,7 +152,8 @@ __global__ __launch_bounds__(256) void assemble_tile_kernel(DevPlan P, const int
             const int32_t* rel = P.relind + P.rel_ptr[c];
             const int32_t* bnd = P.rel_bnd + P.rb_ptr[c];
             const int32_t* cbnd = P.col_bnd + P.cbk_ptr[c];
-            const int ilo = bnd[k], ihi = bnd[k + 1], jlo = cbnd[jb], jhi = cbnd[jb + 1];
+            const int ilo = bnd_at(bnd, k, mbc), ihi = bnd_at(bnd, k + 1, mbc);
+            const int jlo = bnd_at(cbnd, jb, mbc), jhi = bnd_at(cbnd, jb + 1, mbc);
             int pj[ASM_COLS];
 #pragma unroll
             for (int l = 0; l < ASM_COLS; ++l) pj[l] = (jlo + l < jhi && ilo < ihi) ? rel[jlo + l] - j0 : -1;
@@ -773,9 +781,6 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
     __shared__ double2 S[TRSM64_STREAM / 2];
     __shared__ __attribute__((aligned(16))) double colbuf[2 * 4 * COLB];
     __shared__ int s_last;
-#if SC_CRIT_PRIO > 0
-    __builtin_amdgcn_s_setprio(SC_CRIT_PRIO);  // critical path: wins issue over co-resident SYRK waves
-#endif
     const int4 t = tasks[blockIdx.x];
     const int s = t.x, k0 = t.y, r0 = t.z;
     const int tid = threadIdx.x;
@@ -854,10 +859,6 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
 // c = w (mod waves), so children add in their fixed order with no atomics and no
 // barrier per child (deterministic).  A child's CB rows that land in a 64-row block
 // of the parent's CB are one contiguous run (relind is increasing): tile_bnd.
-__device__ __forceinline__ int tile_bnd_at(const int32_t* tb, int k, int mbc) {
-    const int klo = tb[0], khi = tb[1];
-    return k <= klo ? tb[2] : (k >= khi ? mbc : tb[3 + k - klo - 1]);
-}
 // wave-uniform values kept in SGPRs (the child loop is uniform; without this the
 // compiler keeps its counters in VGPRs and branches per lane)
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -897,8 +898,8 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const De
                 const int c = uni(P.child_list[ci]);
                 const int mbc = uni(P.sn_m[c] - (P.sn_start[c + 1] - P.sn_start[c]));
                 const int32_t* tb = uni_ptr(P.tile_bnd + P.tb_ptr[c]);
-                const int ilo = uni(tile_bnd_at(tb, r0 / GR, mbc)), ihi = uni(tile_bnd_at(tb, r0 / GR + 1, mbc));
-                const int jlo = uni(tile_bnd_at(tb, col0 / GR, mbc)), jhi = uni(tile_bnd_at(tb, (col0 + BT) / GR, mbc));
+                const int ilo = uni(bnd_at(tb, r0 / GR, mbc)), ihi = uni(bnd_at(tb, r0 / GR + 1, mbc));
+                const int jlo = uni(bnd_at(tb, col0 / GR, mbc)), jhi = uni(bnd_at(tb, (col0 + BT) / GR, mbc));
                 if (ilo >= ihi || jlo >= jhi) continue;
                 const int32_t* __restrict__ rel = uni_ptr(P.relind + P.rel_ptr[c]);
                 const double* __restrict__ cb = uni_ptr(P.cb_pool + P.cb_off[c]);
@@ -979,12 +980,6 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
     const int wr = wid / WN, wc = wid % WN;
     // static priority for the second-dispatched half of the waves (the arbitration loser
     // on every segment of two co-resident waves per SIMD): 547.8-548.5 -> 544.6-546.0 ms
-#if SC_CRIT_PRIO > 0
-    // main-stream panel updates (TAG 0, EPI 1) are the critical path: above every co-resident SYRK wave
-    if (TAG == 0 && EPI == 1)
-        __builtin_amdgcn_s_setprio(SC_CRIT_PRIO - 1);
-    else
-#endif
     if (wid >= WM * WN / 2) __builtin_amdgcn_s_setprio(1);
     const double* __restrict__ A = T.A;
     const int64_t lda = T.lda;
@@ -1119,13 +1114,6 @@ __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask*
     syrk_tile_body<BT, WM, WN, TAG, EPI>(tasks, tiles, blockIdx.x, plans);
 }
 
-// Capped grid (lookahead-stream updates): workgroup b takes tiles b, b + grid, ...
-// (grid a multiple of 8, so every tile keeps the XCD the host ordered it for).
-template <int BT, int WM, int WN>
-__global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_loop_kernel(const GemmTask* __restrict__ tasks,
-                                                                       const int2* __restrict__ tiles, int ntiles) {
-    for (int bt = blockIdx.x; bt < ntiles; bt += gridDim.x) syrk_tile_body<BT, WM, WN, 0, 0>(tasks, tiles, bt, nullptr);
-}
 
 // ---------------------------------------------------------------------------
 // Launch wrappers
@@ -1192,15 +1180,8 @@ hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hip
 // bt = 64: 64x64 tiles on 4 waves (2x2); bt = 128: 128x128 tiles on 8 waves (2x4).
 // epi: epilogue with its C loads in flight together (see the kernel).
 template <int TAG, int EPI>
-static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int grid, int bt, hipStream_t st,
+static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int bt, hipStream_t st,
                           const DevPlan* plans) {
-    if (TAG == 0 && EPI == 0 && grid < n) {
-        if (bt == 128)
-            hipLaunchKernelGGL((syrk_mfma_loop_kernel<128, 2, 4>), dim3(grid), dim3(512), 0, st, tasks, tiles, n);
-        else
-            hipLaunchKernelGGL((syrk_mfma_loop_kernel<64, 2, 2>), dim3(grid), dim3(256), 0, st, tasks, tiles, n);
-        return;
-    }
     if (bt == 128)
         hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, EPI>), dim3(n), dim3(512), 0, st, tasks, tiles, plans);
     else
@@ -1208,17 +1189,14 @@ static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int g
 }
 
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
-                       int epi, int max_grid, const DevPlan* plans) {
+                       int epi, const DevPlan* plans) {
     if (total_tiles <= 0) return hipSuccess;
-    // max_grid > 0 (a multiple of 8; panel updates without the batched epilogue): at
-    // most that many workgroups, each looping over tiles
-    const int grid = (max_grid > 0 && total_tiles > max_grid && !tag && !epi) ? max_grid : total_tiles;
     if (tag)
-        epi ? launch_syrk_t<1, 1>(tasks, tiles, total_tiles, grid, bt, st, plans)
-            : launch_syrk_t<1, 0>(tasks, tiles, total_tiles, grid, bt, st, plans);
+        epi ? launch_syrk_t<1, 1>(tasks, tiles, total_tiles, bt, st, plans)
+            : launch_syrk_t<1, 0>(tasks, tiles, total_tiles, bt, st, plans);
     else
-        epi ? launch_syrk_t<0, 1>(tasks, tiles, total_tiles, grid, bt, st, plans)
-            : launch_syrk_t<0, 0>(tasks, tiles, total_tiles, grid, bt, st, plans);
+        epi ? launch_syrk_t<0, 1>(tasks, tiles, total_tiles, bt, st, plans)
+            : launch_syrk_t<0, 0>(tasks, tiles, total_tiles, bt, st, plans);
     return hipGetLastError();
 }
 

@@ -24,18 +24,9 @@ constexpr int SYRK_BT_LARGE = 128;
 // section 3): col = lane & 15, row = (lane >> 4) + 4 * reg.
 #define MFMA_F64_ROW(lane, r) (((lane) >> 4) + 4 * (r))
 
-// s_setprio of the critical-path kernels (fused POTRF/TRSM: this value; main-stream
-// panel updates: one less); 0 = off
-#ifndef SC_CRIT_PRIO
-#define SC_CRIT_PRIO 0
-#endif
 // child columns per batch of loads in the CB SYRK's extend-add gather
 #ifndef SC_GATHER_Q
 #define SC_GATHER_Q 4
-#endif
-// workgroups of a lookahead-stream panel update (0 = one per tile)
-#ifndef SC_LA_GRID
-#define SC_LA_GRID 0
 #endif
 
 // All device arrays of the numeric plan (internal numbering).
@@ -183,9 +174,9 @@ hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hip
 // per-block arrival counters, zeroed; task .w - 1 indexes them)
 hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st, bool partial,
                              int32_t* arrive);
-// max_grid > 0 (a multiple of 8): at most that many workgroups, each looping over tiles
+// plans: the hosted ranks' DevPlans (CB tasks with gs >= 0 gather their children's entries)
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
-                       int epi = 0, int max_grid = 0, const DevPlan* plans = nullptr);
+                       int epi = 0, const DevPlan* plans = nullptr);
 hipError_t launch_stamp(uint64_t* slot, hipStream_t st);
 hipError_t launch_fill_random(double* p, int64_t n, hipStream_t st);
 hipError_t launch_mfma_peak(double* out, int blocks, int iters, int nacc, hipStream_t st);

@@ -1192,7 +1192,7 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
         case L_PANEL:
         case L_CB:
             return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st, L.epi,
-                               (L.kind == L_PANEL && L.strm == 1) ? SC_LA_GRID : 0, N.d_plans);
+                               N.d_plans);
         case L_COMM:
             return comm_launch(N, L);
     }

@@ -62,16 +62,18 @@ i64 triplet_to_csc(i64 n, i64 nt, const i32* ti, const i32* tj, const double* tx
 // Here the banner "%%MatrixMarket matrix <format> <field> <symmetry>" decides:
 //   coordinate only (array: SC_ERR_NOTIMPL); field real / integer / pattern
 //   (pattern: value 1; complex: SC_ERR_NOTIMPL);
-//   symmetric, hermitian (real field) or no banner -> as the reference;
+//   symmetric, hermitian (real field), no symmetry token or no banner -> as the
+//     reference (every entry swapped to the upper triangle);
 //   general -> the file must hold both triangles of a symmetric matrix: after
 //     summing duplicates, every off-diagonal (r, c) must equal (c, r) exactly,
 //     else SC_ERR_NOTSYM; only the upper entries are kept (the reference's swap
 //     would add each mirror onto its twin and double the off-diagonal);
 //   skew-symmetric -> SC_ERR_NOTSYM (zero diagonal: never positive definite).
-// Indices out of [1, n], a non-square size or a short file: SC_ERR_ARG.
+// Indices out of [1, n], a non-square size or a short file: SC_ERR_ARG; a file that
+// cannot be opened: SC_ERR_IO.
 i64 read_mtx(const char* path, i64* n_out, i64* Ap, i32* Ai, double* Ax) {
     std::ifstream f(path);
-    if (!f) return SC_ERR_ARG;
+    if (!f) return SC_ERR_IO;
     std::string line;
     bool pattern = false, general = false;
     if (!std::getline(f, line)) return SC_ERR_ARG;
@@ -94,7 +96,7 @@ i64 read_mtx(const char* path, i64* n_out, i64* Ap, i32* Ai, double* Ax) {
                 general = true;
             else if (symmetry == "skew-symmetric")
                 return SC_ERR_NOTSYM;
-            else if (symmetry != "symmetric" && symmetry != "hermitian")
+            else if (!symmetry.empty() && symmetry != "symmetric" && symmetry != "hermitian")
                 return SC_ERR_ARG;
         } else {
             f.seekg(0);

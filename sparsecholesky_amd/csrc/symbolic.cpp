@@ -400,53 +400,35 @@ i64 analyze(i64 n, const i64* Ap, const i32* Ai, const sc_options& opt, Symbolic
                 S.a_pos[q] = pos[a_row[q]];
     }
     S.relind.resize((size_t)S.rel_ptr[ns]);
-    S.rb_ptr.assign((size_t)ns + 1, 0);
-    S.rel_bnd.clear();
-    for (i32 s = 0; s < ns; ++s) {
-        const i32 p = S.sn_parent[s];
-        if (p >= 0) {
-            const i32 nk = (S.sn_m[p] + kAsmRows - 1) / kAsmRows;
-            const i32* rel = S.relind.data() + S.rel_ptr[s];
-            const i32 mbc = (i32)(S.rel_ptr[s + 1] - S.rel_ptr[s]);
-            for (i32 k = 0; k <= nk; ++k)
-                S.rel_bnd.push_back((i32)(std::lower_bound(rel, rel + mbc, k * kAsmRows) - rel));
+    // per child, bounds of its CB rows by blocks of the parent front (the large-front
+    // assembly and the CB SYRK's gather read them instead of binary-searching relind):
+    // g(k) = first CB row whose parent position is >= base + k * blk, stored compactly
+    // over the blocks the child touches: [k_lo, k_hi, g(k_lo), g(k_lo + 1) .. g(k_hi - 1)]
+    // (g = g(k_lo) below k_lo, mbc from k_hi; kernels.hip bnd_at)
+    auto bounds = [&](std::vector<i64>& ptr, std::vector<i32>& out, int blk, bool cb_only) {
+        ptr.assign((size_t)ns + 1, 0);
+        out.clear();
+        for (i32 s = 0; s < ns; ++s) {
+            const i32 p = S.sn_parent[s];
+            if (p >= 0) {
+                const i32 base = cb_only ? S.w(p) : 0;
+                const i32* rel = S.relind.data() + S.rel_ptr[s];
+                const i32 mbc = (i32)(S.rel_ptr[s + 1] - S.rel_ptr[s]);
+                const i32 j0 = (i32)(std::lower_bound(rel, rel + mbc, base) - rel);
+                const i32 klo = j0 < mbc ? (rel[j0] - base) / blk : 0;
+                const i32 khi = j0 < mbc ? (rel[mbc - 1] - base) / blk + 1 : 0;
+                out.push_back(klo);
+                out.push_back(khi);
+                out.push_back(j0);
+                for (i32 k = klo + 1; k < khi; ++k)
+                    out.push_back((i32)(std::lower_bound(rel, rel + mbc, base + blk * k) - rel));
+            }
+            ptr[s + 1] = (i64)out.size();
         }
-        S.rb_ptr[s + 1] = (i64)S.rel_bnd.size();
-    }
-    // per child, the CB rows of each ASM_COLS-column block of its parent (the large-front
-    // assembly kernels read them instead of binary-searching relind)
-    S.cbk_ptr.assign((size_t)ns + 1, 0);
-    S.col_bnd.clear();
-    for (i32 s = 0; s < ns; ++s) {
-        const i32 p = S.sn_parent[s];
-        if (p >= 0) {
-            const i32 nb = (S.sn_m[p] + kAsmCols - 1) / kAsmCols;
-            const i32* rel = S.relind.data() + S.rel_ptr[s];
-            const i32 mbc = (i32)(S.rel_ptr[s + 1] - S.rel_ptr[s]);
-            for (i32 b = 0; b <= nb; ++b)
-                S.col_bnd.push_back((i32)(std::lower_bound(rel, rel + mbc, b * kAsmCols) - rel));
-        }
-        S.cbk_ptr[s + 1] = (i64)S.col_bnd.size();
-    }
-    S.tb_ptr.assign((size_t)ns + 1, 0);
-    S.tile_bnd.clear();
-    for (i32 s = 0; s < ns; ++s) {
-        const i32 p = S.sn_parent[s];
-        if (p >= 0) {
-            const i32 wp = S.w(p);
-            const i32* rel = S.relind.data() + S.rel_ptr[s];
-            const i32 mbc = (i32)(S.rel_ptr[s + 1] - S.rel_ptr[s]);
-            const i32 j0 = (i32)(std::lower_bound(rel, rel + mbc, wp) - rel);
-            const i32 klo = j0 < mbc ? (rel[j0] - wp) / 64 : 0;
-            const i32 khi = j0 < mbc ? (rel[mbc - 1] - wp) / 64 + 1 : 0;
-            S.tile_bnd.push_back(klo);
-            S.tile_bnd.push_back(khi);
-            S.tile_bnd.push_back(j0);
-            for (i32 k = klo + 1; k < khi; ++k)
-                S.tile_bnd.push_back((i32)(std::lower_bound(rel, rel + mbc, wp + 64 * k) - rel));
-        }
-        S.tb_ptr[s + 1] = (i64)S.tile_bnd.size();
-    }
+    };
+    bounds(S.rb_ptr, S.rel_bnd, kAsmRows, false);   // assembly row tiles
+    bounds(S.cbk_ptr, S.col_bnd, kAsmCols, false);  // assembly column blocks
+    bounds(S.tb_ptr, S.tile_bnd, 64, true);         // 64-row blocks of the parent's CB
     S.child_ptr.assign((size_t)ns + 1, 0);
     S.child_list.clear();
     for (i32 s = 0; s < ns; ++s) {

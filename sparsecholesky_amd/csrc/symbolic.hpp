@@ -72,16 +72,14 @@ struct Symbolic {
     std::vector<i32> child_list;
     std::vector<i64> rel_ptr;    // ns+1, CB row -> position in parent front
     std::vector<i32> relind;
-    // per child: first CB row whose parent position is >= k * kAsmRows, for
-    // k = 0 .. ceil(m_parent / kAsmRows) (the assembly's row tiles)
+    // per child: bounds of its CB rows by blocks of the parent front, compact over the
+    // blocks it touches (symbolic.cpp bounds(), kernels.hip bnd_at): the assembly's
+    // kAsmRows-row tiles (rel_bnd), kAsmCols-column blocks (col_bnd), and the 64-row
+    // blocks of the parent's contribution block (tile_bnd, the CB SYRK's extend-add gather)
     std::vector<i64> rb_ptr;     // ns+1
     std::vector<i32> rel_bnd;
     std::vector<i64> cbk_ptr;    // ns+1
-    std::vector<i32> col_bnd;    // per child: CB rows of the parent's kAsmCols-column blocks
-    // per child: its CB rows in the parent's contribution block, by 64-row blocks of the
-    // parent's CB (the CB SYRK's extend-add gather, kernels.hip syrk_gather): g(k) = first
-    // CB row whose parent position is >= w_parent + 64 k, stored compactly as
-    // [k_lo, k_hi, g(k_lo), g(k_lo + 1) .. g(k_hi - 1)] (g = g(k_lo) below k_lo, mbc from k_hi)
+    std::vector<i32> col_bnd;
     std::vector<i64> tb_ptr;     // ns+1
     std::vector<i32> tile_bnd;
     std::vector<i64> panel_off;  // ns+1 (doubles), L panel m x w, ld = m

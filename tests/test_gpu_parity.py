@@ -305,7 +305,8 @@ def lap48_oracle():
     return A, Lp, Li, Lx
 
 
-@pytest.mark.parametrize("opts", [{}, dict(asm_tile_min_m=1024)], ids=["default", "tiled_asm"])
+@pytest.mark.parametrize("opts", [{}, dict(asm_tile_min_m=1024), dict(cb_gather=0)],
+                         ids=["default", "tiled_asm", "assembled_cb"])
 def test_lap48_full_parity(gpu, lap48_oracle, opts):
     # the whole 48^3 factor (n = 110592, F = 7.07e10: a 2304-wide root, CB SYRK with K
     # up to 1152 on 128 x 128 tiles) against the oracle, exact pattern and rel-Fro;
@@ -348,6 +349,35 @@ def test_partitioned_defaults_lap48(gpu, lap48_oracle, nranks, rccl):
     b = np.random.default_rng(6).standard_normal(A.size())
     x = v.solve(b)
     assert _backward_error(A, x, b) < 1e-14
+
+
+@pytest.fixture(scope="module")
+def lap64_oracle():
+    # F = 4.15e11: about 90-100 s of the single-threaded oracle on the GPU box's host
+    A = sc.laplacian3d(64)
+    st, Lp, Li, Lx = oracle.chol(A)
+    assert st == 0
+    return A, Lp, Li, Lx
+
+
+@pytest.mark.parametrize("opts", [{}, dict(asm_tile_min_m=1024)], ids=["default", "tiled_asm"])
+def test_lap64_full_parity(gpu, lap64_oracle, opts):
+    # the whole 64^3 factor (n = 262144, F = 4.15e11) against the oracle: a root of about
+    # 4096 columns in four 1024-column slabs (lookahead-stream outer updates, recursive
+    # inner updates), CB SYRK with K ~ 2048 into ~4096-wide contribution blocks with the
+    # children's entries gathered per tile -- the shapes that carry most of the 128^3
+    # flops (levels 14-18); exact pattern and rel-Fro < 1e-12
+    A, Lp, Li, Lx = lap64_oracle
+    s = sc.Symbolic(A, **opts)
+    st = s.stats()
+    assert st["max_front_w"] >= 3072
+    num = sc.Numeric(s)
+    assert num.factor(A.x) == 0
+    _, L = num.export()
+    assert np.array_equal(L.p, Lp) and np.array_equal(L.i, Li)
+    err = rel_fro(L.x, Lx)
+    print(f"lap64 {opts}: max front w {st['max_front_w']}, m {st['max_front_m']}, rel-Fro {err:.3e}")
+    assert err < TOL
 
 
 def test_solve_after_failed_factor(gpu):

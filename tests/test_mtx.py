@@ -63,5 +63,16 @@ def test_rejected_inputs(name, code):
 
 
 def test_missing_file():
-    with pytest.raises(sc.LibraryError, match="invalid argument"):
+    with pytest.raises(sc.LibraryError, match="could not be opened"):
         load("does_not_exist.mtx")
+
+
+def test_banner_without_symmetry_token(readme5, tmp_path):
+    # "%%MatrixMarket matrix coordinate real" with no symmetry token: the reference
+    # reads every header the same way (mtx_reader.hpp:26-27) and swaps each entry to
+    # the upper triangle, so this is the symmetric form
+    src = open(os.path.join(HERE, "readme5_integer_hermitian.mtx")).read().splitlines()
+    body = [l for l in src[1:]]
+    p = tmp_path / "nosym.mtx"
+    p.write_text("%%MatrixMarket matrix coordinate real\n" + "\n".join(body) + "\n")
+    assert same(sc.load_matrix_market_to_csc(str(p)), readme5)
