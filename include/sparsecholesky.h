@@ -88,6 +88,11 @@ typedef struct sc_options {
     int32_t cb_gather;       /* 1 (default): a large front's contribution block is not assembled; its CB SYRK
                                 gathers the children's entries into each output tile (C = sum - L21 L21^T,
                                 written once); 0: assembly writes the whole front, the SYRK updates it */
+    int32_t panel_tall;      /* 1: in a large front wider than 64 columns the 64-column POTRF/TRSM chain runs on
+                                each slab's diagonal-block rows only and the rows below the slab are solved by
+                                one tall-TRSM launch per slab (row blocks, MFMA, block inverses); 0 (default,
+                                measured faster at 128^3: 512 vs 541 ms): every chain step solves and updates
+                                all rows of the front */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

@@ -6,7 +6,7 @@ while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   d=gpurun_var/$name
   rm -rf "$d"; mkdir -p "$d/profiles/r02" "$d/oracle"
-  cp bench.py "$d/"
+  cp bench.py "$d/"; mkdir -p "$d/scripts"; cp scripts/panel_breakdown.py "$d/scripts/"
   cp profiles/r02/pmc_summary.json profiles/r02/mfma_util.json "$d/profiles/r02/"
   mkdir -p "$d/sparsecholesky_amd"
   cp sparsecholesky_amd/__init__.py "$d/sparsecholesky_amd/"

@@ -755,15 +755,15 @@ __device__ __forceinline__ void trsm_partial(double* pan, int m, int k0, int nb,
 
 // Partial last blocks (nb < 64) of the panel TRSM, launched separately so the
 // full-block kernels keep their own register budgets.  Rows [r0, r0 + nrows).
-__global__ __launch_bounds__(TRSM_ROWS) void trsm_partial_kernel(DevPlan P, const int4* __restrict__ tasks, int nrows) {
+__global__ __launch_bounds__(TRSM_ROWS) void trsm_partial_kernel(DevPlan P, const TrsmTask* __restrict__ tasks) {
     __shared__ double Lc[PNB * (PNB + 2)];
     __shared__ double invd[PNB];
-    const int4 t = tasks[blockIdx.x];
-    const int s = t.x, k0 = t.y, r0 = t.z;
+    const TrsmTask t = tasks[blockIdx.x];
+    const int s = t.s, k0 = t.k0, r0 = t.r0;
     const int c0 = P.sn_start[s];
     const int w = P.sn_start[s + 1] - c0;
     const int m = P.sn_m[s];
-    trsm_partial(P.panel_pool + P.panel_off[s], m, k0, min(PNB, w - k0), r0, nrows, Lc, invd);
+    trsm_partial(P.panel_pool + P.panel_off[s], m, k0, min(PNB, w - k0), r0, min(TRSM_ROWS, t.r1 - r0), Lc, invd);
 }
 
 // Diagonal block POTRF fused with the panel TRSM, rows [r0, r0 + TRSM_ROWS): every
@@ -775,14 +775,14 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_partial_kernel(DevPlan P, cons
 // every workgroup of the block has read it: t.w - 1 indexes the block's arrival
 // counter, and the last workgroup to arrive stores L11 and rearms the counter.  A
 // block with no rows below gets one task with r0 >= m (factor and store only).
-__global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, const int4* __restrict__ tasks,
+__global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, const TrsmTask* __restrict__ tasks,
                                                                  int32_t* __restrict__ arrive) {
     static_assert(TRSM_ROWS == 256, "the fused POTRF maps 4 x 4 tiles onto 256 threads");
     __shared__ double2 S[TRSM64_STREAM / 2];
     __shared__ __attribute__((aligned(16))) double colbuf[2 * 4 * COLB];
     __shared__ int s_last;
-    const int4 t = tasks[blockIdx.x];
-    const int s = t.x, k0 = t.y, r0 = t.z;
+    const TrsmTask t = tasks[blockIdx.x];
+    const int s = t.s, k0 = t.k0, r0 = t.r0, r1 = t.r1;
     const int tid = threadIdx.x;
     const int c0 = P.sn_start[s];
     const int w = P.sn_start[s + 1] - c0;
@@ -814,17 +814,17 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
     const int row = r0 + tid;
     // the 64 block columns, m rows each (< 2^31 bytes for m < 4M); dead lanes masked
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pan + (int64_t)k0 * m, (uint32_t)m * PNB * 8u);
-    const int voff = row < m ? row * 8 : BUF_DEAD;
+    const int voff = row < r1 ? row * 8 : BUF_DEAD;
     double r[PNB];
 #pragma unroll
     for (int c = 0; c < PNB; ++c) r[c] = buf_ld(rs, voff, c * m * 8);
     __syncthreads();
     if (tid == 0) {
         const int k1 = k0 + PNB;
-        const int nwg = (max(m, k1 + 1) - k1 + TRSM_ROWS - 1) / TRSM_ROWS;
-        const int old = __hip_atomic_fetch_add(arrive + (t.w - 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int nwg = (max(r1, k1 + 1) - k1 + TRSM_ROWS - 1) / TRSM_ROWS;
+        const int old = __hip_atomic_fetch_add(arrive + (t.ctr - 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = old == nwg - 1;
-        if (old == nwg - 1) __hip_atomic_store(arrive + (t.w - 1), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == nwg - 1) __hip_atomic_store(arrive + (t.ctr - 1), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (s_last && R.bi[0] >= 0) {
@@ -875,8 +875,12 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const De
     constexpr int NW = WM * WN, NT = 64 * NW;
     constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
     constexpr int GR = 64, GLD = GR + 1;  // rows per chunk, LDS column stride (doubles)
-    constexpr int GQ = SC_GATHER_Q;       // child columns per batch of loads (VGPR budget: 4 waves / SIMD)
-    static_assert(BT * GLD * 8 <= 2 * 2 * 16 * (BT + 16) * 8, "gather chunk fits the operand LDS");
+    // child columns per batch of loads: all of a wave's <= 64 / NW columns per child for
+    // 64-tiles; 4 for 128-tiles (VGPR budget: 4 waves / SIMD)
+    constexpr int GQ = BT == 64 ? 64 / NW : SC_GATHER_Q;
+    constexpr int GC = 64;  // children staged per pass (one lane each)
+    constexpr int OPS = 2 * 2 * 16 * (BT + 16);  // the operand stages' doubles (smem)
+    static_assert(BT * GLD + GC * 6 <= OPS, "gather chunk and child table fit the operand LDS");
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wr = wid / WN, wc = wid % WN;
     const int s = T.gs;
@@ -884,6 +888,11 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const De
     const int mb = T.M;
     const int cp0 = uni(P.child_ptr[s]), cp1 = uni(P.child_ptr[s + 1]);
     double* G = smem;
+    // child table (one entry per staged child): CB base, relind base, then mbc and the
+    // bounds of its CB rows in this chunk's rows and in the tile's columns
+    const double** s_cb = reinterpret_cast<const double**>(smem + BT * GLD);
+    const int32_t** s_rel = reinterpret_cast<const int32_t**>(smem + BT * GLD + GC);
+    int32_t* s_int = reinterpret_cast<int32_t*>(smem + BT * GLD + 2 * GC);  // [5][GC]
     double* __restrict__ C = T.C;
     const int64_t ldc = T.ldc;
     const __amdgpu_buffer_rsrc_t rc = buf_rsrc(C + (int64_t)col0 * ldc, (uint32_t)(min(BT, T.N - col0) * ldc * 8));
@@ -892,17 +901,29 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const De
         const int r0 = row0 + h * GR;  // CB rows of this chunk: [r0, r0 + 64)
         if (h) __syncthreads();        // previous chunk's G fully read
         for (int e = tid; e < BT * GLD; e += NT) G[e] = 0.0;
-        __syncthreads();
-        if (r0 < mb) {
-            for (int ci = cp0; ci < cp1; ++ci) {
-                const int c = uni(P.child_list[ci]);
-                const int mbc = uni(P.sn_m[c] - (P.sn_start[c + 1] - P.sn_start[c]));
-                const int32_t* tb = uni_ptr(P.tile_bnd + P.tb_ptr[c]);
-                const int ilo = uni(bnd_at(tb, r0 / GR, mbc)), ihi = uni(bnd_at(tb, r0 / GR + 1, mbc));
-                const int jlo = uni(bnd_at(tb, col0 / GR, mbc)), jhi = uni(bnd_at(tb, (col0 + BT) / GR, mbc));
+        for (int cbase = cp0;; cbase += GC) {
+            const int nc = min(GC, cp1 - cbase);
+            // one lane per child: every child's metadata loads in flight together
+            if (wid == 0 && lane < nc) {
+                const int c = P.child_list[cbase + lane];
+                const int mbc = P.sn_m[c] - (P.sn_start[c + 1] - P.sn_start[c]);
+                const int32_t* tb = P.tile_bnd + P.tb_ptr[c];
+                s_cb[lane] = P.cb_pool + P.cb_off[c];
+                s_rel[lane] = P.relind + P.rel_ptr[c];
+                s_int[0 * GC + lane] = mbc;
+                s_int[1 * GC + lane] = bnd_at(tb, r0 / GR, mbc);
+                s_int[2 * GC + lane] = bnd_at(tb, r0 / GR + 1, mbc);
+                s_int[3 * GC + lane] = bnd_at(tb, col0 / GR, mbc);
+                s_int[4 * GC + lane] = bnd_at(tb, (col0 + BT) / GR, mbc);
+            }
+            __syncthreads();
+            for (int i = 0; r0 < mb && i < nc; ++i) {
+                const int ilo = uni(s_int[1 * GC + i]), ihi = uni(s_int[2 * GC + i]);
+                const int jlo = uni(s_int[3 * GC + i]), jhi = uni(s_int[4 * GC + i]);
                 if (ilo >= ihi || jlo >= jhi) continue;
-                const int32_t* __restrict__ rel = uni_ptr(P.relind + P.rel_ptr[c]);
-                const double* __restrict__ cb = uni_ptr(P.cb_pool + P.cb_off[c]);
+                const int mbc = uni(s_int[i]);
+                const int32_t* __restrict__ rel = uni_ptr(s_rel[i]);
+                const double* __restrict__ cb = uni_ptr(s_cb[i]);
                 // this lane's row of the chunk (<= 64 child rows map into 64 parent rows)
                 const int ic = ilo + lane;
                 const int prow = ic < ihi ? rel[ic] - w - r0 : -1;
@@ -933,6 +954,8 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const De
                     }
                 }
             }
+            if (cbase + GC >= cp1) break;
+            __syncthreads();  // the child table is restaged
         }
         __syncthreads();
         // the waves whose MFMA rows lie in this chunk (a wave's BT / WM <= 64 rows sit in
@@ -954,42 +977,27 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const De
                     }
         }
     }
-    __syncthreads();  // G fully read before the workgroup's next tile stages operands
 }
 
-template <int BT, int WM, int WN, int TAG, int EPI>
-__device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ tasks, const int2* __restrict__ tiles,
-                                               int bidx, const DevPlan* __restrict__ plans) {
+// The MFMA K loop of one BT x BT output tile: acc += A[row0 + i, :] A[col0 + j, :]^T
+// over k < K (A column-major, ld lda; rows past M (i) / N (j) read as 0).  BK = 16,
+// register-staged double-buffered LDS (As / Bs: 2 stages of BK x (BT + 16) doubles
+// each, +128 B row pad: the two k-rows read by a half-wave hit disjoint banks).
+// AGLC: the row0 operand is loaded with glc (L1 bypassed: rows this workgroup
+// itself stored earlier in the same launch).
+template <int BT, int WM, int WN, int AGLC = 0>
+__device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t lda, int K, int M, int N, int row0,
+                                           int col0, double4_t (&acc)[BT / WM / 16][BT / WN / 16], double* smem) {
     constexpr int NT = 64 * WM * WN;
     constexpr int BK = 16;
-    constexpr int LDT = BT + 16;  // +128 B row pad: the two k-rows read by a half-wave hit disjoint banks
+    constexpr int LDT = BT + 16;
     constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
-    __shared__ double smem[2 * 2 * BK * LDT];  // A and B stages
     double(*As)[BK * LDT] = reinterpret_cast<double(*)[BK * LDT]>(smem);
     double(*Bs)[BK * LDT] = reinterpret_cast<double(*)[BK * LDT]>(smem + 2 * BK * LDT);
-
-    // host-ordered tile list: blocks sharing an XCD walk a contiguous, L2-blocked run of tiles
-    const int2 tl = tiles[bidx];
-    const GemmTask T = tasks[tl.x];
-    const int ti = tl.y >> 16, tj = tl.y & 0xffff;
-    const int row0 = ti * BT, col0 = tj * BT;
-
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = tid >> 6;
     const int wr = wid / WN, wc = wid % WN;
-    // static priority for the second-dispatched half of the waves (the arbitration loser
-    // on every segment of two co-resident waves per SIMD): 547.8-548.5 -> 544.6-546.0 ms
-    if (wid >= WM * WN / 2) __builtin_amdgcn_s_setprio(1);
-    const double* __restrict__ A = T.A;
-    const int64_t lda = T.lda;
-
-    double4_t acc[RTM][RTN];
-#pragma unroll
-    for (int a = 0; a < RTM; ++a)
-#pragma unroll
-        for (int b = 0; b < RTN; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
-
     // staging: BK x BT doubles per operand over NT threads
     constexpr int PER = BT * BK / NT;
     // Operands through a per-stage buffer resource (columns k0 .. k0 + BK of A):
@@ -998,14 +1006,18 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
     // also wait for the next stage's prefetch (flat loads count both).
     double ra[PER], rb[PER];
     auto gload = [&](int k0) {
-        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(A + (int64_t)k0 * lda, (uint32_t)(min(BK, T.K - k0) * lda * 8));
+        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(A + (int64_t)k0 * lda, (uint32_t)(min(BK, K - k0) * lda * 8));
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
             const int e = tid + q * NT;
             const int r = e % BT, kk = e / BT;
             const int gr = row0 + r, gc = col0 + r;
-            ra[q] = buf_ld(rs, gr < T.M ? (int)((gr + kk * lda) * 8) : BUF_DEAD, 0);
-            rb[q] = buf_ld(rs, gc < T.N ? (int)((gc + kk * lda) * 8) : BUF_DEAD, 0);
+            const int va = gr < M ? (int)((gr + kk * lda) * 8) : BUF_DEAD;
+            if constexpr (AGLC)
+                ra[q] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, va, 0, 1));
+            else
+                ra[q] = buf_ld(rs, va, 0);
+            rb[q] = buf_ld(rs, gc < N ? (int)((gc + kk * lda) * 8) : BUF_DEAD, 0);
         }
     };
     auto sstore = [&](int buf) {
@@ -1018,7 +1030,7 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
         }
     };
 
-    const int nk = (T.K + BK - 1) / BK;
+    const int nk = (K + BK - 1) / BK;
     gload(0);
     sstore(0);
     __syncthreads();
@@ -1055,6 +1067,36 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
         }
         __syncthreads();
     }
+}
+
+template <int BT, int WM, int WN, int TAG, int EPI>
+__device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ tasks, const int2* __restrict__ tiles,
+                                               int bidx, const DevPlan* __restrict__ plans) {
+    constexpr int BK = 16;
+    constexpr int LDT = BT + 16;
+    constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
+    __shared__ double smem[2 * 2 * BK * LDT];  // A and B stages
+
+    // host-ordered tile list: blocks sharing an XCD walk a contiguous, L2-blocked run of tiles
+    const int2 tl = tiles[bidx];
+    const GemmTask T = tasks[tl.x];
+    const int ti = tl.y >> 16, tj = tl.y & 0xffff;
+    const int row0 = ti * BT, col0 = tj * BT;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    const int wr = wid / WN, wc = wid % WN;
+    // static priority for the second-dispatched half of the waves (the arbitration loser
+    // on every segment of two co-resident waves per SIMD): 547.8-548.5 -> 544.6-546.0 ms
+    if (wid >= WM * WN / 2) __builtin_amdgcn_s_setprio(1);
+
+    double4_t acc[RTM][RTN];
+#pragma unroll
+    for (int a = 0; a < RTM; ++a)
+#pragma unroll
+        for (int b = 0; b < RTN; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
+    mfma_kloop<BT, WM, WN>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
 
     if constexpr (TAG == 1) {
         if (T.gs >= 0) {  // the front's CB is not assembled: gather the children's entries
@@ -1115,6 +1157,100 @@ __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask*
 }
 
 
+// Tall TRSM of a slab (the reference's cblas_dtrsm, chol.hpp:1292, for the rows below
+// a slab's diagonal block): rows [r0, r0 + 64) of front s against the slab's factored
+// diagonal block L_kk (columns [a, b)), in place, X = A L_kk^-T.  Per 64-column block j:
+//   Y = A(:, j) - X(:, < j) L(j, < j)^T   (MFMA, K = 64 j; X from this workgroup's own
+//                                           earlier stores, loaded with glc)
+//   X(:, j) = Y inv(L_jj)^T                (MFMA, K = 64; inv(L_jj) in the block's strict
+//                                           upper triangle, panel_inv / solve_inv_kernel)
+// A workgroup owns its rows, so a slab's whole tall part is one launch and the 64-column
+// chain runs on the diagonal block's rows only.
+__global__ __launch_bounds__(256) void panel_tall_kernel(DevPlan P, const int4* __restrict__ tasks) {
+    constexpr int BT = 64, WM = 2, WN = 2, BK = 16, LDT = BT + 16;
+    constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
+    __shared__ double smem[2 * 2 * BK * LDT];  // K-loop stages; then Y (k-major, ld LDT)
+    __shared__ double Bs[PNB * LDT];           // inv(L_jj)^T, k-major
+    const int4 t = tasks[blockIdx.x];
+    const int s = t.x, a = t.y, r0 = t.z, b = t.w;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wr = wid / WN, wc = wid % WN;
+    const int m = P.sn_m[s];
+    double* pan = P.panel_pool + P.panel_off[s];
+    const double* A = pan + (int64_t)a * m;  // column a
+    double* Ys = smem;
+    for (int c0 = 0; a + c0 < b; c0 += PNB) {
+        const int nb = min(PNB, b - a - c0);
+        double4_t acc[RTM][RTN];
+#pragma unroll
+        for (int i = 0; i < RTM; ++i)
+#pragma unroll
+            for (int j = 0; j < RTN; ++j) acc[i][j] = (double4_t){0.0, 0.0, 0.0, 0.0};
+        if (c0 > 0) mfma_kloop<BT, WM, WN, 1>(A, m, c0, m, a + c0 + nb, r0, a + c0, acc, smem);
+        // columns a + c0 .. + nb of the rows: a buffer resource over them (dead rows / columns masked)
+        const __amdgpu_buffer_rsrc_t rc = buf_rsrc(pan + (int64_t)(a + c0) * m, (uint32_t)((int64_t)nb * m * 8));
+        // Y = A - acc into LDS, k-major (Ys[col * LDT + row]: the MFMA A-operand layout below)
+#pragma unroll
+        for (int i = 0; i < RTM; ++i)
+#pragma unroll
+            for (int j = 0; j < RTN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int lr = wr * (BT / WM) + i * 16 + MFMA_F64_ROW(lane, r);
+                    const int lc = wc * (BT / WN) + j * 16 + (lane & 15);
+                    const bool live = r0 + lr < m && lc < nb;
+                    Ys[lc * LDT + lr] = buf_ld(rc, live ? (int)((lc * m + r0 + lr) * 8) : BUF_DEAD, 0) - acc[i][j][r];
+                }
+        // inv(L_jj)^T: Bs[k][c] = inv(c, k) = block (k, c) for k < c, 1 / L(k, k) at k = c
+        const double* blk = pan + (int64_t)(a + c0) * m + a + c0;
+#pragma unroll
+        for (int q = 0; q < PNB * PNB / 256; ++q) {
+            const int e = tid + 256 * q, c = e >> 6, k = e & 63;  // lanes along k: coalesced in column c
+            double v = 0.0;
+            if (k < nb && c < nb && k <= c) {
+                const double x = blk[(int64_t)c * m + k];
+                v = k == c ? 1.0 / x : x;
+            }
+            Bs[k * LDT + c] = v;
+        }
+        __syncthreads();
+        // X = Y inv^T (K = 64)
+#pragma unroll
+        for (int i = 0; i < RTM; ++i)
+#pragma unroll
+            for (int j = 0; j < RTN; ++j) acc[i][j] = (double4_t){0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+        for (int kk = 0; kk < PNB; kk += 4) {
+            const int krow = kk + (lane >> 4);
+            double av[RTM], bv[RTN];
+#pragma unroll
+            for (int i = 0; i < RTM; ++i) av[i] = Ys[krow * LDT + wr * (BT / WM) + i * 16 + (lane & 15)];
+#pragma unroll
+            for (int j = 0; j < RTN; ++j) bv[j] = Bs[krow * LDT + wc * (BT / WN) + j * 16 + (lane & 15)];
+#pragma unroll
+            for (int i = 0; i < RTM; ++i)
+#pragma unroll
+                for (int j = 0; j < RTN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], acc[i][j], 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < RTM; ++i)
+#pragma unroll
+            for (int j = 0; j < RTN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int lr = wr * (BT / WM) + i * 16 + MFMA_F64_ROW(lane, r);
+                    const int lc = wc * (BT / WN) + j * 16 + (lane & 15);
+                    const bool live = r0 + lr < m && lc < nb;
+                    buf_st(acc[i][j][r], rc, live ? (int)((lc * m + r0 + lr) * 8) : BUF_DEAD, 0);
+                }
+        // X(:, j) complete before the next block's K loop reads it back (glc) and before
+        // Ys / Bs are overwritten
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Launch wrappers
 // ---------------------------------------------------------------------------
@@ -1166,11 +1302,11 @@ hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hip
     return hipGetLastError();
 }
 
-hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st, bool partial,
+hipError_t launch_trsm_panel(const DevPlan& P, const TrsmTask* tasks, int count, hipStream_t st, bool partial,
                              int32_t* arrive) {
     if (count <= 0) return hipSuccess;
     if (partial)
-        hipLaunchKernelGGL(trsm_partial_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks, TRSM_ROWS);
+        hipLaunchKernelGGL(trsm_partial_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks);
     else
         hipLaunchKernelGGL(trsm_panel_g_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks, arrive);
     return hipGetLastError();
@@ -1573,6 +1709,23 @@ hipError_t launch_solve_gemv(const SolvePlan& P, const int4* tasks, int count, h
 hipError_t launch_solve_diag(const SolvePlan& P, const int2* tasks, int count, hipStream_t st) {
     if (count <= 0) return hipSuccess;
     hipLaunchKernelGGL(solve_diag_kernel, dim3(count), dim3(256), 0, st, P, tasks);
+    return hipGetLastError();
+}
+
+hipError_t launch_panel_inv(const DevPlan& P, const int2* tasks, int count, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    SolvePlan S {};
+    S.sn_start = P.sn_start;
+    S.sn_m = P.sn_m;
+    S.panel_off = P.panel_off;
+    S.panel_pool = P.panel_pool;
+    hipLaunchKernelGGL(solve_inv_kernel, dim3(count), dim3(64), 0, st, S, tasks);
+    return hipGetLastError();
+}
+
+hipError_t launch_panel_tall(const DevPlan& P, const int4* tasks, int count, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(panel_tall_kernel, dim3(count), dim3(256), 0, st, P, tasks);
     return hipGetLastError();
 }
 

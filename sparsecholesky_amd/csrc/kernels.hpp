@@ -170,10 +170,23 @@ hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count,
 // 64 x 64 diagonal POTRF (one wave per block) and the TRSM of the rows below it
 // (TRSM_ROWS rows per task).  partial: every task is a partial last block (nb < 64).
 hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hipStream_t st);
+// One workgroup of the panel TRSM of block k0 (columns k0 .. k0 + 64) of front s: rows
+// [r0, min(r0 + TRSM_ROWS, r1)); ctr - 1 indexes the block's arrival counter (fused POTRF).
+struct TrsmTask {
+    int32_t s, k0, r0, r1, ctr;
+};
 // partial: blocks with nb < 64; else full blocks with the POTRF fused (arrive: the
-// per-block arrival counters, zeroed; task .w - 1 indexes them)
-hipError_t launch_trsm_panel(const DevPlan& P, const int4* tasks, int count, hipStream_t st, bool partial,
+// per-block arrival counters, zeroed)
+hipError_t launch_trsm_panel(const DevPlan& P, const TrsmTask* tasks, int count, hipStream_t st, bool partial,
                              int32_t* arrive);
+// inv(L_jj) of factored 64 x 64 diagonal blocks (s, k0) into their strict upper
+// triangles (the tall TRSM's diagonal solves; the solve's block inverses are the same)
+hipError_t launch_panel_inv(const DevPlan& P, const int2* tasks, int count, hipStream_t st);
+// Tall TRSM of a slab (columns [a, b) of front s, factored diagonal block): tasks
+// (s, a, r0, b), rows [r0, r0 + 64) below the slab solved in place, X = A L_kk^-T.
+hipError_t launch_panel_tall(const DevPlan& P, const int4* tasks, int count, hipStream_t st);
+constexpr int TALL_ROWS = 64;  // rows per tall-TRSM workgroup
+
 // plans: the hosted ranks' DevPlans (CB tasks with gs >= 0 gather their children's entries)
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
                        int epi = 0, const DevPlan* plans = nullptr);

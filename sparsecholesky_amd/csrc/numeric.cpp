@@ -157,8 +157,9 @@ struct SchedBuild {
     std::vector<int2> ta, tph, tpr;
     int32_t tiny_lds = 0;
     std::vector<int32_t> small;
-    std::vector<int2> asmv, potrf;
-    std::vector<int4> trsm;
+    std::vector<int2> asmv, potrf, inv;
+    std::vector<TrsmTask> trsm;
+    std::vector<int4> tall;
     std::vector<GemmTask> gemm;
     std::vector<int2> tiles;
     CommBuild cb;
@@ -169,7 +170,7 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
     std::vector<int32_t>& small = B.small;
     std::vector<int2>& asmv = B.asmv;
     std::vector<int2>& potrf = B.potrf;
-    std::vector<int4>& trsm = B.trsm;
+    std::vector<TrsmTask>& trsm = B.trsm;
     std::vector<GemmTask>& gemm = B.gemm;
     std::vector<int2>& tiles = B.tiles;
     CommBuild& cbld = B.cb;
@@ -472,20 +473,26 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // (stream 1), which overlaps the next slab's factorization.  A later outer
         // update of overlapping columns waits for the stream-1 work first.
         int b_pending = -1;
-        auto add_update = [&](std::vector<GemmTask>& vec, double& fl, double* pan, int m, int c_lo, int c_hi, int ka,
-                              int kb) {
-            if (c_hi <= c_lo || kb <= ka) return;
+        // rows [c_lo, r_hi) of columns [c_lo, c_hi) -= their product over columns [ka, kb)
+        auto add_update = [&](std::vector<GemmTask>& vec, double& fl, double* pan, int m, int r_hi, int c_lo, int c_hi,
+                              int ka, int kb) {
+            if (c_hi <= c_lo || kb <= ka || r_hi <= c_lo) return;
             GemmTask t {};
             t.C = pan + (int64_t)c_lo * m + c_lo;
             t.A = pan + (int64_t)ka * m + c_lo;
             t.ldc = m;
             t.lda = m;
-            t.M = m - c_lo;
+            t.M = r_hi - c_lo;
             t.N = c_hi - c_lo;
             t.K = kb - ka;
             vec.push_back(t);
             fl += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
         };
+        // tall mode (a front of more than one 64-column block): the 64-column chain
+        // (POTRF / TRSM / inner updates) runs on the slab's diagonal-block rows only; at
+        // the slab end the block inverses and one tall-TRSM launch solve every row below
+        // the slab (panel_tall_kernel), then the outer updates as before
+        auto tall = [&](int32_t s) { return S.opt.panel_tall && S.w(s) > PNB; };
         for (int k0 = 0; k0 < maxw; k0 += PNB) {
             Launch Lp {};
             Lp.kind = L_POTRF;
@@ -498,24 +505,27 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
             Lt.vr = v;
             Lt.off = (int64_t)trsm.size();
             std::vector<GemmTask> upd, outer_a, outer_b;
-            std::vector<int4> trsm_part;  // partial last blocks: own launch (big = 1)
+            std::vector<TrsmTask> trsm_part;  // partial last blocks: own launch (big = 1)
+            std::vector<int2> inv_t;           // tall mode, slab end: diagonal-block inverses
+            std::vector<int4> tall_t;          // ... and the tall TRSM of the rows below
             double uflops = 0.0, afl = 0.0, bfl = 0.0;
             for (int32_t s : large) {
                 const int w = S.w(s), m = S.sn_m[s];
                 if (w <= k0) continue;
                 const int nb = std::min(PNB, w - k0);
                 const int k1 = k0 + nb;
-                if (nb < PNB) {
-                    potrf.push_back(make_int2(s, k0));
-                    for (int r0 = k1; r0 < m; r0 += TRSM_ROWS) trsm_part.push_back(make_int4(s, k0, r0, 0));
-                } else {  // fused POTRF (one task if no rows below); .w - 1: arrival counter
-                    const int ctr = (int)trsm.size() + 1;
-                    for (int r0 = k1; r0 < std::max(m, k1 + 1); r0 += TRSM_ROWS)
-                        trsm.push_back(make_int4(s, k0, r0, ctr));
-                }
-                double* pan = panel_pool + poff[s];
                 const int slab0 = (k0 / NBO) * NBO;
                 const int slab1 = std::min(w, slab0 + NBO);
+                const int rend = tall(s) ? slab1 : m;  // rows of this step's TRSM and inner update
+                if (nb < PNB) {
+                    potrf.push_back(make_int2(s, k0));
+                    for (int r0 = k1; r0 < rend; r0 += TRSM_ROWS) trsm_part.push_back(TrsmTask {s, k0, r0, rend, 0});
+                } else {  // fused POTRF (one task if no rows below); ctr - 1: arrival counter
+                    const int ctr = (int)trsm.size() + 1;
+                    for (int r0 = k1; r0 < std::max(rend, k1 + 1); r0 += TRSM_ROWS)
+                        trsm.push_back(TrsmTask {s, k0, r0, rend, ctr});
+                }
+                double* pan = panel_pool + poff[s];
                 if (k1 < slab1 && S.opt.inner_order == 1) {
                     // recursive order: block b of the slab closes a run of 2^t blocks
                     // (t = trailing zeros of b + 1); that run updates the next 2^t
@@ -523,15 +533,20 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     // right-looking, 768 instead of 1792 C columns rewritten per slab.
                     const int b = (k0 - slab0) / PNB;
                     const int span = PNB << __builtin_ctz((unsigned)(b + 1));
-                    add_update(upd, uflops, pan, m, k1, std::min(slab1, k1 + span), k1 - span, k1);
+                    add_update(upd, uflops, pan, m, rend, k1, std::min(slab1, k1 + span), k1 - span, k1);
                 } else if (k1 < slab1) {
-                    add_update(upd, uflops, pan, m, k1, slab1, k0, k1);
-                } else if (k1 == slab1 && slab1 < w) {
+                    add_update(upd, uflops, pan, m, rend, k1, slab1, k0, k1);
+                }
+                if (k1 == slab1 && tall(s)) {
+                    for (int kb = slab0; kb < slab1; kb += PNB) inv_t.push_back(make_int2(s, kb));
+                    for (int r0 = slab1; r0 < m; r0 += TALL_ROWS) tall_t.push_back(make_int4(s, slab0, r0, slab1));
+                }
+                if (k1 == slab1 && slab1 < w) {
                     // outer_a is the last update of block slab1: a pending stream-1 outer
                     // update of those columns is waited for before outer_a runs
                     const int nxt = S.opt.lookahead ? std::min(w, slab1 + NBO) : w;
-                    add_update(outer_a, afl, pan, m, slab1, nxt, slab0, slab1);
-                    add_update(outer_b, bfl, pan, m, nxt, w, slab0, slab1);
+                    add_update(outer_a, afl, pan, m, m, slab1, nxt, slab0, slab1);
+                    add_update(outer_b, bfl, pan, m, m, nxt, w, slab0, slab1);
                 }
             }
             Lp.count = (int32_t)((int64_t)potrf.size() - Lp.off);
@@ -546,14 +561,33 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 trsm.insert(trsm.end(), trsm_part.begin(), trsm_part.end());
                 N.sched.push_back(Lq);
             }
-            // split fronts: a slab is final after the TRSM of its last block
+            push_gemm_launch(L_PANEL, lev, upd, 0, uflops);
+            if (!tall_t.empty() || !inv_t.empty()) {
+                Launch Li {};
+                Li.kind = L_INV;
+                Li.level = lev;
+                Li.vr = v;
+                Li.off = (int64_t)B.inv.size();
+                Li.count = (int32_t)inv_t.size();
+                B.inv.insert(B.inv.end(), inv_t.begin(), inv_t.end());
+                if (Li.count > 0) N.sched.push_back(Li);
+                Launch Lt2 {};
+                Lt2.kind = L_TALL;
+                Lt2.level = lev;
+                Lt2.vr = v;
+                Lt2.off = (int64_t)B.tall.size();
+                Lt2.count = (int32_t)tall_t.size();
+                B.tall.insert(B.tall.end(), tall_t.begin(), tall_t.end());
+                if (Lt2.count > 0) N.sched.push_back(Lt2);
+            }
+            // split fronts: a slab is final after the TRSM of its last block (tall mode:
+            // after the slab's tall TRSM); at a slab end no inner update is pending
             for (int32_t s : large) {
                 const int w = S.w(s);
                 if (!is_split(s) || w <= k0 || slab_step0[s] < 0) continue;
                 const int k1 = std::min(w, k0 + PNB);
                 if (k1 == w || k1 % D.nbo == 0) emit_step(slab_step0[s] + k0 / D.nbo);
             }
-            push_gemm_launch(L_PANEL, lev, upd, 0, uflops);
             int e_trsm = -1;
             if (!outer_b.empty()) e_trsm = push_record(0);
             if (!outer_a.empty()) {
@@ -706,7 +740,7 @@ static int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     Lt.big = nb < PNB ? 1 : 0;
                     const int ctr = nb < PNB ? 0 : (int)trsm.size() + 1;  // fused POTRF: arrival counter
                     for (int r0 = k1; r0 < (nb < PNB ? m : std::max(m, k1 + 1)); r0 += TRSM_ROWS)
-                        trsm.push_back(make_int4(s, k0, r0, ctr));
+                        trsm.push_back(TrsmTask {s, k0, r0, m, ctr});
                     Lt.count = (int32_t)((int64_t)trsm.size() - Lt.off);
                     if (Lt.count > 0) N.sched.push_back(Lt);
                     if (k1 < k1s) {
@@ -1157,6 +1191,7 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     }
     if ((rc = upload(N, B.small, N.d_small)) || (rc = upload(N, B.asmv, N.d_asm)) ||
         (rc = upload(N, B.potrf, N.d_potrf)) || (rc = upload(N, B.trsm, N.d_trsm)) ||
+        (rc = upload(N, B.inv, N.d_inv)) || (rc = upload(N, B.tall, N.d_tall)) ||
         (rc = upload(N, std::vector<int32_t>(B.trsm.size() + 1, 0), N.d_arrive)) ||
         (rc = upload(N, B.gemm, N.d_gemm)) || (rc = upload(N, B.tiles, N.d_tiles)))
         return fail(rc);
@@ -1195,6 +1230,10 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
                                N.d_plans);
         case L_COMM:
             return comm_launch(N, L);
+        case L_INV:
+            return launch_panel_inv(N.R[L.vr].P, N.d_inv + L.off, L.count, N.stream);
+        case L_TALL:
+            return launch_panel_tall(N.R[L.vr].P, N.d_tall + L.off, L.count, N.stream);
     }
     return hipErrorInvalidValue;
 }
@@ -1314,7 +1353,9 @@ int64_t numeric_status(Numeric& N) {
                 case L_SMALL: slot = 2; break;
                 case L_ASM: slot = 3; break;
                 case L_POTRF: slot = 4; break;
-                case L_TRSM: slot = 5; break;
+                case L_TRSM:
+                case L_INV:
+                case L_TALL: slot = 5; break;
                 case L_PANEL: slot = 6; break;
                 case L_CB: slot = 7; break;
                 case L_COMM: slot = 1; break;
@@ -1737,8 +1778,8 @@ static int64_t bench_panel(int which, int M, int reps, double* out) {
         for (int i = 0; i < M; ++i) h[(size_t)j * M + i] = (i == j) ? 64.0 : rnd();
     int32_t hs[2] = {0, w}, hm[1] = {M};
     int64_t ho[2] = {0, (int64_t)nel};
-    std::vector<int4> tr;
-    for (int r0 = w; r0 < M; r0 += TRSM_ROWS) tr.push_back(make_int4(0, 0, r0, 1));
+    std::vector<TrsmTask> tr;
+    for (int r0 = w; r0 < M; r0 += TRSM_ROWS) tr.push_back(TrsmTask {0, 0, r0, M, 1});
     int2 pt = make_int2(0, 0);
     void *d_pan = nullptr, *d_ref = nullptr, *d_s = nullptr, *d_m = nullptr, *d_o = nullptr, *d_info = nullptr,
          *d_pt = nullptr, *d_tr = nullptr, *d_arr = nullptr;
@@ -1747,7 +1788,7 @@ static int64_t bench_panel(int which, int M, int reps, double* out) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (hipMalloc(&d_pan, bytes) || hipMalloc(&d_ref, bytes) || hipMalloc(&d_s, 8) || hipMalloc(&d_m, 4) ||
         hipMalloc(&d_o, 16) || hipMalloc(&d_info, 4) || hipMalloc(&d_pt, 8) ||
-        hipMalloc(&d_tr, std::max<size_t>(1, tr.size()) * sizeof(int4)) || hipMalloc(&d_arr, 4) ||
+        hipMalloc(&d_tr, std::max<size_t>(1, tr.size()) * sizeof(TrsmTask)) || hipMalloc(&d_arr, 4) ||
         hipMemset(d_arr, 0, 4) || hipEventCreate(&e0) ||
         hipEventCreate(&e1)) {
         rc = SC_ERR_DEVMEM;
@@ -1758,7 +1799,7 @@ static int64_t bench_panel(int which, int M, int reps, double* out) {
         (void)hipMemcpy(d_o, ho, 16, hipMemcpyHostToDevice);
         (void)hipMemset(d_info, 0, 4);
         (void)hipMemcpy(d_pt, &pt, 8, hipMemcpyHostToDevice);
-        if (!tr.empty()) (void)hipMemcpy(d_tr, tr.data(), tr.size() * sizeof(int4), hipMemcpyHostToDevice);
+        if (!tr.empty()) (void)hipMemcpy(d_tr, tr.data(), tr.size() * sizeof(TrsmTask), hipMemcpyHostToDevice);
         DevPlan P {};
         P.sn_start = (const int32_t*)d_s;
         P.sn_m = (const int32_t*)d_m;
@@ -1775,7 +1816,7 @@ static int64_t bench_panel(int which, int M, int reps, double* out) {
             if (which == 2)
                 (void)launch_potrf_diag(P, (const int2*)d_pt, 1, nullptr);
             else
-                (void)launch_trsm_panel(P, (const int4*)d_tr, nt, nullptr, false, (int32_t*)d_arr);
+                (void)launch_trsm_panel(P, (const TrsmTask*)d_tr, nt, nullptr, false, (int32_t*)d_arr);
             (void)hipEventRecord(e1, nullptr);
             (void)hipEventSynchronize(e1);
             float ms = 0.f;

@@ -19,9 +19,11 @@ enum LaunchKind : int32_t {
     L_PANEL = 4,
     L_CB = 5,
     L_COMM = 6,    // one comm step of the hosted ranks (pack, transfer group, unpack)
-    L_RECORD = 7,  // record sync event `count` on stream `strm`
-    L_WAIT = 8,    // stream `strm` waits for sync event `count`
-    L_KINDS = 9
+    L_INV = 7,     // inverses of a slab's factored 64 x 64 diagonal blocks (tall TRSM)
+    L_TALL = 8,    // tall TRSM of a slab's rows below its diagonal block
+    L_RECORD = 9,  // record sync event `count` on stream `strm`
+    L_WAIT = 10,   // stream `strm` waits for sync event `count`
+    L_KINDS = 11
 };
 
 // ---------------- multi-GPU plan (dist.cpp) ----------------
@@ -181,7 +183,9 @@ struct Numeric {
     int64_t n_chain = 0;             // chained fronts (descriptors)
     int2* d_asm = nullptr;
     int2* d_potrf = nullptr;
-    int4* d_trsm = nullptr;
+    TrsmTask* d_trsm = nullptr;
+    int2* d_inv = nullptr;   // L_INV tasks (s, k0)
+    int4* d_tall = nullptr;  // L_TALL tasks (s, a, r0, b)
     int32_t* d_arrive = nullptr;  // fused POTRF + TRSM: per-block arrival counters
     GemmTask* d_gemm = nullptr;
     int2* d_tiles = nullptr;

@@ -305,8 +305,8 @@ def lap48_oracle():
     return A, Lp, Li, Lx
 
 
-@pytest.mark.parametrize("opts", [{}, dict(asm_tile_min_m=1024), dict(cb_gather=0)],
-                         ids=["default", "tiled_asm", "assembled_cb"])
+@pytest.mark.parametrize("opts", [{}, dict(asm_tile_min_m=1024), dict(cb_gather=0), dict(panel_tall=1)],
+                         ids=["default", "tiled_asm", "assembled_cb", "tall_trsm"])
 def test_lap48_full_parity(gpu, lap48_oracle, opts):
     # the whole 48^3 factor (n = 110592, F = 7.07e10: a 2304-wide root, CB SYRK with K
     # up to 1152 on 128 x 128 tiles) against the oracle, exact pattern and rel-Fro;
@@ -323,15 +323,16 @@ def test_lap48_full_parity(gpu, lap48_oracle, opts):
     assert err < TOL
 
 
-@pytest.mark.parametrize("nranks,rccl", [(2, False), (4, False), (8, False), (2, True), (4, True), (8, True)])
-def test_partitioned_defaults_lap48(gpu, lap48_oracle, nranks, rccl):
+@pytest.mark.parametrize("nranks,rccl,opts", [(2, False, {}), (4, False, {}), (8, False, {}), (2, True, {}),
+                                               (4, True, {}), (8, True, {}), (8, False, dict(panel_tall=1))])
+def test_partitioned_defaults_lap48(gpu, lap48_oracle, nranks, rccl, opts):
     # the distributed plan at the DEFAULT options the N-GPU bench runs (panel_nb_outer
     # 1024, dist_cbb 1024, small_front_max 128): the 2327-wide root factored 1D
     # slab-cyclic in three 1024-column slabs, split fronts with 1024-wide CB blocks;
     # every rank emulated with private memory, messages as device copies or RCCL
     # send/recv to self (dist.cpp transfer_group)
     A, Lp, Li, Lx = lap48_oracle
-    s = sc.Symbolic(A)
+    s = sc.Symbolic(A, **opts)
     assert s.opt.panel_nb_outer == 1024 and s.opt.dist_cbb == 1024
     info = s.dist_plan_info(nranks)
     assert info["slab_ranks"].max() >= 2
@@ -553,7 +554,8 @@ def test_dense_matrix_large_front(gpu):
 # large-front schedule options: inner slab update order (0 right-looking, 1
 # recursive), lookahead (0 none, 1 trailing updates on a second stream), tiled assembly
 PANEL_OPTS = [dict(inner_order=0), dict(inner_order=0, lookahead=0), dict(lookahead=0), dict(asm_tile_min_m=1),
-              dict(asm_tile_min_m=300), dict(panel_nb_outer=128, lookahead=0)]
+              dict(asm_tile_min_m=300), dict(panel_nb_outer=128, lookahead=0), dict(panel_tall=1),
+              dict(panel_tall=1, panel_nb_outer=128)]
 
 
 @pytest.mark.parametrize("opts", PANEL_OPTS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
