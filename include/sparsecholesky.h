@@ -337,6 +337,9 @@ int64_t sc_debug_chain_stamps(sc_numeric* num, int32_t enable, uint64_t* out, in
  * (TFLOP/s); which=2/3 the panel POTRF / TRSM kernel on an M x 64 front
  * (microseconds per launch). */
 int64_t sc_debug_bench(int32_t which, int32_t M, int32_t K, int32_t reps, int32_t arg, double* tflops);
+/* Placement probe: nwg workgroups of `threads` threads, each spinning spin_ticks of the
+ * 100 MHz clock; out[2 i] = HW_ID, out[2 i + 1] = XCC_ID of workgroup i. */
+int64_t sc_debug_hwid(int32_t nwg, int32_t threads, int32_t spin_ticks, uint32_t* out);
 int64_t sc_device_count(void);
 /* Message of the last failing call on this thread. */
 const char* sc_last_error(void);

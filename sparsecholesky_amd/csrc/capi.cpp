@@ -566,6 +566,17 @@ int64_t sc_debug_bench(int32_t which, int32_t M, int32_t K, int32_t reps, int32_
     return sc::debug_bench(which, M, K, reps, arg, tflops);
 }
 
+int64_t sc_debug_hwid(int32_t nwg, int32_t threads, int32_t spin_ticks, uint32_t* out) {
+    if (!out || nwg <= 0 || threads <= 0 || threads > 1024) return SC_ERR_ARG;
+    void* d = nullptr;
+    if (hipMalloc(&d, (size_t)nwg * 8) != hipSuccess) return SC_ERR_DEVMEM;
+    hipError_t e = sc::launch_hwid((uint32_t*)d, nwg, threads, spin_ticks, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out, d, (size_t)nwg * 8, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    return e == hipSuccess ? SC_OK : SC_ERR_HIP;
+}
+
 int64_t sc_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;

@@ -1356,6 +1356,21 @@ hipError_t launch_fill_random(double* p, int64_t n, hipStream_t st) {
 // Timestamp probe for graph-captured timing (s_memrealtime: constant 100 MHz).
 __global__ void stamp_kernel(uint64_t* slot) { *slot = __builtin_amdgcn_s_memrealtime(); }
 
+// Hardware placement probe: per workgroup its HW_ID (wave/SIMD/CU/SH/SE fields) and XCC_ID.
+__global__ void hwid_kernel(uint32_t* out, int spin) {
+    if (threadIdx.x == 0) {
+        out[2 * blockIdx.x] = __builtin_amdgcn_s_getreg((31 << 11) | 4);      // HW_REG_HW_ID
+        out[2 * blockIdx.x + 1] = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
+    }
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)spin) __builtin_amdgcn_s_sleep(8);
+}
+
+hipError_t launch_hwid(uint32_t* out, int nwg, int threads, int spin, hipStream_t st) {
+    hipLaunchKernelGGL(hwid_kernel, dim3(nwg), dim3(threads), 0, st, out, spin);
+    return hipGetLastError();
+}
+
 hipError_t launch_stamp(uint64_t* slot, hipStream_t st) {
     hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(1), 0, st, slot);
     return hipGetLastError();

@@ -191,6 +191,8 @@ constexpr int TALL_ROWS = 64;  // rows per tall-TRSM workgroup
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
                        int epi = 0, const DevPlan* plans = nullptr);
 hipError_t launch_stamp(uint64_t* slot, hipStream_t st);
+
+hipError_t launch_hwid(uint32_t* out, int nwg, int threads, int spin, hipStream_t st);
 hipError_t launch_fill_random(double* p, int64_t n, hipStream_t st);
 hipError_t launch_mfma_peak(double* out, int blocks, int iters, int nacc, hipStream_t st);
 
