@@ -189,8 +189,7 @@ struct Numeric {
     int32_t* d_arrive = nullptr;  // fused POTRF + TRSM: per-block arrival counters
     GemmTask* d_gemm = nullptr;
     int2* d_tiles = nullptr;
-    DevPlan* d_plans = nullptr;
-    int32_t* d_la_ctr = nullptr;  // lookahead updates on unreserved CUs: per-XCD tile counters + exit counter  // the hosted ranks' DevPlans (CB SYRK extend-add gather)
+    DevPlan* d_plans = nullptr;  // the hosted ranks' DevPlans (CB SYRK extend-add gather)
     int32_t* d_info = nullptr;       // shared by the hosted ranks' DevPlans
     int32_t* h_info = nullptr;       // pinned host copy, written at the end of each factorization
     double* d_Ax_owned = nullptr;
