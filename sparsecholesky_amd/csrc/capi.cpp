@@ -523,6 +523,20 @@ int64_t sc_numeric_memory(sc_numeric* num, int64_t* info, int32_t n) {
     return SC_OK;
 }
 
+int64_t sc_dist_steps(const sc_symbolic* sym, int32_t nranks, int32_t* kind, int32_t* level, int32_t* front,
+                      int64_t cap) {
+    if (!sym || nranks <= 0) return SC_ERR_ARG;
+    sc::DistPlan D;
+    int64_t rc = sc::dist_plan(sym->S, nranks, D);
+    if (rc != SC_OK) return rc;
+    for (size_t i = 0; i < D.steps.size() && (int64_t)i < cap; ++i) {
+        if (kind) kind[i] = D.steps[i].kind;
+        if (level) level[i] = D.steps[i].level;
+        if (front) front[i] = D.steps[i].s;
+    }
+    return (int64_t)D.steps.size();
+}
+
 int64_t sc_dist_plan_info(const sc_symbolic* sym, int32_t nranks, int32_t* gsize, int32_t* split_cb_ranks,
                           int32_t* slab_ranks, int64_t* n_steps) {
     if (!sym || nranks <= 0) return SC_ERR_ARG;

@@ -1,0 +1,880 @@
+// Static launch schedule of the numeric factorization (host).  Per assembly-tree
+// level: small fronts (register kernels, chains, tiny trees), then the large fronts'
+// assembly, the 64-column POTRF / TRSM chain with recursive inner updates and
+// lookahead outer updates, and the CB SYRK (K = w, the children's CB entries
+// gathered per tile).  Multi-rank handles add the comm steps of the plan (dist.cpp)
+// and the distributed panels' slab schedule.  Task pointers are final device
+// addresses, so the whole schedule can be captured once into a hipGraph.
+#include "numeric_impl.hpp"
+
+namespace sc {
+
+static int bucket_of(int m) {
+    if (m <= 32) return 32;
+    if (m <= 64) return 64;
+    if (m <= 96) return 96;
+    return 128;
+}
+
+// register width of the small-front POTRF / TRSM (w > 64: right-looking path)
+static int wbucket_of(int w) {
+    if (w <= 16) return 16;
+    if (w <= 32) return 32;
+    if (w <= 64) return 64;
+    return 128;
+}
+
+// Build the static launch schedule (host).  Task pointers into the pools are
+// final device addresses, so the schedule can be replayed or graph-captured.
+void append_tiles(std::vector<int2>& out, int task, int M, int N, int bt, int G) {
+    const int TM = (M + bt - 1) / bt, TN = (N + bt - 1) / bt;
+    for (int sj = 0; sj < TN; sj += G)
+        for (int si = sj; si < TM; si += G)
+            for (int tj = sj; tj < std::min(TN, sj + G); ++tj)
+                for (int ti = std::max(si, tj); ti < std::min(TM, si + G); ++ti)
+                    out.push_back(make_int2(task, (ti << 16) | tj));
+}
+
+void xcd_order(int2* tiles, int64_t n) {
+    if (n <= 8) return;
+    std::vector<int2> src(tiles, tiles + n);
+    const int64_t q = n / 8, r = n % 8;
+    for (int64_t b = 0; b < n; ++b) {
+        const int64_t x = b % 8, j = b / 8;
+        tiles[b] = src[x * q + std::min(x, r) + j];
+    }
+}
+
+// Work-balanced XCD order of a multi-task launch (workgroup b runs on XCD b % 8,
+// each XCD has its own L2).  The tiles arrive task-contiguous, each task in
+// supertile order.  Every task is cut into 8 contiguous chunks, one per XCD, with
+// the remainders dealt round robin across tasks so that each XCD receives exactly
+// its ceil((n - x) / 8) tiles; an XCD walks its chunks in decreasing K (longest
+// tiles first).  With one task this is xcd_order.
+void xcd_order_tasks(int2* tiles, int64_t n, const GemmTask* tasks, int ntasks) {
+    if (n <= 8) return;
+    std::vector<int64_t> beg((size_t)ntasks + 1, 0);
+    for (int64_t i = 0; i < n; ++i) beg[(size_t)tiles[i].x + 1]++;
+    for (int t = 0; t < ntasks; ++t) beg[t + 1] += beg[t];
+    std::vector<int> ord((size_t)ntasks);
+    for (int t = 0; t < ntasks; ++t) ord[t] = t;
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return tasks[a].K > tasks[b].K; });
+    std::vector<std::vector<int2>> per(8);
+    int p = 0;
+    for (int t : ord) {
+        const int64_t nt = beg[t + 1] - beg[t], base = nt / 8, rem = nt % 8;
+        int64_t off = beg[t];
+        for (int x = 0; x < 8; ++x) {
+            const int64_t cnt = base + (((x - p + 8) % 8) < rem ? 1 : 0);
+            per[x].insert(per[x].end(), tiles + off, tiles + off + cnt);
+            off += cnt;
+        }
+        p = (int)((p + rem) % 8);
+    }
+    for (int x = 0; x < 8; ++x)
+        if ((int64_t)per[x].size() != (n - x + 7) / 8) return xcd_order(tiles, n);  // cannot happen
+    for (int64_t b = 0; b < n; ++b) tiles[b] = per[b % 8][b / 8];
+}
+
+int64_t build_schedule(Numeric& N, SchedBuild& B) {
+    const Symbolic& S = *N.S;
+    std::vector<int32_t>& small = B.small;
+    std::vector<int2>& asmv = B.asmv;
+    std::vector<int2>& potrf = B.potrf;
+    std::vector<TrsmTask>& trsm = B.trsm;
+    std::vector<GemmTask>& gemm = B.gemm;
+    std::vector<int2>& tiles = B.tiles;
+    CommBuild& cbld = B.cb;
+    const int NBO = std::max(PNB, (S.opt.panel_nb_outer / PNB) * PNB);
+    std::vector<std::vector<int32_t>> by_level((size_t)S.nlevels);
+    for (int32_t s = 0; s < S.ns; ++s) by_level[S.level[s]].push_back(s);
+    // multi-rank plan lookups
+    const DistPlan& D = N.D;
+    const bool multi = !N.owner.empty();
+    const DistPlan* Dp = multi ? &D : nullptr;
+    auto is_split = [&](int32_t s) { return multi && D.split[s] >= 0; };
+    auto is_dpanel = [&](int32_t s) { return multi && D.pd[s] >= 0; };
+    std::vector<int32_t> hosted_of((size_t)std::max(N.nranks, 1), -1);  // rank -> index into N.R
+    for (size_t v = 0; v < N.R.size(); ++v) hosted_of[N.R[v].rank] = (int32_t)v;
+    std::vector<int32_t> init_step, slab_step0, early_step0, deliver_step((size_t)S.nlevels, -1);
+    std::vector<std::vector<int32_t>> slab_step;  // distributed panels: step of slab k, -1 = none
+    std::vector<std::vector<int>> early_ev((size_t)S.ns);  // sender: event after each CB column group
+    std::vector<int64_t> step_beg;
+    std::vector<char> emitted;
+    if (multi) {
+        init_step.assign((size_t)S.ns, -1);
+        slab_step0.assign((size_t)S.ns, -1);
+        slab_step.assign((size_t)S.ns, std::vector<int32_t>());
+        for (size_t q = 0; q < D.pd_s.size(); ++q) slab_step[D.pd_s[q]].assign(D.slab_rank[q].size(), -1);
+        early_step0.assign((size_t)S.ns, -1);
+        for (int32_t id = 0; id < (int32_t)D.steps.size(); ++id) {
+            const DistStep& t = D.steps[id];
+            if (t.kind == STEP_INIT) init_step[t.s] = id;
+            if (t.kind == STEP_SLAB && t.k == 0) slab_step0[t.s] = id;
+            if (t.kind == STEP_SLAB && D.pd[t.s] >= 0) slab_step[t.s][t.k] = id;
+            if (t.kind == STEP_DELIVER && t.s < 0) deliver_step[t.level] = id;
+            if (t.kind == STEP_DELIVER && t.s >= 0 && t.k == 0) early_step0[t.s] = id;
+        }
+        step_beg.assign(D.steps.size() + 1, 0);
+        for (const DistMsg& g : D.msgs) step_beg[g.step + 1]++;
+        for (size_t i = 0; i < D.steps.size(); ++i) step_beg[i + 1] += step_beg[i];
+        emitted.assign(D.steps.size(), 0);
+    }
+    // device address of logical element (row, col) of a region on hosted rank v
+    auto addr = [&](int v, int kind, int s, int row, int col, int64_t& ld) -> double* {
+        int arena = 0;
+        int64_t off = 0;
+        if (!region_addr(S, Dp, N.R[v], kind, s, row, col, arena, off, ld)) return nullptr;
+        return (arena == 0 ? N.R[v].P.panel_pool : N.R[v].P.cb_pool) + off;
+    };
+    auto push_gemm_launch = [&](int kind, int level, const std::vector<GemmTask>& tasks, int big,
+                                double flops, int strm = 0) {
+        if (tasks.empty()) return;
+        Launch L {};
+        L.kind = kind;
+        L.level = level;
+        L.strm = strm;
+        L.off = (int64_t)gemm.size();
+        // 128x128 tiles on 8 waves when every task is at least 256 wide (random data,
+        // 16384 x 4096: 61 vs 52 TF/s for 64x64); 64x64 on 4 waves for narrow updates
+        int minN = INT32_MAX, maxK = 0;
+        for (auto& t : tasks) {
+            minN = std::min(minN, (int)t.N);
+            maxK = std::max(maxK, (int)t.K);
+        }
+        const bool wide = minN >= 256;
+        L.bt = (S.opt.syrk_tile == 128 || (S.opt.syrk_tile == 0 && wide)) ? SYRK_BT_LARGE : SYRK_BT_SMALL;
+        // batched C epilogue on the critical path (main-stream panel updates) and where
+        // K is short enough that the epilogue dominates a tile (CB of levels 4-7 at
+        // 128^3); deep-K CB updates and the lookahead stream keep the trickle epilogue
+        L.epi = (kind == L_PANEL && strm == 0) || (kind == L_CB && maxK < SC_EPI_KMAX);
+        L.toff = (int64_t)tiles.size();
+        for (size_t q = 0; q < tasks.size(); ++q) {
+            append_tiles(tiles, (int)q, tasks[q].M, tasks[q].N, L.bt);
+            gemm.push_back(tasks[q]);
+        }
+        L.count = (int32_t)((int64_t)tiles.size() - L.toff);
+        xcd_order_tasks(tiles.data() + L.toff, L.count, tasks.data(), (int)tasks.size());
+        L.ntasks = (int32_t)tasks.size();
+        L.big = big;
+        L.flops = flops;
+        N.sched.push_back(L);
+    };
+    // cross-stream dependencies: record an event on a stream / make a stream wait on it
+    auto push_record = [&](int strm) -> int {
+        Launch L {};
+        L.kind = L_RECORD;
+        L.strm = strm;
+        L.count = N.n_sync_events++;
+        N.sched.push_back(L);
+        return L.count;
+    };
+    auto push_wait = [&](int strm, int ev) {
+        Launch L {};
+        L.kind = L_WAIT;
+        L.strm = strm;
+        L.count = ev;
+        N.sched.push_back(L);
+    };
+    // The hosted ranks' part of comm step `id` on the comm stream (strm 2), emitted
+    // once, at the first call (the sender's point in an emulated schedule).  Sends
+    // wait for the main stream's work so far (their data); the main stream waits
+    // for the step when it receives.  Messages keep the plan order, so every peer
+    // pair posts its matching sends and receives in the same order.
+    auto emit_step = [&](int32_t id, int send_ev = -1) {
+        if (!multi || id < 0 || emitted[id]) return;
+        emitted[id] = 1;
+        Launch L {};
+        L.kind = L_COMM;
+        L.level = D.steps[id].level;
+        L.strm = 2;
+        L.step = id;
+        L.off = (int64_t)N.msgs.size();
+        bool any_send = false, any_recv = false;
+        std::vector<int32_t> pack_d, unpack_d;  // copy descriptors of the sends / receives
+        // (buffer, staging slot) of one end: the region itself when contiguous
+        auto end_of = [&](int v, int kind, int s, int row, int col, int rows, int cols, bool pack, double*& buf,
+                          int64_t& slot) {
+            int64_t ld = 0;
+            double* a = addr(v, kind, s, row, col, ld);
+            if (!a) return false;
+            if (ld == rows || cols == 1) {
+                buf = a;
+                slot = -1;
+                return true;
+            }
+            buf = nullptr;
+            slot = cbld.stage_total;
+            Copy2D c {};
+            c.a = a;
+            c.lda = ld;
+            c.rows = rows;
+            c.cols = cols;
+            (pack ? pack_d : unpack_d).push_back((int32_t)cbld.copies.size());
+            cbld.copies.push_back(c);
+            cbld.copy_slot.push_back(slot);
+            cbld.stage_total += (int64_t)rows * cols;
+            return true;
+        };
+        for (int64_t q = step_beg[id]; q < step_beg[id + 1]; ++q) {
+            const DistMsg& g = D.msgs[q];
+            const int vs = hosted_of[g.src], vd = hosted_of[g.dst];
+            if (vs < 0 && vd < 0) continue;
+            const int64_t cnt = (int64_t)g.rows * g.cols;
+            double *sb = nullptr, *db = nullptr;
+            int64_t ss = -1, ds = -1;
+            if (vs >= 0 && !end_of(vs, g.skind, g.s, g.srow, g.scol, g.rows, g.cols, true, sb, ss)) {
+                N.err = "comm plan: send region missing";
+                return;
+            }
+            if (vd >= 0 && !end_of(vd, g.dkind, g.s, g.drow, g.dcol, g.rows, g.cols, false, db, ds)) {
+                N.err = "comm plan: receive region missing";
+                return;
+            }
+            any_send |= vs >= 0;
+            any_recv |= vd >= 0;
+            auto push = [&](double* b, int64_t slot, double* src, int64_t src_slot, int peer, int op) {
+                Msg m {};
+                m.buf = b;
+                m.src_buf = src;
+                m.count = cnt;
+                m.peer = peer;
+                m.op = op;
+                N.msgs.push_back(m);
+                cbld.msg_slot.push_back(slot);
+                cbld.msg_src_slot.push_back(src_slot);
+            };
+            if (vs >= 0 && vd >= 0) {  // both ends in this process (emulated ranks)
+                if (N.emul_rccl) {
+                    push(sb, ss, nullptr, -1, 0, MSG_SEND);
+                    push(db, ds, nullptr, -1, 0, MSG_RECV);
+                } else {
+                    push(db, ds, sb, ss, 0, MSG_COPY);
+                }
+            } else if (vs >= 0) {
+                push(sb, ss, nullptr, -1, g.dst, MSG_SEND);
+            } else {
+                push(db, ds, nullptr, -1, g.src, MSG_RECV);
+            }
+        }
+        L.count = (int32_t)((int64_t)N.msgs.size() - L.off);
+        if (L.count == 0) return;
+        auto add_tiles = [&](const std::vector<int32_t>& ds) {
+            for (int32_t d : ds)
+                for (int j = 0; j < cbld.copies[d].cols; j += COPY_COLS) cbld.ctiles.push_back(make_int2(d, j));
+        };
+        L.poff = (int64_t)cbld.ctiles.size();
+        add_tiles(pack_d);
+        L.pcount = (int32_t)((int64_t)cbld.ctiles.size() - L.poff);
+        L.uoff = (int64_t)cbld.ctiles.size();
+        add_tiles(unpack_d);
+        L.ucount = (int32_t)((int64_t)cbld.ctiles.size() - L.uoff);
+        // sends wait for the data (default: everything the main stream has so far);
+        // receive-only steps post as soon as the main stream has finished the previous
+        // level (the per-level guard below)
+        if (any_send) push_wait(2, send_ev >= 0 ? send_ev : push_record(0));
+        N.sched.push_back(L);
+        if (any_recv) push_wait(0, push_record(2));
+    };
+    auto is_early_sender = [&](int32_t s, int v) {
+        return multi && D.early[s] && D.owner[s] == N.R[v].rank;
+    };
+    // CB rank (hosted index v) of split front s: per final panel slab, CB -= L21_k
+    // L21_k^T on the column blocks it owns (K = slab width), from its R_LAND copy
+    auto emit_cb_rank = [&](int32_t lev, int32_t s, int v) {
+        const int who = N.R[v].rank;
+        const std::vector<int32_t>& cbr = D.cb_rank[D.split[s]];
+        const int w = S.w(s), m = S.sn_m[s], mb = m - w;
+        emit_step(init_step[s]);
+        for (int k0 = 0, k = 0; k0 < w; k0 += D.nbo, ++k) {
+            const int k1 = std::min(w, k0 + D.nbo);
+            emit_step(slab_step0[s] < 0 ? -1 : slab_step0[s] + k);
+            std::vector<GemmTask> cbt;
+            double fl = 0.0;
+            for (int jb = 0; jb < (int)cbr.size(); ++jb) {
+                if (cbr[jb] != who) continue;
+                const int r0 = jb * D.cbb;
+                GemmTask t {};
+                int64_t ldc = 0, lda = 0;
+                t.C = addr(v, R_CB, s, r0, r0, ldc);
+                t.A = addr(v, R_LAND, s, r0, k0, lda);
+                t.ldc = ldc;
+                t.lda = lda;
+                t.M = mb - r0;
+                t.N = std::min(D.cbb, mb - r0);
+                t.K = k1 - k0;
+                cbt.push_back(t);
+                fl += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
+            }
+            push_gemm_launch(L_CB, lev, cbt, w >= 256 ? 1 : 0, fl);
+        }
+    };
+    // one level's fronts of hosted rank v
+    auto emit_level = [&](int32_t lev, const std::vector<int32_t>& nodes, int v) {
+        double* panel_pool = N.R[v].P.panel_pool;
+        double* cb_pool = N.R[v].P.cb_pool;
+        const std::vector<int64_t>& poff = N.R[v].panel_off;
+        const std::vector<int64_t>& coff = N.R[v].cb_off;
+        // small fronts: one launch sized for the level's largest front when the level
+        // fits one workgroup per CU (fewer dependent launches on thin levels), else one
+        // launch per LDS bucket (small fronts keep their occupancy on wide levels)
+        int nsmall = 0, bmax = 0;
+        for (int32_t s : nodes)
+            if (S.fclass[s] == FRONT_SMALL) {
+                ++nsmall;
+                bmax = std::max(bmax, bucket_of(S.sn_m[s]));
+            }
+        for (int b : {32, 64, 96, 128}) {
+            if (nsmall <= 256 && b != bmax) continue;
+            Launch L {};
+            L.kind = L_SMALL;
+            L.level = lev;
+            L.vr = v;
+            L.off = (int64_t)small.size();
+            L.maxm = b;
+            L.bt = 16;
+            for (int32_t s : nodes)
+                if (S.fclass[s] == FRONT_SMALL && (nsmall <= 256 || bucket_of(S.sn_m[s]) == b)) {
+                    small.push_back(s);
+                    L.bt = std::max(L.bt, wbucket_of(S.w(s)));
+                }
+            L.count = (int32_t)((int64_t)small.size() - L.off);
+            if (L.count > 0) N.sched.push_back(L);
+        }
+        std::vector<int32_t> large;
+        for (int32_t s : nodes)
+            if (S.fclass[s] == FRONT_LARGE) large.push_back(s);
+        if (large.empty()) return;
+        // fronts whose CB SYRK gathers the children's CB entries itself (one CB launch
+        // task covering the whole CB): their assembly stops at the panel columns
+        auto gather = [&](int32_t s) { return S.opt.cb_gather && S.mb(s) > 0 && !is_split(s) && !is_early_sender(s, v); };
+        // assembly: fronts with m >= ASM_TILE_MIN_M one workgroup per (front, 16
+        // columns, 256-row tile), write-once (big = 1); smaller fronts one workgroup per
+        // (front, 16 columns) streaming child columns (measured faster below ~8k rows)
+        const int tile_min_m = S.opt.asm_tile_min_m > 0 ? S.opt.asm_tile_min_m : ASM_TILE_MIN_M;
+        for (int tiled = 1; tiled >= 0; --tiled) {
+            Launch L {};
+            L.kind = L_ASM;
+            L.level = lev;
+            L.vr = v;
+            L.big = tiled;
+            L.off = (int64_t)asmv.size();
+            for (int32_t s : large) {
+                const int m = S.sn_m[s];
+                if ((m >= tile_min_m) != (tiled == 1)) continue;
+                const int ncol = gather(s) ? S.w(s) : m;  // assembled columns
+                for (int cb = 0; cb * ASM_COLS < ncol; ++cb) {
+                    if (!tiled) {
+                        asmv.push_back(make_int2(s, cb));
+                        continue;
+                    }
+                    for (int k = cb * ASM_COLS / ASM_ROWS; k * ASM_ROWS < m; ++k)
+                        asmv.push_back(make_int2(s, (k << 16) | cb));
+                }
+            }
+            L.count = (int32_t)((int64_t)asmv.size() - L.off);
+            if (L.count > 0) N.sched.push_back(L);
+        }
+        for (int32_t s : large)
+            if (is_split(s)) emit_step(init_step[s]);
+        int maxw = 0;
+        for (int32_t s : large) maxw = std::max(maxw, S.w(s));
+        // Lookahead: at a slab end the outer rank-NBO update is split into the next
+        // slab's columns (stream 0, needed by the next POTRF/TRSM) and the rest
+        // (stream 1), which overlaps the next slab's factorization.  A later outer
+        // update of overlapping columns waits for the stream-1 work first.
+        int b_pending = -1;
+        // rows [c_lo, r_hi) of columns [c_lo, c_hi) -= their product over columns [ka, kb)
+        auto add_update = [&](std::vector<GemmTask>& vec, double& fl, double* pan, int m, int r_hi, int c_lo, int c_hi,
+                              int ka, int kb) {
+            if (c_hi <= c_lo || kb <= ka || r_hi <= c_lo) return;
+            GemmTask t {};
+            t.C = pan + (int64_t)c_lo * m + c_lo;
+            t.A = pan + (int64_t)ka * m + c_lo;
+            t.ldc = m;
+            t.lda = m;
+            t.M = r_hi - c_lo;
+            t.N = c_hi - c_lo;
+            t.K = kb - ka;
+            vec.push_back(t);
+            fl += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
+        };
+        // tall mode (a front of more than one 64-column block): the 64-column chain
+        // (POTRF / TRSM / inner updates) runs on the slab's diagonal-block rows only; at
+        // the slab end the block inverses and one tall-TRSM launch solve every row below
+        // the slab (panel_tall_kernel), then the outer updates as before
+        auto tall = [&](int32_t s) { return S.opt.panel_tall && S.w(s) > PNB; };
+        for (int k0 = 0; k0 < maxw; k0 += PNB) {
+            Launch Lp {};
+            Lp.kind = L_POTRF;
+            Lp.level = lev;
+            Lp.vr = v;
+            Lp.off = (int64_t)potrf.size();
+            Launch Lt {};
+            Lt.kind = L_TRSM;
+            Lt.level = lev;
+            Lt.vr = v;
+            Lt.off = (int64_t)trsm.size();
+            std::vector<GemmTask> upd, outer_a, outer_b;
+            std::vector<TrsmTask> trsm_part;  // partial last blocks: own launch (big = 1)
+            std::vector<int2> inv_t;           // tall mode, slab end: diagonal-block inverses
+            std::vector<int4> tall_t;          // ... and the tall TRSM of the rows below
+            double uflops = 0.0, afl = 0.0, bfl = 0.0;
+            for (int32_t s : large) {
+                const int w = S.w(s), m = S.sn_m[s];
+                if (w <= k0) continue;
+                const int nb = std::min(PNB, w - k0);
+                const int k1 = k0 + nb;
+                const int slab0 = (k0 / NBO) * NBO;
+                const int slab1 = std::min(w, slab0 + NBO);
+                const int rend = tall(s) ? slab1 : m;  // rows of this step's TRSM and inner update
+                if (nb < PNB) {
+                    potrf.push_back(make_int2(s, k0));
+                    for (int r0 = k1; r0 < rend; r0 += TRSM_ROWS) trsm_part.push_back(TrsmTask {s, k0, r0, rend, 0});
+                } else {  // fused POTRF (one task if no rows below); ctr - 1: arrival counter
+                    const int ctr = (int)trsm.size() + 1;
+                    for (int r0 = k1; r0 < std::max(rend, k1 + 1); r0 += TRSM_ROWS)
+                        trsm.push_back(TrsmTask {s, k0, r0, rend, ctr});
+                }
+                double* pan = panel_pool + poff[s];
+                if (k1 < slab1 && S.opt.inner_order == 1) {
+                    // recursive order: block b of the slab closes a run of 2^t blocks
+                    // (t = trailing zeros of b + 1); that run updates the next 2^t
+                    // blocks (K = 64 * 2^t).  Same flops and dependencies as
+                    // right-looking, 768 instead of 1792 C columns rewritten per slab.
+                    const int b = (k0 - slab0) / PNB;
+                    const int span = PNB << __builtin_ctz((unsigned)(b + 1));
+                    add_update(upd, uflops, pan, m, rend, k1, std::min(slab1, k1 + span), k1 - span, k1);
+                } else if (k1 < slab1) {
+                    add_update(upd, uflops, pan, m, rend, k1, slab1, k0, k1);
+                }
+                if (k1 == slab1 && tall(s)) {
+                    for (int kb = slab0; kb < slab1; kb += PNB) inv_t.push_back(make_int2(s, kb));
+                    for (int r0 = slab1; r0 < m; r0 += TALL_ROWS) tall_t.push_back(make_int4(s, slab0, r0, slab1));
+                }
+                if (k1 == slab1 && slab1 < w) {
+                    // outer_a is the last update of block slab1: a pending stream-1 outer
+                    // update of those columns is waited for before outer_a runs
+                    const int nxt = S.opt.lookahead ? std::min(w, slab1 + NBO) : w;
+                    add_update(outer_a, afl, pan, m, m, slab1, nxt, slab0, slab1);
+                    add_update(outer_b, bfl, pan, m, m, nxt, w, slab0, slab1);
+                }
+            }
+            Lp.count = (int32_t)((int64_t)potrf.size() - Lp.off);
+            Lt.count = (int32_t)((int64_t)trsm.size() - Lt.off);
+            if (Lp.count > 0) N.sched.push_back(Lp);
+            if (Lt.count > 0) N.sched.push_back(Lt);
+            if (!trsm_part.empty()) {
+                Launch Lq = Lt;
+                Lq.off = (int64_t)trsm.size();
+                Lq.count = (int32_t)trsm_part.size();
+                Lq.big = 1;
+                trsm.insert(trsm.end(), trsm_part.begin(), trsm_part.end());
+                N.sched.push_back(Lq);
+            }
+            push_gemm_launch(L_PANEL, lev, upd, 0, uflops);
+            if (!tall_t.empty() || !inv_t.empty()) {
+                Launch Li {};
+                Li.kind = L_INV;
+                Li.level = lev;
+                Li.vr = v;
+                Li.off = (int64_t)B.inv.size();
+                Li.count = (int32_t)inv_t.size();
+                B.inv.insert(B.inv.end(), inv_t.begin(), inv_t.end());
+                if (Li.count > 0) N.sched.push_back(Li);
+                Launch Lt2 {};
+                Lt2.kind = L_TALL;
+                Lt2.level = lev;
+                Lt2.vr = v;
+                Lt2.off = (int64_t)B.tall.size();
+                Lt2.count = (int32_t)tall_t.size();
+                B.tall.insert(B.tall.end(), tall_t.begin(), tall_t.end());
+                if (Lt2.count > 0) N.sched.push_back(Lt2);
+            }
+            // split fronts: a slab is final after the TRSM of its last block (tall mode:
+            // after the slab's tall TRSM); at a slab end no inner update is pending
+            for (int32_t s : large) {
+                const int w = S.w(s);
+                if (!is_split(s) || w <= k0 || slab_step0[s] < 0) continue;
+                const int k1 = std::min(w, k0 + PNB);
+                if (k1 == w || k1 % D.nbo == 0) emit_step(slab_step0[s] + k0 / D.nbo);
+            }
+            int e_trsm = -1;
+            if (!outer_b.empty()) e_trsm = push_record(0);
+            if (!outer_a.empty()) {
+                if (b_pending >= 0) {
+                    push_wait(0, b_pending);
+                    b_pending = -1;
+                }
+                push_gemm_launch(L_PANEL, lev, outer_a, 0, afl);
+            }
+            if (!outer_b.empty()) {
+                push_wait(1, e_trsm);
+                push_gemm_launch(L_PANEL, lev, outer_b, 0, bfl, 1);
+                b_pending = push_record(1);
+            }
+        }
+        if (b_pending >= 0) push_wait(0, b_pending);
+        // early-delivery children: the CB SYRK in column groups, an event after each
+        // (the group's comm sub-step waits for exactly that event)
+        for (int32_t s : large) {
+            if (!is_early_sender(s, v)) continue;
+            const int w = S.w(s), m = S.sn_m[s], mb = m - w;
+            for (int j0 = 0; j0 < mb; j0 += D.early_gw) {
+                GemmTask t {};
+                t.C = cb_pool + coff[s] + (int64_t)j0 * mb + j0;
+                t.A = panel_pool + poff[s] + w + j0;
+                t.ldc = mb;
+                t.lda = m;
+                t.M = mb - j0;
+                t.N = std::min(D.early_gw, mb - j0);
+                t.K = w;
+                const double fl = 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
+                push_gemm_launch(L_CB, lev, std::vector<GemmTask> {t}, w >= 256 ? 1 : 0, fl);
+                early_ev[s].push_back(push_record(0));
+            }
+        }
+        // contribution-block SYRK, K = w; fronts with w >= 256 in their own launch
+        for (int big = 1; big >= 0; --big) {
+            std::vector<GemmTask> cbt;
+            double fl = 0.0;
+            for (int32_t s : large) {
+                const int w = S.w(s), m = S.sn_m[s], mb = m - w;
+                if (mb <= 0 || (w >= 256) != (big == 1) || is_split(s) || is_early_sender(s, v)) continue;
+                GemmTask t {};
+                t.C = cb_pool + coff[s];
+                t.A = panel_pool + poff[s] + w;
+                t.ldc = mb;
+                t.lda = m;
+                t.M = mb;
+                t.N = mb;
+                t.K = w;
+                if (gather(s)) {
+                    t.gs = s;
+                    t.gv = v;
+                }
+                cbt.push_back(t);
+                fl += (double)mb * (mb + 1.0) * t.K;
+            }
+            push_gemm_launch(L_CB, lev, cbt, big, fl);
+        }
+    };
+    // Distributed panel of front s (dist.cpp): every hosted rank of its holders.  Per
+    // slab k: its owner factors it (the 64-column POTRF / TRSM / inner-update chain
+    // on the main stream), the SLAB step moves it, then every rank that needs it
+    // updates its own next slab on the main stream (critical path) and its other
+    // later slabs and CB blocks on the lookahead stream.  A lookahead-stream update
+    // of slab j (from slab k <= j - 2) is waited for before the main stream touches
+    // slab j (event after the lookahead launch of step j - 2, covering all earlier
+    // ones: the stream is in order).
+    auto emit_dist_front = [&](int32_t lev, int32_t s) {
+        const int q = D.pd[s];
+        const std::vector<int32_t>& sr = D.slab_rank[q];
+        const int w = S.w(s), m = S.sn_m[s], mb = m - w, nsl = (int)sr.size();
+        const int own = D.owner[s];
+        std::vector<int> vs;  // hosted holders
+        for (int32_t r : D.holders[q])
+            if (hosted_of[r] >= 0) vs.push_back(hosted_of[r]);
+        if (hosted_of[own] >= 0 && std::find(vs.begin(), vs.end(), hosted_of[own]) == vs.end())
+            vs.push_back(hosted_of[own]);
+        if (vs.empty()) return;
+        auto pan_of = [&](int v) { return N.R[v].P.panel_pool + N.R[v].panel_off[s]; };
+        auto slab_c0 = [&](int k) { return k * D.nbo; };
+        auto slab_c1 = [&](int k) { return std::min(w, (k + 1) * D.nbo); };
+        const int vo = hosted_of[own];
+        if (vo >= 0) {  // the owner assembles the whole front (tiled or column-streaming)
+            const int tile_min_m = S.opt.asm_tile_min_m > 0 ? S.opt.asm_tile_min_m : ASM_TILE_MIN_M;
+            Launch L {};
+            L.kind = L_ASM;
+            L.level = lev;
+            L.vr = vo;
+            L.big = m >= tile_min_m ? 1 : 0;
+            L.off = (int64_t)asmv.size();
+            for (int cb = 0; cb * ASM_COLS < m; ++cb) {
+                if (!L.big) {
+                    asmv.push_back(make_int2(s, cb));
+                    continue;
+                }
+                for (int kk = cb * ASM_COLS / ASM_ROWS; kk * ASM_ROWS < m; ++kk)
+                    asmv.push_back(make_int2(s, (kk << 16) | cb));
+            }
+            L.count = (int32_t)((int64_t)asmv.size() - L.off);
+            N.sched.push_back(L);
+        }
+        emit_step(init_step[s]);
+        std::vector<std::vector<int>> ev1((size_t)N.R.size(), std::vector<int>((size_t)nsl, -1));
+        auto last_ev1 = [&](int v, int kmax) {  // latest lookahead event of steps <= kmax
+            for (int k = std::min(kmax, nsl - 1); k >= 0; --k)
+                if (ev1[v][k] >= 0) return ev1[v][k];
+            return -1;
+        };
+        auto upd_task = [&](std::vector<GemmTask>& vec, double& fl, double* C, int64_t ldc, const double* A,
+                            int64_t lda, int M, int Nn, int K) {
+            if (M <= 0 || Nn <= 0 || K <= 0) return;
+            GemmTask t {};
+            t.C = C;
+            t.A = A;
+            t.ldc = ldc;
+            t.lda = lda;
+            t.M = M;
+            t.N = Nn;
+            t.K = K;
+            vec.push_back(t);
+            fl += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
+        };
+        for (int k = 0; k < nsl; ++k) {
+            const int k0s = slab_c0(k), k1s = slab_c1(k);
+            const int vk = hosted_of[sr[k]];
+            if (vk >= 0) {
+                // factor slab k: per 64 columns POTRF, TRSM of the rows below, and the
+                // update of the slab's next columns (recursive order, as emit_level)
+                const int e = last_ev1(vk, k - 2);
+                if (e >= 0) push_wait(0, e);
+                double* pan = pan_of(vk);
+                for (int k0 = k0s; k0 < k1s; k0 += PNB) {
+                    const int nb = std::min(PNB, k1s - k0), k1 = k0 + nb;
+                    Launch Lp {};
+                    Lp.kind = L_POTRF;
+                    Lp.level = lev;
+                    Lp.vr = vk;
+                    Lp.off = (int64_t)potrf.size();
+                    Lp.count = 1;
+                    if (nb < PNB) {  // full blocks: POTRF fused into the TRSM
+                        potrf.push_back(make_int2(s, k0));
+                        N.sched.push_back(Lp);
+                    }
+                    Launch Lt {};
+                    Lt.kind = L_TRSM;
+                    Lt.level = lev;
+                    Lt.vr = vk;
+                    Lt.off = (int64_t)trsm.size();
+                    Lt.big = nb < PNB ? 1 : 0;
+                    const int ctr = nb < PNB ? 0 : (int)trsm.size() + 1;  // fused POTRF: arrival counter
+                    for (int r0 = k1; r0 < (nb < PNB ? m : std::max(m, k1 + 1)); r0 += TRSM_ROWS)
+                        trsm.push_back(TrsmTask {s, k0, r0, m, ctr});
+                    Lt.count = (int32_t)((int64_t)trsm.size() - Lt.off);
+                    if (Lt.count > 0) N.sched.push_back(Lt);
+                    if (k1 < k1s) {
+                        std::vector<GemmTask> upd;
+                        double fl = 0.0;
+                        if (S.opt.inner_order == 1) {
+                            const int b = (k0 - k0s) / PNB;
+                            const int span = PNB << __builtin_ctz((unsigned)(b + 1));
+                            const int c1 = std::min(k1s, k1 + span);
+                            upd_task(upd, fl, pan + (int64_t)k1 * m + k1, m, pan + (int64_t)(k1 - span) * m + k1, m,
+                                     m - k1, c1 - k1, span);
+                        } else {
+                            upd_task(upd, fl, pan + (int64_t)k1 * m + k1, m, pan + (int64_t)k0 * m + k1, m, m - k1,
+                                     k1s - k1, nb);
+                        }
+                        push_gemm_launch(L_PANEL, lev, upd, 0, fl);
+                    }
+                }
+            }
+            if (slab_step[s].size() > (size_t)k) emit_step(slab_step[s][k]);
+            // slab k's update on every hosted rank that needs it
+            for (int v : vs) {
+                const int r = N.R[v].rank;
+                if (D.need_row(S, s, k, r) >= m) continue;
+                double* pan = pan_of(v);
+                const double* Lk = pan + (int64_t)k0s * m;  // column k0s of the slab, row 0
+                const int K = k1s - k0s;
+                if (k + 1 < nsl && sr[k + 1] == r) {  // the next slab: critical path
+                    const int e = last_ev1(v, k - 1);
+                    if (e >= 0) push_wait(0, e);
+                    const int j0 = slab_c0(k + 1), j1 = slab_c1(k + 1);
+                    std::vector<GemmTask> t0;
+                    double fl = 0.0;
+                    upd_task(t0, fl, pan + (int64_t)j0 * m + j0, m, Lk + j0, m, m - j0, j1 - j0, K);
+                    push_gemm_launch(L_PANEL, lev, t0, 0, fl);
+                }
+                std::vector<GemmTask> t1;
+                double fl = 0.0;
+                for (int j = k + 2; j < nsl; ++j) {
+                    if (sr[j] != r) continue;
+                    const int j0 = slab_c0(j), j1 = slab_c1(j);
+                    upd_task(t1, fl, pan + (int64_t)j0 * m + j0, m, Lk + j0, m, m - j0, j1 - j0, K);
+                }
+                if (is_split(s)) {  // CB blocks: CB -= L21_k L21_k^T
+                    const std::vector<int32_t>& cbr = D.cb_rank[D.split[s]];
+                    for (int jb = 0; jb < (int)cbr.size(); ++jb) {
+                        if (cbr[jb] != r) continue;
+                        const int r0 = jb * D.cbb;
+                        int64_t ldc = 0;
+                        double* C = addr(v, R_CB, s, r0, r0, ldc);
+                        upd_task(t1, fl, C, ldc, Lk + w + r0, m, mb - r0, std::min(D.cbb, mb - r0), K);
+                    }
+                } else if (!is_split(s) && mb > 0 && r == own) {  // unsplit: the owner's whole CB
+                    int64_t ldc = 0;
+                    double* C = addr(v, R_CB, s, 0, 0, ldc);
+                    upd_task(t1, fl, C, ldc, Lk + w, m, mb, mb, K);
+                }
+                if (t1.empty()) continue;
+                push_wait(1, push_record(0));
+                push_gemm_launch(L_PANEL, lev, t1, 0, fl, 1);
+                ev1[v][k] = push_record(1);
+            }
+        }
+        for (int v : vs) {  // join the lookahead stream before the level's deliveries
+            const int e = last_ev1(v, nsl - 1);
+            if (e >= 0) push_wait(0, e);
+        }
+    };
+    if (multi) push_wait(2, push_record(0));  // previous factorization's reads are done
+    // multi-rank work-arena reuse guard (memplan.cpp): the comm steps of level L run
+    // after the main stream has finished level L - 1, and the main stream starts level
+    // L + 2 only after the comm steps of level L, so a region a step of level L touches
+    // is never reused before level L + 2
+    std::vector<int> comm_done((size_t)S.nlevels, -1);
+    // single device: a run of >= 2 levels holding one small front each (a chain: each
+    // front the parent of the one before) runs as one single-workgroup launch
+    auto chain_front = [&](int32_t lev) {
+        return !multi && by_level[lev].size() == 1 && S.fclass[by_level[lev][0]] == FRONT_SMALL;
+    };
+    // single device, a tiny tree (at most TINY_MAX_FRONTS fronts, all small with m <= 64,
+    // every image and CB fitting LDS): the whole factorization as one single-workgroup
+    // launch, postorder (the internal numbering), everything in LDS
+    bool tiny = !multi && S.ns > 1 && S.ns <= TINY_MAX_FRONTS;
+    {
+        int64_t lds = 0;
+        for (int32_t s = 0; tiny && s < S.ns; ++s) {
+            const int64_t m = S.sn_m[s], mb = S.mb(s);
+            tiny = S.fclass[s] == FRONT_SMALL && m <= 64;
+            lds += m * (m + 1) / 2 + mb * (mb + 1) / 2;
+        }
+        tiny = tiny && lds <= TINY_MAX_LDS;
+    }
+    if (tiny) {
+        auto pk = [](int64_t m, int64_t j) { return j * m - j * (j - 1) / 2; };
+        std::vector<int32_t> img((size_t)S.ns), cbo((size_t)S.ns);
+        int32_t off = 0;
+        for (int32_t s = 0; s < S.ns; ++s) {
+            img[s] = off;
+            off += S.sn_m[s] * (S.sn_m[s] + 1) / 2;
+            cbo[s] = off;
+            off += S.mb(s) * (S.mb(s) + 1) / 2;
+        }
+        B.tiny_lds = off;
+        for (int32_t s = 0; s < S.ns; ++s) {
+            const int m = S.sn_m[s], w = S.w(s), c0 = S.sn_start[s];
+            TinyFront f {};
+            f.s = s;
+            f.c0 = c0;
+            f.w = w;
+            f.m = m;
+            f.img = img[s];
+            f.cb = cbo[s];
+            f.e0 = (int32_t)B.tph.size();
+            f.panel_off = N.R[0].panel_off[s];
+            for (int lc = 0; lc < w; ++lc)
+                for (int64_t q = S.a_ptr[c0 + lc]; q < S.a_ptr[c0 + lc + 1]; ++q)
+                    B.ta.push_back(make_int2((int32_t)S.a_src[q], img[s] + (int32_t)(pk(m, lc) + S.a_pos[q] - lc)));
+            for (int32_t ci = S.child_ptr[s]; ci < S.child_ptr[s + 1]; ++ci) {
+                const int32_t c = S.child_list[ci];
+                const int mbc = S.mb(c);
+                const int32_t* rel = S.relind.data() + S.rel_ptr[c];
+                const int32_t beg = (int32_t)B.tpr.size();
+                for (int jc = 0; jc < mbc; ++jc)
+                    for (int ic = jc; ic < mbc; ++ic)
+                        B.tpr.push_back(make_int2(cbo[c] + (int32_t)(pk(mbc, jc) + ic - jc),
+                                                  img[s] + (int32_t)(pk(m, rel[jc]) + rel[ic] - rel[jc])));
+                B.tph.push_back(make_int2(beg, (int32_t)B.tpr.size()));
+            }
+            f.np = (int32_t)B.tph.size() - f.e0;
+            B.tfr.push_back(f);
+        }
+        Launch L {};
+        L.kind = L_SMALL;
+        L.level = 0;
+        L.maxm = 64;
+        L.big = 2;  // tiny tree
+        L.count = 1;
+        N.sched.push_back(L);
+    }
+    for (int32_t lev = tiny ? S.nlevels : 0; lev < S.nlevels; ++lev) {
+        if (chain_front(lev) && lev + 1 < S.nlevels && chain_front(lev + 1)) {
+            Launch L {};
+            L.kind = L_SMALL;
+            L.level = lev;
+            L.off = (int64_t)B.cdesc.size();
+            L.maxm = 32;
+            L.big = 1;  // chain
+            int32_t sp = -1;
+            for (; lev < S.nlevels && chain_front(lev) && (int64_t)B.cdesc.size() - L.off < CHAIN_MAXF; ++lev) {
+                const int32_t s = by_level[lev][0];
+                const int w = S.w(s), m = S.sn_m[s];
+                L.maxm = std::max(L.maxm, bucket_of(m));
+                ChainDesc d {};
+                d.s = s;
+                d.c0 = S.sn_start[s];
+                d.w = w;
+                d.m = m;
+                d.sp = sp;
+                d.panel_off = N.R[0].panel_off[s];
+                d.cb_off = N.R[0].cb_off[s] < 0 ? 0 : N.R[0].cb_off[s];
+                d.init_off = B.chain_init;
+                d.relp_off = (int64_t)B.crelp.size();
+                for (int t0 = 0; t0 < m; t0 += 4) {  // parent rows of CB rows, packed per tile row
+                    uint32_t wd = 0;
+                    for (int t = 0; t < 4; ++t) {
+                        const int i = t0 + t;
+                        const int32_t pr = (i >= w && i < m) ? S.relind[(size_t)S.rel_ptr[s] + (i - w)] : 0;
+                        wd |= (uint32_t)(pr & 255) << (8 * t);
+                    }
+                    B.crelp.push_back(wd);
+                }
+                B.chain_init += ((int64_t)m * (m + 1) / 2 + 63) / 64 * 64;
+                B.cdesc.push_back(d);
+                sp = s;
+            }
+            L.count = (int32_t)((int64_t)B.cdesc.size() - L.off);
+            N.sched.push_back(L);
+            --lev;
+            continue;
+        }
+        if (multi) {
+            if (lev >= 2 && comm_done[lev - 2] >= 0) push_wait(0, comm_done[lev - 2]);
+            push_wait(2, push_record(0));
+        }
+        for (size_t v = 0; v < N.R.size(); ++v) {
+            if (!multi) {
+                emit_level(lev, by_level[lev], (int)v);
+                continue;
+            }
+            std::vector<int32_t> mine;
+            for (int32_t s : by_level[lev])
+                if (D.owner[s] == N.R[v].rank && !is_dpanel(s)) mine.push_back(s);
+            if (!mine.empty()) emit_level(lev, mine, (int)v);
+        }
+        if (!multi) continue;
+        for (int32_t s : by_level[lev])
+            if (is_dpanel(s)) emit_dist_front(lev, s);
+        // contribution-block ranks of this level's split fronts (emulated: after the
+        // owners' panels, whose steps already moved the data)
+        for (int32_t s : by_level[lev]) {
+            if (!is_split(s) || is_dpanel(s)) continue;
+            const std::vector<int32_t>& cbr = D.cb_rank[D.split[s]];
+            for (size_t v = 0; v < N.R.size(); ++v) {
+                const int who = N.R[v].rank;
+                if (who != D.owner[s] && std::find(cbr.begin(), cbr.end(), who) != cbr.end())
+                    emit_cb_rank(lev, s, (int)v);
+            }
+        }
+        // contribution blocks that leave / enter the hosted ranks after this level:
+        // early children's column groups first, then the rest
+        for (int32_t c : by_level[lev]) {
+            if (!D.early[c] || early_step0[c] < 0) continue;
+            const int ng = (S.mb(c) + D.early_gw - 1) / D.early_gw;
+            const int vs = hosted_of[D.owner[c]];
+            for (int g = 0; g < ng; ++g)
+                emit_step(early_step0[c] + g, vs >= 0 && !early_ev[c].empty() ? early_ev[c][g] : -1);
+        }
+        emit_step(deliver_step[lev]);
+        comm_done[lev] = push_record(2);
+    }
+    if (multi) push_wait(0, push_record(2));  // join the comm stream (its last sends)
+    if (!N.err.empty()) return SC_ERR_ARG;
+    return SC_OK;
+}
+
+}  // namespace sc
