@@ -71,7 +71,7 @@ def cb_syrk_traffic():
     """HBM bytes per CB SYRK launch from the committed PMC profile
     (scripts/gpu_pmc.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE
     doubled per the gfx950 note); None when the profile is absent."""
-    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r02", "pmc_summary.json")
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r03", "pmc_summary.json")
     try:
         with open(p) as f:
             cb = json.load(f)["cb_syrk_128"]
@@ -79,14 +79,14 @@ def cb_syrk_traffic():
         return None, None
     b = cb["fetch_bytes_per_launch"] + cb["write_bytes_per_launch"]
     return round(b), ("bytes per syrk_mfma_kernel<128,2,4,1> launch (FETCH_SIZE x2 + WRITE_SIZE), "
-                      "profiles/r02/pmc_summary.json; L2-miss bytes incl. Infinity-Cache hits")
+                      "profiles/r03/pmc_summary.json; L2-miss bytes incl. Infinity-Cache hits")
 
 
 def cb_syrk_mfma_counters():
     """MFMA utilisation and clock of the CB SYRK from the committed counter pass
     (scripts/gpu_mfma_util.sh: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024
     SIMDs) on an eager bench step); None when the profile is absent."""
-    p = os.path.join(ROOT, "profiles", "r02", "mfma_util.json")
+    p = os.path.join(ROOT, "profiles", "r03", "mfma_util.json")
     try:
         with open(p) as f:
             ks = json.load(f)["step_kernels"]
@@ -95,7 +95,7 @@ def cb_syrk_mfma_counters():
     for name, v in ks.items():
         if "syrk_mfma_kernel<128, 2, 4, 1>" in name or "syrk_mfma_kernel<128, 2, 4, 1, 0>" in name:
             return {"mfma_busy_frac": v["raw_mfma_ratio"], "clock_GHz": v["clock_GHz"],
-                    "source": "profiles/r02/mfma_util.json (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE)"}
+                    "source": "profiles/r03/mfma_util.json (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE)"}
     return None
 
 

@@ -18,7 +18,7 @@ def short(n):
                  ("syrk_mfma_kernel<64, 2, 2, 1", "CB64"), ("syrk_mfma_kernel<128, 2, 4, 0, 0>", "LA"),
                  ("syrk_mfma_kernel<128, 2, 4, 0, 1>", "UPD128"), ("syrk_mfma_kernel<64, 2, 2, 0, 1>", "UPD64"),
                  ("panel_tall", "TALL"), ("solve_inv", "INV"), ("assemble", "ASM"), ("stamp", "stamp"),
-                 ("solve", "solve"), ("front_small", "small")):
+                 ("solve_fwd", "solve"), ("solve_gemv", "solve"), ("solve_diag", "solve"), ("front_small", "small")):
         if k in n:
             return v
     return n[:24]
@@ -43,7 +43,7 @@ def main():
         if not seg:
             continue
         t0 = seg[0][1]
-        chain_end = max(r[2] for r in seg if r[0] not in ("CB", "stamp"))
+        chain_end = max(r[2] for r in seg if r[0] in ("TRSM", "TRSMp", "POTRF", "LA", "UPD128", "UPD64", "ASM", "TALL"))
         la = [r for r in seg if r[0] == "LA"]
         tr = [r for r in seg if r[0] == "TRSM"]
         print(f"{name}: panel phase {(chain_end - t0) / 1e6:.2f} ms, lookahead launches {len(la)} "

@@ -512,8 +512,16 @@ __global__ __launch_bounds__(256) void tiny_tree_kernel(DevPlan P, TinyPlan T, c
     extern __shared__ double Lm[];
     __shared__ __attribute__((aligned(16))) double colbuf[2 * 4 * COLB];
     __shared__ TinyFront fr[TINY_MAX_FRONTS];
+    __shared__ int2 s_ph[TINY_MAX_FRONTS * TINY_MAX_FRONTS];
+    __shared__ int2 s_pr[TINY_PR_LDS];
+    __shared__ int32_t s_info;
     const int tid = threadIdx.x;
+    // every plan word this workgroup will read, and the A values, loaded in one pass:
+    // one global latency instead of one per extend-add phase
     if (tid < T.nf) fr[tid] = T.fr[tid];
+    for (int e = tid; e < T.nph; e += 256) s_ph[e] = T.ph[e];
+    for (int e = tid; e < min(T.npr, TINY_PR_LDS); e += 256) s_pr[e] = T.pr[e];
+    if (tid == 0) s_info = 0x7f7f7f7f;
     for (int i = tid; i < T.lds; i += 256) Lm[i] = 0.0;
     lds_barrier();
     for (int e = tid; e < T.na; e += 256) {
@@ -521,12 +529,13 @@ __global__ __launch_bounds__(256) void tiny_tree_kernel(DevPlan P, TinyPlan T, c
         Lm[a.y] = Ax[a.x];
     }
     lds_barrier();
+    int32_t* info = T.host_info ? &s_info : P.info;
     for (int f = 0; f < T.nf; ++f) {
         const TinyFront d = fr[f];
         for (int p = 0; p < d.np; ++p) {
-            const int2 q = T.ph[d.e0 + p];
+            const int2 q = s_ph[d.e0 + p];
             for (int e = q.x + tid; e < q.y; e += 256) {
-                const int2 pr = T.pr[e];
+                const int2 pr = e < TINY_PR_LDS ? s_pr[e] : T.pr[e];
                 Lm[pr.y] += Lm[pr.x];
             }
             lds_barrier();
@@ -534,7 +543,7 @@ __global__ __launch_bounds__(256) void tiny_tree_kernel(DevPlan P, TinyPlan T, c
         SmallRegs<1> R;
         small_tiles<1>(R, d.m, d.w);
         small_load<1>(R, Lm + d.img, d.m);
-        small_steps<1>(R, colbuf, d.w, P.info, d.c0);
+        small_steps<1>(R, colbuf, d.w, info, d.c0);
         small_store_panel<1>(R, P.panel_pool + d.panel_off, d.m, d.w);
         if (d.m > d.w && R.bi[0] >= 0) {
             const int mb = d.m - d.w;
@@ -549,11 +558,16 @@ __global__ __launch_bounds__(256) void tiny_tree_kernel(DevPlan P, TinyPlan T, c
         }
         lds_barrier();
     }
+    if (T.host_info && tid == 0) {  // the status word straight to the pinned host copy
+        P.info[0] = s_info;
+        __hip_atomic_store(T.host_info, s_info, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 hipError_t launch_tiny_tree(const DevPlan& P, const TinyPlan& T, int maxm, const double* Ax, hipStream_t st) {
     if (T.nf <= 0) return hipSuccess;
-    if (T.nf > TINY_MAX_FRONTS || T.lds > TINY_MAX_LDS || maxm > 64) return hipErrorInvalidValue;
+    if (T.nf > TINY_MAX_FRONTS || T.lds > TINY_MAX_LDS || maxm > 64 || T.nph > TINY_MAX_FRONTS * TINY_MAX_FRONTS)
+        return hipErrorInvalidValue;
     hipLaunchKernelGGL(tiny_tree_kernel, dim3(1), dim3(256), (size_t)T.lds * sizeof(double), st, P, T, Ax);
     return hipGetLastError();
 }

@@ -155,9 +155,12 @@ struct TinyPlan {
     const int2* pr;   // (LDS CB index, LDS image index)
     int32_t nf, na, nph, npr;
     int32_t lds;      // doubles of images + CBs
+    int32_t* host_info;  // device view of the handle's pinned status word: the kernel owns the status
+                         // (no reset / copy launches around it), or null
 };
 constexpr int TINY_MAX_FRONTS = 16;
 constexpr int TINY_MAX_LDS = 12288;  // doubles of images + CBs (96 KB)
+constexpr int TINY_PR_LDS = 2048;    // extend-add pairs staged in LDS with the A loads (the rest from HBM)
 hipError_t launch_tiny_tree(const DevPlan& P, const TinyPlan& T, int maxm, const double* Ax, hipStream_t st);
 
 hipError_t launch_front_chain(const DevPlan& P, const ChainPlan& C, int first, int count, int maxm,

@@ -160,7 +160,8 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     if ((rc = dalloc(N, 64, p))) return fail(rc);
     N.d_info = (int32_t*)p;
     P0.info = N.d_info;
-    if (hipHostMalloc((void**)&N.h_info, sizeof(int32_t) * 16, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc((void**)&N.h_info, sizeof(int32_t) * 16, hipHostMallocMapped | hipHostMallocCoherent) !=
+        hipSuccess) {
         N.err = "hipHostMalloc failed";
         return fail(SC_ERR_NOMEM);
     }
@@ -243,6 +244,17 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
         N.TP.nph = (int32_t)B.tph.size();
         N.TP.npr = (int32_t)B.tpr.size();
         N.TP.lds = B.tiny_lds;
+        // a tiny-tree handle is one launch: the kernel owns the status word (initial
+        // value, failures, the copy to pinned host memory), so a factorization is one
+        // dispatch with no reset / copy around it
+        if (N.sched.size() == 1 && N.sched[0].kind == L_SMALL && N.sched[0].big == 2) {
+            void* dp = nullptr;
+            if (hipHostGetDevicePointer(&dp, N.h_info, 0) != hipSuccess) {
+                N.err = "hipHostGetDevicePointer failed";
+                return fail(SC_ERR_HIP);
+            }
+            N.TP.host_info = (int32_t*)dp;
+        }
     }
     if ((rc = upload(N, B.small, N.d_small)) || (rc = upload(N, B.asmv, N.d_asm)) ||
         (rc = upload(N, B.potrf, N.d_potrf)) || (rc = upload(N, B.trsm, N.d_trsm)) ||
@@ -291,7 +303,8 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
 }
 
 static int64_t enqueue_all(Numeric& N, const double* d_Ax, int prof) {
-    HIP_TRY(hipMemsetAsync(N.d_info, 0x7f, sizeof(int32_t), N.stream));
+    const bool own_status = N.TP.host_info != nullptr;  // tiny tree: the kernel writes the status
+    if (!own_status) HIP_TRY(hipMemsetAsync(N.d_info, 0x7f, sizeof(int32_t), N.stream));
     for (size_t i = 0; i < N.sched.size(); ++i) {
         const Launch& L = N.sched[i];
         const bool timed = prof == 1 && L.kind < L_RECORD;
@@ -305,7 +318,7 @@ static int64_t enqueue_all(Numeric& N, const double* d_Ax, int prof) {
     }
     // the status word to pinned host memory on the main stream, which every other
     // stream has joined by now: the status read needs one stream sync, no extra copy
-    HIP_TRY(hipMemcpyAsync(N.h_info, N.d_info, sizeof(int32_t), hipMemcpyDeviceToHost, N.stream));
+    if (!own_status) HIP_TRY(hipMemcpyAsync(N.h_info, N.d_info, sizeof(int32_t), hipMemcpyDeviceToHost, N.stream));
     return SC_OK;
 }
 

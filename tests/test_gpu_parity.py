@@ -116,6 +116,26 @@ def test_not_positive_definite_large_front(gpu):
     assert r.status > 0
 
 
+def test_not_positive_definite_tiny_tree(gpu, mtx):
+    # bcsstk01 runs as one tiny-tree launch that owns the status word (no reset / copy
+    # launches): a broken pivot must still be reported, with the oracle's column, and a
+    # refactorization with good values through the same handle must clear it
+    A = mtx("bcsstk01")
+    s = sc.Symbolic(A)
+    num = sc.Numeric(s)
+    assert num.factor(A.x) == 0
+    for k in (40, 3):
+        x = A.x.copy()
+        diag = A.p[k + 1] - 1
+        assert A.i[diag] == k
+        x[diag] = -1.0
+        B = sc.csc_matrix(A.n_rows, A.n_cols, A.p, A.i, x)
+        st, *_ = oracle.chol(B)
+        assert st > 0
+        assert num.factor(x) == st, (k, st)
+        assert num.factor(A.x) == 0
+
+
 def test_repeat_factorization_bitwise_deterministic(gpu):
     A = sc.laplacian3d(16)
     s = sc.Symbolic(A)
