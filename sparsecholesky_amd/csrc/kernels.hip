@@ -789,11 +789,19 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_partial_kernel(DevPlan P, cons
 // every workgroup of the block has read it: t.w - 1 indexes the block's arrival
 // counter, and the last workgroup to arrive stores L11 and rearms the counter.  A
 // block with no rows below gets one task with r0 >= m (factor and store only).
+#ifndef TRSM_PRE_CH
+#define TRSM_PRE_CH 16  // previous-block values of a row in flight per chunk (VGPR budget)
+#endif
+template <int PRE>
 __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, const TrsmTask* __restrict__ tasks,
                                                                  int32_t* __restrict__ arrive) {
     static_assert(TRSM_ROWS == 256, "the fused POTRF maps 4 x 4 tiles onto 256 threads");
     __shared__ double2 S[TRSM64_STREAM / 2];
     __shared__ __attribute__((aligned(16))) double colbuf[2 * 4 * COLB];
+    // PRE: Lp[j * LPD + k] = L(k0 + j, k0 - 64 + k), the pending block's rows of this diagonal
+    // block, row-major (k contiguous: a row's update reads two k per ds_read_b128)
+    constexpr int LPD = PNB + 2;
+    __shared__ __attribute__((aligned(16))) double Lp[PRE ? PNB * LPD : 2];
     __shared__ int s_last;
     const TrsmTask t = tasks[blockIdx.x];
     const int s = t.s, k0 = t.k0, r0 = t.r0, r1 = t.r1;
@@ -806,6 +814,14 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
     if (nb < PNB) return;  // partial blocks: potrf_tiles_kernel + trsm_partial_kernel
     double* blk = pan + (int64_t)k0 * m + k0;
     double* Sd = reinterpret_cast<double*>(S);
+    constexpr bool pre = PRE != 0;
+    if (pre) {  // the previous block's rows of this diagonal block, final since the last launch
+#pragma unroll
+        for (int q = 0; q < PNB * PNB / 256; ++q) {
+            const int e = tid + 256 * q, k = e >> 6, j = e & 63;  // lanes along j: coalesced rows
+            Lp[j * LPD + k] = pan[(int64_t)(k0 - PNB + k) * m + k0 + j];
+        }
+    }
     SmallRegs<1> R;
     small_tiles<1>(R, PNB, PNB);
 #pragma unroll
@@ -815,6 +831,26 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
             const int i = 4 * R.bi[0] + r, j = 4 * R.bj[0] + c;
             R.v[0][r * 4 + c] = (R.bi[0] >= 0 && i >= j) ? blk[(int64_t)j * m + i] : 0.0;
         }
+    if (pre) {  // diagonal block -= Lp^T Lp (this thread's 4 x 4 tile)
+        __syncthreads();
+        if (R.bi[0] >= 0) {
+            const int i0 = 4 * R.bi[0], j0 = 4 * R.bj[0];
+#pragma unroll 2
+            for (int k = 0; k < PNB; k += 2) {
+                double2 li[4], lj[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    li[r] = *reinterpret_cast<const double2*>(Lp + (i0 + r) * LPD + k);
+                    lj[r] = *reinterpret_cast<const double2*>(Lp + (j0 + r) * LPD + k);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+                        R.v[0][r * 4 + c] = fma(-li[r].y, lj[c].y, fma(-li[r].x, lj[c].x, R.v[0][r * 4 + c]));
+            }
+        }
+    }
     small_steps<1>(R, colbuf, PNB, P.info, c0 + k0);  // every block load has returned
     if (R.bi[0] >= 0) {
 #pragma unroll
@@ -832,6 +868,24 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
     double r[PNB];
 #pragma unroll
     for (int c = 0; c < PNB; ++c) r[c] = buf_ld(rs, voff, c * m * 8);
+    if (pre) {  // this row -= L(row, previous block) Lp: its 64 previous-block values streamed in
+        const __amdgpu_buffer_rsrc_t rp = buf_rsrc(pan + (int64_t)(k0 - PNB) * m, (uint32_t)m * PNB * 8u);
+#pragma unroll 1
+        for (int k0c = 0; k0c < PNB; k0c += TRSM_PRE_CH) {
+            double l[TRSM_PRE_CH];
+#pragma unroll
+            for (int q = 0; q < TRSM_PRE_CH; ++q) l[q] = buf_ld(rp, voff, (k0c + q) * m * 8);
+#pragma unroll
+            for (int c = 0; c < PNB; ++c) {
+                const double* lc = Lp + c * LPD + k0c;
+#pragma unroll
+                for (int q = 0; q < TRSM_PRE_CH; q += 2) {
+                    const double2 v = *reinterpret_cast<const double2*>(lc + q);
+                    r[c] = fma(-l[q + 1], v.y, fma(-l[q], v.x, r[c]));
+                }
+            }
+        }
+    }
     __syncthreads();
     if (tid == 0) {
         const int k1 = k0 + PNB;
@@ -1317,12 +1371,14 @@ hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hip
 }
 
 hipError_t launch_trsm_panel(const DevPlan& P, const TrsmTask* tasks, int count, hipStream_t st, bool partial,
-                             int32_t* arrive) {
+                             int32_t* arrive, bool pre) {
     if (count <= 0) return hipSuccess;
     if (partial)
         hipLaunchKernelGGL(trsm_partial_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks);
+    else if (pre)
+        hipLaunchKernelGGL(trsm_panel_g_kernel<1>, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks, arrive);
     else
-        hipLaunchKernelGGL(trsm_panel_g_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks, arrive);
+        hipLaunchKernelGGL(trsm_panel_g_kernel<0>, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks, arrive);
     return hipGetLastError();
 }
 

@@ -177,11 +177,14 @@ hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hip
 // [r0, min(r0 + TRSM_ROWS, r1)); ctr - 1 indexes the block's arrival counter (fused POTRF).
 struct TrsmTask {
     int32_t s, k0, r0, r1, ctr;
+    int32_t pre;  // 1: first apply the pending rank-64 update from block k0 - 64 (the recursive
+                  // order's span-64 inner update, folded into this launch; launch with pre = true)
 };
 // partial: blocks with nb < 64; else full blocks with the POTRF fused (arrive: the
 // per-block arrival counters, zeroed)
+// pre: every task folds in the pending span-64 update from block k0 - 64 (TrsmTask::pre)
 hipError_t launch_trsm_panel(const DevPlan& P, const TrsmTask* tasks, int count, hipStream_t st, bool partial,
-                             int32_t* arrive);
+                             int32_t* arrive, bool pre = false);
 // inv(L_jj) of factored 64 x 64 diagonal blocks (s, k0) into their strict upper
 // triangles (the tall TRSM's diagonal solves; the solve's block inverses are the same)
 hipError_t launch_panel_inv(const DevPlan& P, const int2* tasks, int count, hipStream_t st);

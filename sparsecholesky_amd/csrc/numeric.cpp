@@ -287,7 +287,8 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
         case L_POTRF:
             return launch_potrf_diag(N.R[L.vr].P, N.d_potrf + L.off, L.count, N.stream);
         case L_TRSM:
-            return launch_trsm_panel(N.R[L.vr].P, N.d_trsm + L.off, L.count, N.stream, L.big != 0, N.d_arrive);
+            return launch_trsm_panel(N.R[L.vr].P, N.d_trsm + L.off, L.count, N.stream, L.big != 0, N.d_arrive,
+                                     L.epi != 0);
         case L_PANEL:
         case L_CB:
             return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st, L.epi,

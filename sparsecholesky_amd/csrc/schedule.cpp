@@ -404,6 +404,11 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // the slab end the block inverses and one tall-TRSM launch solve every row below
         // the slab (panel_tall_kernel), then the outer updates as before
         auto tall = [&](int32_t s) { return S.opt.panel_tall && S.w(s) > PNB; };
+        // fronts whose next TRSM launch folds in the pending span-64 inner update (recursive
+        // order, an even block of the slab followed by a full block): the update launch of
+        // that step is dropped, one dispatch fewer on the chain per two steps
+        std::vector<char> pre_next((size_t)S.ns, 0);
+        auto fold = [&](int32_t s) { return S.opt.trsm_fold && S.opt.inner_order == 1 && !tall(s); };
         for (int k0 = 0; k0 < maxw; k0 += PNB) {
             Launch Lp {};
             Lp.kind = L_POTRF;
@@ -417,6 +422,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             Lt.off = (int64_t)trsm.size();
             std::vector<GemmTask> upd, outer_a, outer_b;
             std::vector<TrsmTask> trsm_part;  // partial last blocks: own launch (big = 1)
+            std::vector<TrsmTask> trsm_pre;   // full blocks folding the pending update in (own launch)
             std::vector<int2> inv_t;           // tall mode, slab end: diagonal-block inverses
             std::vector<int4> tall_t;          // ... and the tall TRSM of the rows below
             double uflops = 0.0, afl = 0.0, bfl = 0.0;
@@ -432,10 +438,12 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     potrf.push_back(make_int2(s, k0));
                     for (int r0 = k1; r0 < rend; r0 += TRSM_ROWS) trsm_part.push_back(TrsmTask {s, k0, r0, rend, 0});
                 } else {  // fused POTRF (one task if no rows below); ctr - 1: arrival counter
-                    const int ctr = (int)trsm.size() + 1;
+                    const int ctr = (int)(trsm.size() + trsm_pre.size()) + 1;
+                    const int pre = pre_next[s];
                     for (int r0 = k1; r0 < std::max(rend, k1 + 1); r0 += TRSM_ROWS)
-                        trsm.push_back(TrsmTask {s, k0, r0, rend, ctr});
+                        (pre ? trsm_pre : trsm).push_back(TrsmTask {s, k0, r0, rend, ctr, pre});
                 }
+                pre_next[s] = 0;
                 double* pan = panel_pool + poff[s];
                 if (k1 < slab1 && S.opt.inner_order == 1) {
                     // recursive order: block b of the slab closes a run of 2^t blocks
@@ -444,7 +452,10 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     // right-looking, 768 instead of 1792 C columns rewritten per slab.
                     const int b = (k0 - slab0) / PNB;
                     const int span = PNB << __builtin_ctz((unsigned)(b + 1));
-                    add_update(upd, uflops, pan, m, rend, k1, std::min(slab1, k1 + span), k1 - span, k1);
+                    if (span == PNB && nb == PNB && std::min(PNB, w - k1) == PNB && fold(s))
+                        pre_next[s] = 1;  // folded into the next TRSM launch
+                    else
+                        add_update(upd, uflops, pan, m, rend, k1, std::min(slab1, k1 + span), k1 - span, k1);
                 } else if (k1 < slab1) {
                     add_update(upd, uflops, pan, m, rend, k1, slab1, k0, k1);
                 }
@@ -464,6 +475,14 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             Lt.count = (int32_t)((int64_t)trsm.size() - Lt.off);
             if (Lp.count > 0) N.sched.push_back(Lp);
             if (Lt.count > 0) N.sched.push_back(Lt);
+            if (!trsm_pre.empty()) {
+                Launch Lr = Lt;
+                Lr.off = (int64_t)trsm.size();
+                Lr.count = (int32_t)trsm_pre.size();
+                Lr.epi = 1;  // the folding kernel instance
+                trsm.insert(trsm.end(), trsm_pre.begin(), trsm_pre.end());
+                N.sched.push_back(Lr);
+            }
             if (!trsm_part.empty()) {
                 Launch Lq = Lt;
                 Lq.off = (int64_t)trsm.size();
