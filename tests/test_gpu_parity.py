@@ -575,7 +575,7 @@ def test_dense_matrix_large_front(gpu):
 # recursive), lookahead (0 none, 1 trailing updates on a second stream), tiled assembly
 PANEL_OPTS = [dict(inner_order=0), dict(inner_order=0, lookahead=0), dict(lookahead=0), dict(asm_tile_min_m=1),
               dict(asm_tile_min_m=300), dict(panel_nb_outer=128, lookahead=0), dict(panel_tall=1),
-              dict(panel_tall=1, panel_nb_outer=128), dict(trsm_fold=0), dict(trsm_fold=0, panel_nb_outer=128)]
+              dict(panel_tall=1, panel_nb_outer=128), dict(trsm_fold=1), dict(trsm_fold=1, panel_nb_outer=128)]
 
 
 @pytest.mark.parametrize("opts", PANEL_OPTS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
