@@ -98,6 +98,9 @@ typedef struct sc_options {
                                 workgroup applies it to its rows and to the diagonal block) instead of being a
                                 launch of its own; 0 (default, measured faster at 128^3: 516 vs 533 ms): a
                                 separate update launch */
+    int32_t dist_slab_block; /* multi-GPU distributed panels: consecutive slabs per rank in the cyclic deal
+                                (default 2: every other slab hand-over is rank-local, off the critical path;
+                                capped at slabs / ranks so that every rank of the group gets a block) */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

@@ -97,7 +97,10 @@ case "$task" in
     rc=$?; echo "rccl rc=$rc"; grep -v "^$" gpurun_out/rccl_emul.log | tail -8; exit $rc ;;
   small)
     timeout -k 10 600 python3 scripts/small_configs.py > gpurun_out/small_configs.jsonl 2> gpurun_out/small_configs.err
-    rc=$?; echo "small rc=$rc"; cat gpurun_out/small_configs.jsonl; exit $rc ;;
+    rc=$?; echo "small rc=$rc"; cat gpurun_out/small_configs.jsonl; [ $rc -eq 0 ] || exit $rc
+    # kernel durations of the same runs (tiny tree, small-front levels)
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_small -o small -- \
+      python3 scripts/small_configs.py > /dev/null 2> gpurun_out/small_prof.err ;;
   solve)
     timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -k "solve" -x -v --timeout 240 \
       --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_solve.log 2>&1

@@ -71,6 +71,7 @@ class Options(C.Structure):
         ("asm_tile_min_m", C.c_int32), ("dist_split", C.c_int32), ("dist_cbb", C.c_int32),
         ("ordering", C.c_int32), ("dist_early", C.c_int32), ("dist_panel", C.c_int32),
         ("cb_gather", C.c_int32), ("panel_tall", C.c_int32), ("trsm_fold", C.c_int32),
+        ("dist_slab_block", C.c_int32),
     ]
 
 

@@ -89,6 +89,7 @@ void sc_default_options(sc_options* opt) {
     opt->cb_gather = 1;
     opt->panel_tall = 0;
     opt->trsm_fold = 0;
+    opt->dist_slab_block = 2;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,

@@ -171,10 +171,15 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
             // slab k on group rank (owner + k) mod g: the whole group is free at a
             // shared front (its subtrees are done), so the slabs go round the group
             // rather than to the ranks with the least total work
+            // slab blocks of dist_slab_block consecutive slabs per rank: the hand-over from a
+            // slab to the next (its owner's send, the next owner's update) leaves the critical
+            // path inside a block; a front with fewer than two blocks per rank deals single
+            // slabs (parallel trailing updates matter more there)
             const int g = hi - lo, nsl = (w + D.nbo - 1) / D.nbo;
+            const int sb = std::max(1, std::min(S.opt.dist_slab_block, nsl / g));
             std::vector<i32> sr((size_t)nsl);
             for (int k = 0; k < nsl; ++k) {
-                sr[k] = lo + (own - lo + k) % g;
+                sr[k] = lo + (own - lo + k / sb) % g;
                 D.work[sr[k]] += slab_work(S, s, k * D.nbo, std::min(w, (k + 1) * D.nbo));
             }
             D.pd[s] = (i32)D.pd_s.size();

@@ -101,20 +101,27 @@ def test_split_front_plan(k, nranks):
     assert (s0.dist_plan_info(nranks)["split_cb_ranks"] == 0).all()
 
 
+@pytest.mark.parametrize("sb", [1, 2, 3])
 @pytest.mark.parametrize("k,nranks", [(20, 4), (24, 8), (24, 3)])
-def test_distributed_panel_plan(k, nranks):
+def test_distributed_panel_plan(k, nranks, sb):
     # shared fronts wider than one slab (the root included) have their slabs factored
-    # slab-cyclic over the whole group; narrower or unshared fronts stay on one rank
-    s = sc.Symbolic(sc.laplacian3d(k), panel_nb_outer=128, dist_cbb=64, small_front_max=32)
+    # block-cyclic (sb consecutive slabs per rank) over the whole group; narrower or
+    # unshared fronts stay on one rank
+    s = sc.Symbolic(sc.laplacian3d(k), panel_nb_outer=128, dist_cbb=64, small_front_max=32, dist_slab_block=sb)
     info = s.dist_plan_info(nranks)
     sn = s.supernodes()
     g, slr = info["gsize"], info["slab_ranks"]
     root = int(np.nonzero(sn["parent"] < 0)[0][-1])
-    assert slr[root] == min(g[root], -(-int(sn["w"][root]) // 128))
+    def blocks(v):  # slab blocks of min(sb, nsl / g) slabs (at least one)
+        nsl = -(-int(sn["w"][v]) // 128)
+        b = max(1, min(sb, nsl // max(1, int(g[v]))))
+        return -(-nsl // b)
+
+    assert slr[root] == min(g[root], blocks(root))
     for v in range(len(g)):
         nsl = -(-int(sn["w"][v]) // 128)
         if g[v] > 1 and nsl > 1:
-            assert slr[v] == min(g[v], nsl)
+            assert slr[v] == min(g[v], blocks(v))
         else:
             assert slr[v] == 0
     s0 = sc.Symbolic(sc.laplacian3d(k), panel_nb_outer=128, dist_cbb=64, small_front_max=32, dist_panel=0)
