@@ -101,6 +101,15 @@ typedef struct sc_options {
     int32_t dist_slab_block; /* multi-GPU distributed panels: consecutive slabs per rank in the cyclic deal
                                 (default 2: every other slab hand-over is rank-local, off the critical path;
                                 capped at slabs / ranks so that every rank of the group gets a block) */
+    int32_t trsm_split_wg;   /* a 64-column chain step whose TRSM launch spans more than this many 256-row
+                                workgroups (more than the GPU holds at once) factors its diagonal blocks in a
+                                launch of their own (one workgroup per block) and the TRSM workgroups load the
+                                factored blocks instead of each refactoring them (default 1024; 0: always fused) */
+    int32_t syrk_lean_kmax;  /* SYRK launches on 64 x 64 tiles whose deepest K is at most this use the lean
+                                kernel instance (K staged 8 deep, 32-row extend-add chunks: half the LDS, six
+                                workgroups per CU instead of four); default 128, 0: never */
+    int32_t cb_tail_split;   /* 1 (default): the last, partial round of a deep-K CB launch on 128 x 128 tiles
+                                runs as 64 x 64 tiles in a launch of its own (a shorter tail); 0: one launch */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

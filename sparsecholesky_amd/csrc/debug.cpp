@@ -27,7 +27,8 @@ int64_t debug_syrk(double* dC, int ldc, const double* dA, int lda, int M, int Nn
     hipError_t e = hipMemcpy(d, &t, sizeof(t), hipMemcpyHostToDevice);
     if (e == hipSuccess && !tiles.empty())
         e = hipMemcpy(dt, tiles.data(), tiles.size() * sizeof(int2), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = launch_syrk(d, dt, (int)tiles.size(), bt, 0, nullptr);
+    // K <= 128: the lean instance (as the schedule's default syrk_lean_kmax picks it)
+    if (e == hipSuccess) e = launch_syrk(d, dt, (int)tiles.size(), bt, 0, nullptr, 0, nullptr, K <= 128);
     hipError_t e2 = hipDeviceSynchronize();
     (void)hipFree(d);
     (void)hipFree(dt);

@@ -801,7 +801,7 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
     // PRE: Lp[j * LPD + k] = L(k0 + j, k0 - 64 + k), the pending block's rows of this diagonal
     // block, row-major (k contiguous: a row's update reads two k per ds_read_b128)
     constexpr int LPD = PNB + 2;
-    __shared__ __attribute__((aligned(16))) double Lp[PRE ? PNB * LPD : 2];
+    __shared__ __attribute__((aligned(16))) double Lp[PRE == 1 ? PNB * LPD : 2];
     __shared__ int s_last;
     const TrsmTask t = tasks[blockIdx.x];
     const int s = t.s, k0 = t.k0, r0 = t.r0, r1 = t.r1;
@@ -814,7 +814,7 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
     if (nb < PNB) return;  // partial blocks: potrf_tiles_kernel + trsm_partial_kernel
     double* blk = pan + (int64_t)k0 * m + k0;
     double* Sd = reinterpret_cast<double*>(S);
-    constexpr bool pre = PRE != 0;
+    constexpr bool pre = PRE == 1;
     if (pre) {  // the previous block's rows of this diagonal block, final since the last launch
 #pragma unroll
         for (int q = 0; q < PNB * PNB / 256; ++q) {
@@ -831,6 +831,28 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
             const int i = 4 * R.bi[0] + r, j = 4 * R.bj[0] + c;
             R.v[0][r * 4 + c] = (R.bi[0] >= 0 && i >= j) ? blk[(int64_t)j * m + i] : 0.0;
         }
+    if constexpr (PRE == 2) {  // the block is L11 already (its own launch): stream it, solve the rows
+        if (R.bi[0] >= 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int i = 4 * R.bi[0] + r, j = 4 * R.bj[0] + c;
+                    if (i >= j) Sd[PNB * j - j * (j - 1) / 2 + (i - j)] = (i == j) ? 1.0 / R.v[0][r * 4 + c] : R.v[0][r * 4 + c];
+                }
+        }
+        const int row = r0 + tid;
+        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pan + (int64_t)k0 * m, (uint32_t)m * PNB * 8u);
+        const int voff = row < r1 ? row * 8 : BUF_DEAD;
+        double r[PNB];
+#pragma unroll
+        for (int c = 0; c < PNB; ++c) r[c] = buf_ld(rs, voff, c * m * 8);
+        __syncthreads();
+        trsm64_full(r, S);
+#pragma unroll
+        for (int c = 0; c < PNB; ++c) buf_st(r[c], rs, voff, c * m * 8);
+        return;
+    }
     if (pre) {  // diagonal block -= Lp^T Lp (this thread's 4 x 4 tile)
         __syncthreads();
         if (R.bi[0] >= 0) {
@@ -937,17 +959,19 @@ __device__ __forceinline__ T* uni_ptr(T* p) {
     return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
 }
 
-template <int BT, int WM, int WN>
+template <int BT, int WM, int WN, int BK = 16, int GR = 64>
 __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const DevPlan& P, int row0, int col0,
                                                      double4_t (&acc)[BT / WM / 16][BT / WN / 16], double* smem) {
     constexpr int NW = WM * WN, NT = 64 * NW;
     constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
-    constexpr int GR = 64, GLD = GR + 1;  // rows per chunk, LDS column stride (doubles)
+    // GR: rows per chunk (64, or 32 for the lean instance), GLD: LDS column stride
+    // (doubles); TB: row granularity of tile_bnd (the parent's 64-row CB blocks)
+    constexpr int GLD = GR + 1, TB = 64;
     // child columns per batch of loads: all of a wave's <= 64 / NW columns per child for
     // 64-tiles; 4 for 128-tiles (VGPR budget: 4 waves / SIMD)
-    constexpr int GQ = BT == 64 ? 64 / NW : SC_GATHER_Q;
+    constexpr int GQ = BT == 64 ? (GR == 32 ? 8 : 64 / NW) : SC_GATHER_Q;
     constexpr int GC = 64;  // children staged per pass (one lane each)
-    constexpr int OPS = 2 * 2 * 16 * (BT + 16);  // the operand stages' doubles (smem)
+    constexpr int OPS = 2 * 2 * BK * (BT + 16);  // the operand stages' doubles (smem)
     static_assert(BT * GLD + GC * 6 <= OPS, "gather chunk and child table fit the operand LDS");
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wr = wid / WN, wc = wid % WN;
@@ -966,7 +990,7 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const De
     const __amdgpu_buffer_rsrc_t rc = buf_rsrc(C + (int64_t)col0 * ldc, (uint32_t)(min(BT, T.N - col0) * ldc * 8));
 #pragma unroll 1
     for (int h = 0; h < BT / GR; ++h) {
-        const int r0 = row0 + h * GR;  // CB rows of this chunk: [r0, r0 + 64)
+        const int r0 = row0 + h * GR;  // CB rows of this chunk: [r0, r0 + GR)
         if (h) __syncthreads();        // previous chunk's G fully read
         for (int e = tid; e < BT * GLD; e += NT) G[e] = 0.0;
         for (int cbase = cp0;; cbase += GC) {
@@ -979,10 +1003,10 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const De
                 s_cb[lane] = P.cb_pool + P.cb_off[c];
                 s_rel[lane] = P.relind + P.rel_ptr[c];
                 s_int[0 * GC + lane] = mbc;
-                s_int[1 * GC + lane] = bnd_at(tb, r0 / GR, mbc);
-                s_int[2 * GC + lane] = bnd_at(tb, r0 / GR + 1, mbc);
-                s_int[3 * GC + lane] = bnd_at(tb, col0 / GR, mbc);
-                s_int[4 * GC + lane] = bnd_at(tb, (col0 + BT) / GR, mbc);
+                s_int[1 * GC + lane] = bnd_at(tb, r0 / TB, mbc);
+                s_int[2 * GC + lane] = bnd_at(tb, r0 / TB + 1, mbc);
+                s_int[3 * GC + lane] = bnd_at(tb, col0 / TB, mbc);
+                s_int[4 * GC + lane] = bnd_at(tb, (col0 + BT) / TB, mbc);
             }
             __syncthreads();
             for (int i = 0; r0 < mb && i < nc; ++i) {
@@ -994,7 +1018,8 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const De
                 const double* __restrict__ cb = uni_ptr(s_cb[i]);
                 // this lane's row of the chunk (<= 64 child rows map into 64 parent rows)
                 const int ic = ilo + lane;
-                const int prow = ic < ihi ? rel[ic] - w - r0 : -1;
+                int prow = ic < ihi ? rel[ic] - w - r0 : -1;
+                if (prow >= GR) prow = -1;  // 32-row chunks: the other half of the 64-row block
                 for (int jb = jlo; jb < jhi; jb += 64) {
                     const int jl = jb + lane;
                     const int pcl = jl < jhi ? rel[jl] - w - col0 : -1;
@@ -1053,11 +1078,11 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const De
 // each, +128 B row pad: the two k-rows read by a half-wave hit disjoint banks).
 // AGLC: the row0 operand is loaded with glc (L1 bypassed: rows this workgroup
 // itself stored earlier in the same launch).
-template <int BT, int WM, int WN, int AGLC = 0>
+template <int BT, int WM, int WN, int AGLC = 0, int BK = 16>
 __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t lda, int K, int M, int N, int row0,
                                            int col0, double4_t (&acc)[BT / WM / 16][BT / WN / 16], double* smem) {
+    static_assert(BK == 16 || BK == 8, "four-deep k sub-steps of the MFMA");
     constexpr int NT = 64 * WM * WN;
-    constexpr int BK = 16;
     constexpr int LDT = BT + 16;
     constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
     double(*As)[BK * LDT] = reinterpret_cast<double(*)[BK * LDT]>(smem);
@@ -1131,16 +1156,19 @@ __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t
             // between them and the barrier: 547 -> 532 ms at 128^3 (stores after sub-step
             // 1: 535.8; A after 1 and B after 2: 533.0; the loads issued after sub-step 0
             // instead: 533.3, both: 536.8)
-            if (kk == 8 && kt + 1 < nk) sstore(cur ^ 1);
+            if (kk == BK - 8 && kt + 1 < nk) sstore(cur ^ 1);
         }
         __syncthreads();
     }
 }
 
-template <int BT, int WM, int WN, int TAG, int EPI>
+// LEAN (short-K launches on 64 x 64 tiles): BK = 8 and 32-row gather chunks halve the
+// LDS (20 KB), so six workgroups fit a CU instead of four -- these launches are latency-
+// bound (a few K stages, then the C traffic), not MFMA-bound
+template <int BT, int WM, int WN, int TAG, int EPI, int LEAN = 0>
 __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ tasks, const int2* __restrict__ tiles,
                                                int bidx, const DevPlan* __restrict__ plans) {
-    constexpr int BK = 16;
+    constexpr int BK = LEAN ? 8 : 16;
     constexpr int LDT = BT + 16;
     constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
     __shared__ double smem[2 * 2 * BK * LDT];  // A and B stages
@@ -1164,11 +1192,11 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
     for (int a = 0; a < RTM; ++a)
 #pragma unroll
         for (int b = 0; b < RTN; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
-    mfma_kloop<BT, WM, WN>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
+    mfma_kloop<BT, WM, WN, 0, BK>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
 
     if constexpr (TAG == 1) {
         if (T.gs >= 0) {  // the front's CB is not assembled: gather the children's entries
-            syrk_gather_epilogue<BT, WM, WN>(T, plans[T.gv], row0, col0, acc, smem);
+            syrk_gather_epilogue<BT, WM, WN, BK, LEAN ? 32 : 64>(T, plans[T.gv], row0, col0, acc, smem);
             return;
         }
     }
@@ -1217,11 +1245,11 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
     }
 }
 
-template <int BT, int WM, int WN, int TAG, int EPI>
-__global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
+template <int BT, int WM, int WN, int TAG, int EPI, int LEAN = 0>
+__global__ __launch_bounds__(64 * WM * WN, LEAN ? (TAG ? 5 : 6) : 1) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
                                                                   const int2* __restrict__ tiles,
                                                                   const DevPlan* __restrict__ plans) {
-    syrk_tile_body<BT, WM, WN, TAG, EPI>(tasks, tiles, blockIdx.x, plans);
+    syrk_tile_body<BT, WM, WN, TAG, EPI, LEAN>(tasks, tiles, blockIdx.x, plans);
 }
 
 
@@ -1371,10 +1399,12 @@ hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hip
 }
 
 hipError_t launch_trsm_panel(const DevPlan& P, const TrsmTask* tasks, int count, hipStream_t st, bool partial,
-                             int32_t* arrive, bool pre) {
+                             int32_t* arrive, int pre) {
     if (count <= 0) return hipSuccess;
     if (partial)
         hipLaunchKernelGGL(trsm_partial_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks);
+    else if (pre == 2)
+        hipLaunchKernelGGL(trsm_panel_g_kernel<2>, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks, arrive);
     else if (pre)
         hipLaunchKernelGGL(trsm_panel_g_kernel<1>, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks, arrive);
     else
@@ -1387,22 +1417,24 @@ hipError_t launch_trsm_panel(const DevPlan& P, const TrsmTask* tasks, int count,
 // epi: epilogue with its C loads in flight together (see the kernel).
 template <int TAG, int EPI>
 static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int bt, hipStream_t st,
-                          const DevPlan* plans) {
-    if (bt == 128)
+                          const DevPlan* plans, bool lean) {
+    if (bt == 64 && lean)
+        hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG, EPI, 1>), dim3(n), dim3(256), 0, st, tasks, tiles, plans);
+    else if (bt == 128)
         hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, EPI>), dim3(n), dim3(512), 0, st, tasks, tiles, plans);
     else
         hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG, EPI>), dim3(n), dim3(256), 0, st, tasks, tiles, plans);
 }
 
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
-                       int epi, const DevPlan* plans) {
+                       int epi, const DevPlan* plans, bool lean) {
     if (total_tiles <= 0) return hipSuccess;
     if (tag)
-        epi ? launch_syrk_t<1, 1>(tasks, tiles, total_tiles, bt, st, plans)
-            : launch_syrk_t<1, 0>(tasks, tiles, total_tiles, bt, st, plans);
+        epi ? launch_syrk_t<1, 1>(tasks, tiles, total_tiles, bt, st, plans, lean)
+            : launch_syrk_t<1, 0>(tasks, tiles, total_tiles, bt, st, plans, lean);
     else
-        epi ? launch_syrk_t<0, 1>(tasks, tiles, total_tiles, bt, st, plans)
-            : launch_syrk_t<0, 0>(tasks, tiles, total_tiles, bt, st, plans);
+        epi ? launch_syrk_t<0, 1>(tasks, tiles, total_tiles, bt, st, plans, lean)
+            : launch_syrk_t<0, 0>(tasks, tiles, total_tiles, bt, st, plans, lean);
     return hipGetLastError();
 }
 

@@ -182,9 +182,10 @@ struct TrsmTask {
 };
 // partial: blocks with nb < 64; else full blocks with the POTRF fused (arrive: the
 // per-block arrival counters, zeroed)
-// pre: every task folds in the pending span-64 update from block k0 - 64 (TrsmTask::pre)
+// pre: 0 fused POTRF, 1 fused POTRF + the pending span-64 update (trsm_fold),
+// 2 the diagonal blocks already factored by their own launch (trsm_split_wg)
 hipError_t launch_trsm_panel(const DevPlan& P, const TrsmTask* tasks, int count, hipStream_t st, bool partial,
-                             int32_t* arrive, bool pre = false);
+                             int32_t* arrive, int pre = 0);
 // inv(L_jj) of factored 64 x 64 diagonal blocks (s, k0) into their strict upper
 // triangles (the tall TRSM's diagonal solves; the solve's block inverses are the same)
 hipError_t launch_panel_inv(const DevPlan& P, const int2* tasks, int count, hipStream_t st);
@@ -194,8 +195,9 @@ hipError_t launch_panel_tall(const DevPlan& P, const int4* tasks, int count, hip
 constexpr int TALL_ROWS = 64;  // rows per tall-TRSM workgroup
 
 // plans: the hosted ranks' DevPlans (CB tasks with gs >= 0 gather their children's entries)
+// lean: 64 x 64 tiles with half the LDS (BK = 8; short-K launches, syrk_lean_kmax)
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
-                       int epi = 0, const DevPlan* plans = nullptr);
+                       int epi = 0, const DevPlan* plans = nullptr, bool lean = false);
 hipError_t launch_stamp(uint64_t* slot, hipStream_t st);
 
 hipError_t launch_hwid(uint32_t* out, int nwg, int threads, int spin, hipStream_t st);

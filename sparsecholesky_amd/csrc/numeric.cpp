@@ -288,11 +288,11 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
             return launch_potrf_diag(N.R[L.vr].P, N.d_potrf + L.off, L.count, N.stream);
         case L_TRSM:
             return launch_trsm_panel(N.R[L.vr].P, N.d_trsm + L.off, L.count, N.stream, L.big != 0, N.d_arrive,
-                                     L.epi != 0);
+                                     L.epi);
         case L_PANEL:
         case L_CB:
             return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st, L.epi,
-                               N.d_plans);
+                               N.d_plans, L.lean != 0);
         case L_COMM:
             return comm_launch(N, L);
         case L_INV:

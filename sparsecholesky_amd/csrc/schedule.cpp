@@ -9,9 +9,12 @@
 
 namespace sc {
 
+// LDS edge of a small front's launch.  88: the widest front whose 4 x 4 tiles fit one
+// per thread (KT = 1, 124 VGPRs, 4 workgroups per CU; 96 needs KT = 2 at 2 per CU)
 static int bucket_of(int m) {
     if (m <= 32) return 32;
     if (m <= 64) return 64;
+    if (m <= 88) return 88;
     if (m <= 96) return 96;
     return 128;
 }
@@ -148,6 +151,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // K is short enough that the epilogue dominates a tile (CB of levels 4-7 at
         // 128^3); deep-K CB updates and the lookahead stream keep the trickle epilogue
         L.epi = (kind == L_PANEL && strm == 0) || (kind == L_CB && maxK < SC_EPI_KMAX);
+        L.lean = L.bt == SYRK_BT_SMALL && S.opt.syrk_lean_kmax > 0 && maxK <= S.opt.syrk_lean_kmax;
         L.toff = (int64_t)tiles.size();
         for (size_t q = 0; q < tasks.size(); ++q) {
             append_tiles(tiles, (int)q, tasks[q].M, tasks[q].N, L.bt);
@@ -158,6 +162,49 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         L.ntasks = (int32_t)tasks.size();
         L.big = big;
         L.flops = flops;
+        // Deep-K CB launch on 128-tiles: every tile takes about the same time and 512 run
+        // at once (two per CU), so a last partial round leaves most CUs idle for one whole
+        // tile time (~2 ms at K = 8192).  Its tiles -- the last ones dispatched -- are re-cut
+        // into 64 x 64 tiles in a launch of their own (up to 1024 at once, each ~1/4 of
+        // the work): the tail shrinks to about a third (cb_tail_split).
+        constexpr int64_t SLOTS = 512;
+        const int64_t rem = L.count % SLOTS;
+        if (kind == L_CB && L.bt == SYRK_BT_LARGE && S.opt.cb_tail_split && !L.epi && L.count > SLOTS && rem > 0 &&
+            rem * 4 <= SLOTS * 3) {
+            std::vector<int2> tail(tiles.end() - rem, tiles.end());
+            tiles.resize(tiles.size() - (size_t)rem);
+            L.count -= (int32_t)rem;
+            std::stable_sort(tail.begin(), tail.end(), [](const int2& a, const int2& b) { return a.x < b.x; });
+            Launch T = L;
+            T.bt = SYRK_BT_SMALL;
+            T.off = (int64_t)gemm.size();
+            T.toff = (int64_t)tiles.size();
+            gemm.insert(gemm.end(), tasks.begin(), tasks.end());
+            double tfl = 0.0;
+            for (const int2& t : tail) {
+                const GemmTask& g = tasks[t.x];
+                const int ti = t.y >> 16, tj = t.y & 0xffff;
+                for (int a = 0; a < 2; ++a)
+                    for (int b = 0; b < 2; ++b) {
+                        const int si = 2 * ti + a, sj = 2 * tj + b;
+                        if (si < sj || si * SYRK_BT_SMALL >= g.M || sj * SYRK_BT_SMALL >= g.N) continue;
+                        tiles.push_back(make_int2(t.x, (si << 16) | sj));
+                        // lower-triangle pairs of the sub-tile, 2 K flops each
+                        const int64_t i0 = (int64_t)si * SYRK_BT_SMALL, i1 = std::min<int64_t>(i0 + SYRK_BT_SMALL, g.M);
+                        const int64_t j0 = (int64_t)sj * SYRK_BT_SMALL, j1 = std::min<int64_t>(j0 + SYRK_BT_SMALL, g.N);
+                        int64_t pairs = 0;
+                        for (int64_t j = j0; j < j1; ++j) pairs += std::max<int64_t>(0, i1 - std::max(i0, j));
+                        tfl += 2.0 * g.K * (double)pairs;
+                    }
+            }
+            T.count = (int32_t)((int64_t)tiles.size() - T.toff);
+            xcd_order_tasks(tiles.data() + T.toff, T.count, tasks.data(), (int)tasks.size());
+            T.flops = tfl;
+            L.flops -= tfl;
+            N.sched.push_back(L);
+            N.sched.push_back(T);
+            return;
+        }
         N.sched.push_back(L);
     };
     // cross-stream dependencies: record an event on a stream / make a stream wait on it
@@ -324,7 +371,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 ++nsmall;
                 bmax = std::max(bmax, bucket_of(S.sn_m[s]));
             }
-        for (int b : {32, 64, 96, 128}) {
+        for (int b : {32, 64, 88, 96, 128}) {
             if (nsmall <= 256 && b != bmax) continue;
             Launch L {};
             L.kind = L_SMALL;
@@ -423,6 +470,19 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             std::vector<GemmTask> upd, outer_a, outer_b;
             std::vector<TrsmTask> trsm_part;  // partial last blocks: own launch (big = 1)
             std::vector<TrsmTask> trsm_pre;   // full blocks folding the pending update in (own launch)
+            std::vector<TrsmTask> trsm_split; // full blocks factored by the POTRF launch (own launch)
+            // a step whose fused launch would exceed trsm_split_wg workgroups (more than the GPU
+            // holds at once) factors each diagonal block once, in the POTRF launch, instead of
+            // in every workgroup of every round
+            int64_t step_wg = 0;
+            for (int32_t s : large) {
+                const int w = S.w(s);
+                if (w < k0 + PNB) continue;
+                const int slab1 = std::min(w, (k0 / NBO) * NBO + NBO);
+                const int rend = tall(s) ? slab1 : S.sn_m[s];
+                step_wg += (std::max(rend, k0 + PNB + 1) - (k0 + PNB) + TRSM_ROWS - 1) / TRSM_ROWS;
+            }
+            const bool split_step = S.opt.trsm_split_wg > 0 && step_wg > S.opt.trsm_split_wg;
             std::vector<int2> inv_t;           // tall mode, slab end: diagonal-block inverses
             std::vector<int4> tall_t;          // ... and the tall TRSM of the rows below
             double uflops = 0.0, afl = 0.0, bfl = 0.0;
@@ -437,6 +497,9 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 if (nb < PNB) {
                     potrf.push_back(make_int2(s, k0));
                     for (int r0 = k1; r0 < rend; r0 += TRSM_ROWS) trsm_part.push_back(TrsmTask {s, k0, r0, rend, 0});
+                } else if (split_step && !pre_next[s]) {
+                    potrf.push_back(make_int2(s, k0));
+                    for (int r0 = k1; r0 < rend; r0 += TRSM_ROWS) trsm_split.push_back(TrsmTask {s, k0, r0, rend, 0, 0});
                 } else {  // fused POTRF (one task if no rows below); ctr - 1: arrival counter
                     const int ctr = (int)(trsm.size() + trsm_pre.size()) + 1;
                     const int pre = pre_next[s];
@@ -482,6 +545,14 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 Lr.epi = 1;  // the folding kernel instance
                 trsm.insert(trsm.end(), trsm_pre.begin(), trsm_pre.end());
                 N.sched.push_back(Lr);
+            }
+            if (!trsm_split.empty()) {
+                Launch Ls = Lt;
+                Ls.off = (int64_t)trsm.size();
+                Ls.count = (int32_t)trsm_split.size();
+                Ls.epi = 2;  // the prefactored-block kernel instance
+                trsm.insert(trsm.end(), trsm_split.begin(), trsm_split.end());
+                N.sched.push_back(Ls);
             }
             if (!trsm_part.empty()) {
                 Launch Lq = Lt;

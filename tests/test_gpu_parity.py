@@ -147,6 +147,35 @@ def test_repeat_factorization_bitwise_deterministic(gpu):
     assert np.array_equal(L1.x, L2.x)
 
 
+@pytest.mark.parametrize("opts", [dict(trsm_split_wg=0), dict(syrk_lean_kmax=0), dict(cb_tail_split=0),
+                                  dict(trsm_split_wg=1)], ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
+def test_schedule_variants_bitwise_lap48(gpu, lap48_oracle, opts):
+    # the split POTRF launch, the lean short-K SYRK instance and the CB tail re-cut into
+    # 64 x 64 tiles change only where and when the same sums are formed, not their order:
+    # the factor is bitwise equal to the default schedule's (at 48^3 the CB launches of
+    # levels 10 and 11 have a partial last round of 128-tiles)
+    A = lap48_oracle[0]
+    facs = []
+    for o in ({}, opts):
+        num = sc.Numeric(sc.Symbolic(A, **o))
+        assert num.factor(A.x) == 0
+        facs.append(num.export()[1].x.copy())
+    assert np.array_equal(facs[0], facs[1])
+
+
+def test_split_potrf_bitwise_equal_fused(gpu):
+    # trsm_split_wg: the diagonal blocks factored once by their own launch give the same
+    # L11 bits as the fused kernel's per-workgroup factorization, so the whole factor is
+    # bitwise equal
+    A = sc.laplacian3d(20)
+    facs = []
+    for split in (0, 1):
+        num = sc.Numeric(sc.Symbolic(A, small_front_max=0, trsm_split_wg=split))
+        assert num.factor(A.x) == 0
+        facs.append(num.export()[1].x.copy())
+    assert np.array_equal(facs[0], facs[1])
+
+
 def test_graph_replay_matches_eager(gpu):
     A = sc.laplacian3d(16)
     a = sc.chol(A).value()
@@ -325,8 +354,9 @@ def lap48_oracle():
     return A, Lp, Li, Lx
 
 
-@pytest.mark.parametrize("opts", [{}, dict(asm_tile_min_m=1024), dict(cb_gather=0), dict(panel_tall=1)],
-                         ids=["default", "tiled_asm", "assembled_cb", "tall_trsm"])
+@pytest.mark.parametrize("opts", [{}, dict(asm_tile_min_m=1024), dict(cb_gather=0), dict(panel_tall=1),
+                                  dict(trsm_split_wg=1)],
+                         ids=["default", "tiled_asm", "assembled_cb", "tall_trsm", "split_potrf"])
 def test_lap48_full_parity(gpu, lap48_oracle, opts):
     # the whole 48^3 factor (n = 110592, F = 7.07e10: a 2304-wide root, CB SYRK with K
     # up to 1152 on 128 x 128 tiles) against the oracle, exact pattern and rel-Fro;
@@ -575,7 +605,8 @@ def test_dense_matrix_large_front(gpu):
 # recursive), lookahead (0 none, 1 trailing updates on a second stream), tiled assembly
 PANEL_OPTS = [dict(inner_order=0), dict(inner_order=0, lookahead=0), dict(lookahead=0), dict(asm_tile_min_m=1),
               dict(asm_tile_min_m=300), dict(panel_nb_outer=128, lookahead=0), dict(panel_tall=1),
-              dict(panel_tall=1, panel_nb_outer=128), dict(trsm_fold=1), dict(trsm_fold=1, panel_nb_outer=128)]
+              dict(panel_tall=1, panel_nb_outer=128), dict(trsm_fold=1), dict(trsm_fold=1, panel_nb_outer=128),
+              dict(trsm_split_wg=1), dict(trsm_split_wg=1, panel_nb_outer=128), dict(trsm_split_wg=1, panel_tall=1)]
 
 
 @pytest.mark.parametrize("opts", PANEL_OPTS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
