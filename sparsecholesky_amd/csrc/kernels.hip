@@ -415,6 +415,100 @@ __device__ __forceinline__ void small_steps(SmallRegs<KT>& R, double* colbuf, in
     }
 }
 
+#ifndef SC_POTRF_FAST
+#define SC_POTRF_FAST 1
+#endif
+// small_steps<1> restated for latency (the 64 x 64 diagonal blocks of the panel chain,
+// and the tiny tree): one tile per thread, and after each step's barrier every LDS read
+// of the step -- the 4 x 4 block D and this tile's 4 column rows and 4 row rows -- is in
+// flight at once, before the serial L_D factorization; the pivot checks are folded into
+// one report per step.  Same arithmetic in the same order as small_steps (bitwise equal).
+__device__ __forceinline__ void small_steps1_fast(SmallRegs<1>& R, double* colbuf, int w, int32_t* info, int c0) {
+    const int bi = R.bi[0], bj = R.bj[0];
+    for (int J = 0, b = 0; J < w; J += 4, ++b) {
+        double* cb = colbuf + (b & 1) * 4 * COLB;
+        const int nb = min(4, w - J);
+        if (bj == b) {  // publish tile column b
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                double* row = cb + 4 * (4 * bi + r);
+                *reinterpret_cast<double2*>(row) = make_double2(R.v[0][r * 4], R.v[0][r * 4 + 1]);
+                *reinterpret_cast<double2*>(row + 2) = make_double2(R.v[0][r * 4 + 2], R.v[0][r * 4 + 3]);
+            }
+        }
+        lds_barrier();
+        const bool act = bi >= 0 && bj >= b;
+        const int rj = act ? 4 * bj : J, ri = act ? 4 * bi : J;
+        double2 d01[4], d23[4], j01[4], j23[4], i01[4], i23[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            d01[r] = *reinterpret_cast<const double2*>(cb + 4 * (J + r));
+            d23[r] = *reinterpret_cast<const double2*>(cb + 4 * (J + r) + 2);
+            j01[r] = *reinterpret_cast<const double2*>(cb + 4 * (rj + r));
+            j23[r] = *reinterpret_cast<const double2*>(cb + 4 * (rj + r) + 2);
+            i01[r] = *reinterpret_cast<const double2*>(cb + 4 * (ri + r));
+            i23[r] = *reinterpret_cast<const double2*>(cb + 4 * (ri + r) + 2);
+        }
+        double D[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            D[r][0] = d01[r].x;
+            D[r][1] = d01[r].y;
+            D[r][2] = d23[r].x;
+            D[r][3] = d23[r].y;
+        }
+        double Ld[4][4], rc[4];
+        int bad = 4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            double dd = D[c][c];
+#pragma unroll
+            for (int t = 0; t < c; ++t) dd = fma(-Ld[c][t], Ld[c][t], dd);
+            if (c < nb && !(dd > 0.0)) bad = min(bad, c);
+            rc[c] = c < nb ? rsqrt_f64(dd) : 0.0;
+            Ld[c][c] = dd * rc[c];
+#pragma unroll
+            for (int r = c + 1; r < 4; ++r) {
+                double x = D[r][c];
+#pragma unroll
+                for (int t = 0; t < c; ++t) x = fma(-Ld[r][t], Ld[c][t], x);
+                Ld[r][c] = x * rc[c];
+            }
+        }
+        if (bad < 4 && threadIdx.x == 0) report_fail(info, c0 + J + bad);
+        if (!act) continue;
+        auto solve = [&](const double2& x01, const double2& x23, double (&l)[4]) {
+            const double cr[4] = {x01.x, x01.y, x23.x, x23.y};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                double x = cr[k];
+#pragma unroll
+                for (int t = 0; t < k; ++t) x = fma(-l[t], Ld[k][t], x);
+                l[k] = x * rc[k];
+            }
+        };
+        double lj[4][4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) solve(j01[c], j23[c], lj[c]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            double li[4];
+            solve(i01[r], i23[r], li);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                double x = R.v[0][r * 4 + c];
+                if (bj == b && c < nb) {
+                    x = li[c];
+                } else {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) x = fma(-li[t], lj[c][t], x);
+                }
+                R.v[0][r * 4 + c] = x;
+            }
+        }
+    }
+}
+
 // The panel (columns < w, rows >= the column) to HBM.
 template <int KT>
 __device__ __forceinline__ void small_store_panel(const SmallRegs<KT>& R, double* __restrict__ panel, int m, int w) {
@@ -449,32 +543,101 @@ __device__ __forceinline__ void small_store_cb(const SmallRegs<KT>& R, double* _
 }
 
 // Zero, A entries, children's CBs from HBM (children in child-list order; skip: a
-// child left out, the chain child of a chained front).
+// child left out, the chain child of a chained front).  Latency-bound (a few entries
+// per lane, several dependent global loads each), so every wave issues the loads of
+// SA_U of its columns before the LDS stores / adds, and the next child's metadata is
+// loaded while the current child is added.  SA_U = 4 where registers allow (the
+// register-tile kernels with KT = 1 stay at 4 waves per SIMD only with SA_U = 1).
+template <int SA_U = 4>
 __device__ __forceinline__ void small_assemble(const DevPlan& P, int s, int c0, int w, int m,
                                                const double* __restrict__ Ax, double* F, int skip = -1) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int tot = (m * (m + 1)) >> 1;
     for (int idx = tid; idx < tot; idx += 256) F[idx] = 0.0;
     lds_barrier();
-    for (int lc = wid; lc < w; lc += 4) {
-        const int64_t a0 = P.a_ptr[c0 + lc], a1 = P.a_ptr[c0 + lc + 1];
-        double* Fcol = F + pk_col(m, lc) - lc;
-        for (int64_t q = a0 + lane; q < a1; q += 64) Fcol[P.a_pos[q]] = Ax[P.a_src[q]];
+    for (int l0 = wid; l0 < w; l0 += 4 * SA_U) {  // A entries of the pivot columns
+        int64_t q[SA_U];
+        bool ok[SA_U];
+        int pos[SA_U];
+        int64_t src[SA_U];
+#pragma unroll
+        for (int u = 0; u < SA_U; ++u) {
+            const int lc = l0 + 4 * u;
+            const int64_t a0 = lc < w ? P.a_ptr[c0 + lc] : 0, a1 = lc < w ? P.a_ptr[c0 + lc + 1] : 0;
+            q[u] = a0 + lane;
+            ok[u] = q[u] < a1;
+        }
+#pragma unroll
+        for (int u = 0; u < SA_U; ++u) {
+            pos[u] = ok[u] ? P.a_pos[q[u]] : 0;
+            src[u] = ok[u] ? P.a_src[q[u]] : 0;
+        }
+        double v[SA_U];
+#pragma unroll
+        for (int u = 0; u < SA_U; ++u) v[u] = ok[u] ? Ax[src[u]] : 0.0;
+#pragma unroll
+        for (int u = 0; u < SA_U; ++u) {
+            const int lc = l0 + 4 * u;
+            if (ok[u]) F[pk_col(m, lc) - lc + pos[u]] = v[u];
+        }
+        // rare long columns (more than 64 entries): the rest one column at a time
+#pragma unroll 1
+        for (int u = 0; u < SA_U; ++u) {
+            const int lc = l0 + 4 * u;
+            if (lc >= w) break;
+            const int64_t a1 = P.a_ptr[c0 + lc + 1];
+            double* Fcol = F + pk_col(m, lc) - lc;
+            for (int64_t qq = P.a_ptr[c0 + lc] + 64 + lane; qq < a1; qq += 64) Fcol[P.a_pos[qq]] = Ax[P.a_src[qq]];
+        }
     }
     lds_barrier();
-    for (int ci = P.child_ptr[s]; ci < P.child_ptr[s + 1]; ++ci) {
-        const int c = P.child_list[ci];
-        if (c == skip) continue;
-        const int mbc = P.sn_m[c] - (P.sn_start[c + 1] - P.sn_start[c]);
-        const int32_t* __restrict__ rel = P.relind + P.rel_ptr[c];
-        const double* __restrict__ cb = P.cb_pool + P.cb_off[c];
-        for (int jc = wid; jc < mbc; jc += 4) {
-            const int pj = rel[jc];
-            double* Fcol = F + pk_col(m, pj) - pj;
-            const double* __restrict__ src = cb + (int64_t)jc * mbc;
-            for (int ic = jc + lane; ic < mbc; ic += 64) Fcol[rel[ic]] += src[ic];
+    const int cp0 = P.child_ptr[s], cp1 = P.child_ptr[s + 1];
+    auto meta = [&](int ci, int& c, int& mbc, const int32_t*& rel, const double*& cb) {
+        c = ci < cp1 ? P.child_list[ci] : -1;
+        if (c < 0) return;
+        mbc = P.sn_m[c] - (P.sn_start[c + 1] - P.sn_start[c]);
+        rel = P.relind + P.rel_ptr[c];
+        cb = P.cb_pool + P.cb_off[c];
+    };
+    int c = -1, mbc = 0;
+    const int32_t* rel = nullptr;
+    const double* cb = nullptr;
+    meta(cp0, c, mbc, rel, cb);
+    for (int ci = cp0; ci < cp1; ++ci) {
+        int cn = -1, mbn = 0;
+        const int32_t* reln = nullptr;
+        const double* cbn = nullptr;
+        meta(ci + 1, cn, mbn, reln, cbn);  // in flight under this child's adds
+        if (c != skip) {
+            for (int j0 = wid; j0 < mbc; j0 += 4 * SA_U) {
+                // SA_U columns jc = j0 + 4u of the child's CB, rows jc + lane (+ 64):
+                // parent column, parent rows and values, all loads in flight first
+                int pj[SA_U], r0[SA_U], r1[SA_U];
+                double v0[SA_U], v1[SA_U];
+#pragma unroll
+                for (int u = 0; u < SA_U; ++u) {
+                    const int jc = j0 + 4 * u;
+                    const int i0 = jc + lane, i1 = i0 + 64;
+                    pj[u] = jc < mbc ? rel[jc] : 0;
+                    const bool k0 = jc < mbc && i0 < mbc, k1 = jc < mbc && i1 < mbc;
+                    r0[u] = k0 ? rel[i0] : -1;
+                    r1[u] = k1 ? rel[i1] : -1;
+                    v0[u] = k0 ? cb[(int64_t)jc * mbc + i0] : 0.0;
+                    v1[u] = k1 ? cb[(int64_t)jc * mbc + i1] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < SA_U; ++u) {
+                    double* Fcol = F + pk_col(m, pj[u]) - pj[u];
+                    if (r0[u] >= 0) Fcol[r0[u]] += v0[u];
+                    if (r1[u] >= 0) Fcol[r1[u]] += v1[u];
+                }
+            }
+            lds_barrier();
         }
-        lds_barrier();
+        c = cn;
+        mbc = mbn;
+        rel = reln;
+        cb = cbn;
     }
 }
 
@@ -495,7 +658,7 @@ __global__ __launch_bounds__(256) void front_small_kernel(DevPlan P, const int32
         const int m = P.sn_m[s];
         SmallRegs<KT> R;
         small_tiles<KT>(R, m, w);
-        small_assemble(P, s, c0, w, m, Ax, F);
+        small_assemble<KT == 1 ? 1 : 4>(P, s, c0, w, m, Ax, F);
         small_load<KT>(R, F, m);
         small_steps<KT>(R, colbuf, w, P.info, c0);
         small_store_panel<KT>(R, P.panel_pool + P.panel_off[s], m, w);
@@ -543,7 +706,10 @@ __global__ __launch_bounds__(256) void tiny_tree_kernel(DevPlan P, TinyPlan T, c
         SmallRegs<1> R;
         small_tiles<1>(R, d.m, d.w);
         small_load<1>(R, Lm + d.img, d.m);
-        small_steps<1>(R, colbuf, d.w, info, d.c0);
+        if (SC_POTRF_FAST)
+            small_steps1_fast(R, colbuf, d.w, info, d.c0);
+        else
+            small_steps<1>(R, colbuf, d.w, info, d.c0);
         small_store_panel<1>(R, P.panel_pool + d.panel_off, d.m, d.w);
         if (d.m > d.w && R.bi[0] >= 0) {
             const int mb = d.m - d.w;
@@ -727,7 +893,10 @@ __global__ __launch_bounds__(256) void potrf_tiles_kernel(DevPlan P, const int2*
             const int i = 4 * R.bi[0] + r, j = 4 * R.bj[0] + c;
             R.v[0][r * 4 + c] = (R.bi[0] >= 0 && i < nb && i >= j) ? blk[(int64_t)j * m + i] : 0.0;
         }
-    small_steps<1>(R, colbuf, nb, P.info, c0 + k0);
+    if (SC_POTRF_FAST)
+        small_steps1_fast(R, colbuf, nb, P.info, c0 + k0);
+    else
+        small_steps<1>(R, colbuf, nb, P.info, c0 + k0);
     if (R.bi[0] < 0) return;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -873,7 +1042,10 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
             }
         }
     }
-    small_steps<1>(R, colbuf, PNB, P.info, c0 + k0);  // every block load has returned
+    if (SC_POTRF_FAST)  // every block load has returned
+        small_steps1_fast(R, colbuf, PNB, P.info, c0 + k0);
+    else
+        small_steps<1>(R, colbuf, PNB, P.info, c0 + k0);
     if (R.bi[0] >= 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)

@@ -151,7 +151,10 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // K is short enough that the epilogue dominates a tile (CB of levels 4-7 at
         // 128^3); deep-K CB updates and the lookahead stream keep the trickle epilogue
         L.epi = (kind == L_PANEL && strm == 0) || (kind == L_CB && maxK < SC_EPI_KMAX);
-        L.lean = L.bt == SYRK_BT_SMALL && S.opt.syrk_lean_kmax > 0 && maxK <= S.opt.syrk_lean_kmax;
+        // (CB launches with K <= 64 -- levels 4-6 at 128^3 -- are gather-bound and lose
+        // more to the lean instance's smaller gather batches than they gain in occupancy)
+        L.lean = L.bt == SYRK_BT_SMALL && S.opt.syrk_lean_kmax > 0 && maxK <= S.opt.syrk_lean_kmax &&
+                 (kind == L_PANEL || maxK > 64);
         L.toff = (int64_t)tiles.size();
         for (size_t q = 0; q < tasks.size(); ++q) {
             append_tiles(tiles, (int)q, tasks[q].M, tasks[q].N, L.bt);

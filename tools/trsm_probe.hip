@@ -2,6 +2,7 @@
 // variants on one m x 64 panel, 200 back-to-back launches each, us per launch.
 //   0 fused kernel (as shipped)     1 POTRF part only      2 row loads + stores only
 //   3 solve only (stream built from the block without factoring)
+//   4 POTRF part only, small_steps1_fast      5 fused kernel with small_steps1_fast
 #include "../sparsecholesky_amd/csrc/kernels.hip"
 
 #include <cstdio>
@@ -26,7 +27,10 @@ __global__ __launch_bounds__(TRSM_ROWS) void probe_kernel(double* pan, int m, in
                 const int i = 4 * R.bi[0] + r, j = 4 * R.bj[0] + c;
                 R.v[0][r * 4 + c] = (R.bi[0] >= 0 && i >= j) ? blk[(int64_t)j * m + i] : 0.0;
             }
-        if (V != 3) small_steps<1>(R, colbuf, PNB, info, 0);
+        if (V == 4 || V == 5)
+            small_steps1_fast(R, colbuf, PNB, info, 0);
+        else if (V != 3)
+            small_steps<1>(R, colbuf, PNB, info, 0);
         if (R.bi[0] >= 0) {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
@@ -37,7 +41,7 @@ __global__ __launch_bounds__(TRSM_ROWS) void probe_kernel(double* pan, int m, in
                 }
         }
     }
-    if (V == 1) {
+    if (V == 1 || V == 4) {
         if (R.bi[0] >= 0 && blockIdx.x == 0) pan[(int64_t)m * PNB + tid] = R.v[0][0] + Sd[tid];
         return;
     }
@@ -70,7 +74,7 @@ int main(int argc, char** argv) {
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     const int nwg = (m - 64 + sc::TRSM_ROWS - 1) / sc::TRSM_ROWS;
-    for (int v = 0; v < 4; ++v) {
+    for (int v = 0; v < 6; ++v) {
         for (int pass = 0; pass < 2; ++pass) {
             hipMemcpy(d, dref, h.size() * 8, hipMemcpyDeviceToDevice);
             hipEventRecord(e0, nullptr);
@@ -79,6 +83,8 @@ int main(int argc, char** argv) {
                 if (v == 1) hipLaunchKernelGGL(sc::probe_kernel<1>, dim3(nwg), dim3(256), 0, nullptr, d, m, info);
                 if (v == 2) hipLaunchKernelGGL(sc::probe_kernel<2>, dim3(nwg), dim3(256), 0, nullptr, d, m, info);
                 if (v == 3) hipLaunchKernelGGL(sc::probe_kernel<3>, dim3(nwg), dim3(256), 0, nullptr, d, m, info);
+                if (v == 4) hipLaunchKernelGGL(sc::probe_kernel<4>, dim3(nwg), dim3(256), 0, nullptr, d, m, info);
+                if (v == 5) hipLaunchKernelGGL(sc::probe_kernel<5>, dim3(nwg), dim3(256), 0, nullptr, d, m, info);
             }
             hipEventRecord(e1, nullptr);
             hipEventSynchronize(e1);
