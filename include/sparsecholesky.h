@@ -110,6 +110,9 @@ typedef struct sc_options {
                                 workgroups per CU instead of four); default 128, 0: never */
     int32_t cb_tail_split;   /* 1 (default): the last, partial round of a deep-K CB launch on 128 x 128 tiles
                                 runs as 64 x 64 tiles in a launch of its own (a shorter tail); 0: one launch */
+    int32_t tiny_dense;      /* 1 (default): on one device, a matrix with n <= 64 factors as one dense n x n
+                                lower triangle in a single wave (the symbolic pattern is exact: entries outside
+                                it come out as exact zeros and are not exported); 0: the tiny-tree launch */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

@@ -93,6 +93,7 @@ void sc_default_options(sc_options* opt) {
     opt->trsm_split_wg = 1024;
     opt->syrk_lean_kmax = 128;
     opt->cb_tail_split = 1;
+    opt->tiny_dense = 1;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,

@@ -738,6 +738,251 @@ hipError_t launch_tiny_tree(const DevPlan& P, const TinyPlan& T, int maxm, const
     return hipGetLastError();
 }
 
+// Tiny dense: a matrix with n <= 64 as one dense lower triangle, factored right-looking
+// by a single wave (no workgroup barriers: one wave's LDS operations complete in issue
+// order).  Lane i holds row i in registers; the matrix is padded to NP = n rounded up
+// to 16 with identity rows, so every loop is straight-line code.  Four pivots per step:
+// the rows publish their four step columns to LDS, every lane factors the 4 x 4 diagonal
+// block D redundantly, solves its own row of the step panel and publishes it, updates
+// the next step's four columns first, publishes them and factors the next D, and only
+// then applies the rest of the rank-4 update -- so the next step's serial chain (LDS
+// round trip, four pivots) overlaps this step's bulk FMAs.  Entries outside the
+// symbolic pattern come out as exact zeros (every product of the update has a
+// structurally zero factor) and are not stored: the panel entries of every supernode
+// are gathered from the dense image by a host-built list.  Status as tiny_tree_kernel.
+#ifndef SC_TD_LA
+#define SC_TD_LA 1  // 1: the next step's D factored under this step's bulk update
+#endif
+#ifndef SC_TD_PROBE
+#define SC_TD_PROBE 0  // timing probes (scripts/tiny_probe.py): 1 no factorization
+#endif
+// raw[4 * r .. 4 * r + 3] = step columns of row r (published) -> D and its factor
+__device__ __forceinline__ void td_factor_d(const double* raw, int J, double (&Ld)[4][4], double (&rc)[4], int& bad) {
+    double D[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const double2 x01 = *reinterpret_cast<const double2*>(raw + 4 * (J + r));
+        const double2 x23 = *reinterpret_cast<const double2*>(raw + 4 * (J + r) + 2);
+        D[r][0] = x01.x;
+        D[r][1] = x01.y;
+        D[r][2] = x23.x;
+        D[r][3] = x23.y;
+    }
+    bad = 4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        double dd = D[c][c];
+#pragma unroll
+        for (int t = 0; t < c; ++t) dd = fma(-Ld[c][t], Ld[c][t], dd);
+        if (!(dd > 0.0)) bad = min(bad, c);
+        rc[c] = rsqrt_f64(dd);
+        Ld[c][c] = dd * rc[c];
+#pragma unroll
+        for (int r = c + 1; r < 4; ++r) {
+            double x = D[r][c];
+#pragma unroll
+            for (int t = 0; t < c; ++t) x = fma(-Ld[r][t], Ld[c][t], x);
+            Ld[r][c] = x * rc[c];
+        }
+    }
+}
+
+// One four-pivot step of tiny_dense_kernel at compile-time column J (recursive over
+// the steps, so that every register index is a constant).
+template <int NP, int J>
+__device__ __forceinline__ void td_steps(double (&a)[NP], double (&Ld)[4][4], double (&rc)[4], int& bad, int& fail,
+                                         double* raw, double* lv, int i) {
+    if constexpr (J < NP) {
+        __builtin_amdgcn_sched_barrier(0);  // one step's live registers at a time
+        if (bad < 4) fail = min(fail, J + bad);
+        // this row's part of the step panel: l = a[J..J+3] L_D^-T
+        const bool below = i >= J + 4;
+        double l[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            double x = below ? a[J + k] : 0.0;
+#pragma unroll
+            for (int t = 0; t < k; ++t) x = fma(-l[t], Ld[k][t], x);
+            l[k] = x * rc[k];
+        }
+        *reinterpret_cast<double2*>(lv + 4 * i) = make_double2(l[0], l[1]);
+        *reinterpret_cast<double2*>(lv + 4 * i + 2) = make_double2(l[2], l[3]);
+        // the step's columns of this row become final: L_D rows (the diagonal block's
+        // rows) or l (below it); selects, not branches, so that a[] stays in registers
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            double v = below ? l[c] : a[J + c];
+#pragma unroll
+            for (int r = c; r < 4; ++r) v = i == J + r ? Ld[r][c] : v;
+            a[J + c] = v;
+        }
+        auto update = [&](int jj) {  // rank-4 update of column jj of this row
+            const double2 x01 = *reinterpret_cast<const double2*>(lv + 4 * jj);
+            const double2 x23 = *reinterpret_cast<const double2*>(lv + 4 * jj + 2);
+            double x = a[jj];
+            x = fma(-l[0], x01.x, x);
+            x = fma(-l[1], x01.y, x);
+            x = fma(-l[2], x23.x, x);
+            x = fma(-l[3], x23.y, x);
+            a[jj] = x;
+        };
+        if constexpr (J + 4 < NP && !SC_TD_LA) {  // no lookahead: the whole update, then the next D
+#pragma unroll
+            for (int jj = J + 4; jj < NP; ++jj) update(jj);
+            *reinterpret_cast<double2*>(raw + 4 * i) = make_double2(a[J + 4], a[J + 5]);
+            *reinterpret_cast<double2*>(raw + 4 * i + 2) = make_double2(a[J + 6], a[J + 7]);
+            td_factor_d(raw, J + 4, Ld, rc, bad);
+        }
+        if constexpr (J + 4 < NP && SC_TD_LA) {
+            // the next step's columns first, published, and its D loaded ...
+#pragma unroll
+            for (int jj = J + 4; jj < J + 8; ++jj) update(jj);
+            *reinterpret_cast<double2*>(raw + 4 * i) = make_double2(a[J + 4], a[J + 5]);
+            *reinterpret_cast<double2*>(raw + 4 * i + 2) = make_double2(a[J + 6], a[J + 7]);
+            double Dn[4][4], Ln[4][4], rn[4];
+            int bn = 4;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double2 x01 = *reinterpret_cast<const double2*>(raw + 4 * (J + 4 + r));
+                const double2 x23 = *reinterpret_cast<const double2*>(raw + 4 * (J + 4 + r) + 2);
+                Dn[r][0] = x01.x;
+                Dn[r][1] = x01.y;
+                Dn[r][2] = x23.x;
+                Dn[r][3] = x23.y;
+            }
+            auto pivot = [&](int c) {  // pivot c of the next D (td_factor_d, one column)
+                double dd = Dn[c][c];
+#pragma unroll
+                for (int t = 0; t < c; ++t) dd = fma(-Ln[c][t], Ln[c][t], dd);
+                if (!(dd > 0.0)) bn = min(bn, c);
+                rn[c] = rsqrt_f64(dd);
+                Ln[c][c] = dd * rn[c];
+#pragma unroll
+                for (int r = c + 1; r < 4; ++r) {
+                    double x = Dn[r][c];
+#pragma unroll
+                    for (int t = 0; t < c; ++t) x = fma(-Ln[r][t], Ln[c][t], x);
+                    Ln[r][c] = x * rn[c];
+                }
+            };
+            // ... and factored under the rest of this step's update, in groups of GW
+            // columns with one pivot of the next D per group (the scheduling barriers
+            // bound the registers the compiler's load hoisting takes; entries above the
+            // diagonal are computed too and never read)
+            constexpr int GW = NP > 48 ? 4 : 8;  // columns per group (registers: a[] is 2 NP VGPRs)
+            constexpr int NG = (NP - J - 8 + GW - 1) / GW;
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                if (g < 4) pivot(g);
+#pragma unroll
+                for (int u = 0; u < GW; ++u)
+                    if (J + 8 + GW * g + u < NP) update(J + 8 + GW * g + u);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int c = NG; c < 4; ++c) pivot(c);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                rc[r] = rn[r];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) Ld[r][c] = Ln[r][c];
+            }
+            bad = bn;
+        }
+        td_steps<NP, J + 4>(a, Ld, rc, bad, fail, raw, lv, i);
+    }
+}
+
+template <int NP>
+__global__ __launch_bounds__(64) void tiny_dense_kernel(DevPlan P, TinyPlan T, int n, const double* __restrict__ Ax) {
+    constexpr int LD = TINY_DENSE_LD, U = 8, UP = 8;
+    __shared__ double Dm[NP * LD];
+    __shared__ __attribute__((aligned(16))) double raw[NP * 4];
+    __shared__ __attribute__((aligned(16))) double lv[NP * 4];
+    __shared__ int2 prl[UP * 64];  // the first UP * 64 panel entries of the plan, staged at the start
+    const int i = threadIdx.x;
+    // the first U * 64 A entries and UP * 64 panel entries of the plan in flight while
+    // the image is zeroed (the panel entries wait in LDS for the end)
+    int2 ae[U], pe[UP];
+    double av[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int e = u * 64 + i;
+        ae[u] = e < T.na ? T.a[e] : make_int2(-1, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < UP; ++u) {
+        const int e = u * 64 + i;
+        pe[u] = e < T.npr ? T.pr[e] : make_int2(-1, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) av[u] = ae[u].x >= 0 ? Ax[ae[u].x] : 0.0;
+    for (int e = i; e < NP * LD; e += 64) Dm[e] = 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (ae[u].x >= 0) Dm[ae[u].y] = av[u];
+#pragma unroll
+    for (int u = 0; u < UP; ++u) prl[u * 64 + i] = pe[u];
+    for (int e = U * 64 + i; e < T.na; e += 64) {  // rare: more than U * 64 entries
+        const int2 q = T.a[e];
+        Dm[q.y] = Ax[q.x];
+    }
+    __syncthreads();
+    double a[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) a[j] = j <= i ? Dm[i * LD + j] : 0.0;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) a[j] = (i == j && i >= n) ? 1.0 : a[j];  // identity padding
+    int fail = n;
+    double Ld[4][4], rc[4];
+    int bad;
+    if (SC_TD_PROBE != 1) {
+        *reinterpret_cast<double2*>(raw + 4 * i) = make_double2(a[0], a[1]);
+        *reinterpret_cast<double2*>(raw + 4 * i + 2) = make_double2(a[2], a[3]);
+        td_factor_d(raw, 0, Ld, rc, bad);
+    }
+    if (SC_TD_PROBE != 1) td_steps<NP, 0>(a, Ld, rc, bad, fail, raw, lv, i);
+    if (fail > n) fail = n;  // padding pivots never fail; a failure at or past n is none
+#pragma unroll
+    for (int j = 0; j < NP; ++j)
+        if (j <= i && i < n) Dm[i * LD + j] = a[j];
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < UP; ++u) {
+        const int2 q = prl[u * 64 + i];
+        if (q.x >= 0) P.panel_pool[q.y] = Dm[q.x];
+    }
+    for (int e = UP * 64 + i; e < T.npr; e += 64) {  // the rest of the panel entries
+        const int2 q = T.pr[e];
+        P.panel_pool[q.y] = Dm[q.x];
+    }
+    __syncthreads();
+    if (i == 0) {
+        if (T.host_info) {  // the status word straight to the pinned host copy
+            const int32_t st = fail < n ? fail + 1 : 0x7f7f7f7f;
+            P.info[0] = st;
+            __hip_atomic_store(T.host_info, st, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else if (fail < n) {
+            report_fail(P.info, fail);
+        }
+    }
+}
+
+hipError_t launch_tiny_dense(const DevPlan& P, const TinyPlan& T, int n, const double* Ax, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    if (n > TINY_DENSE_N) return hipErrorInvalidValue;
+    if (n <= 16)
+        hipLaunchKernelGGL(tiny_dense_kernel<16>, dim3(1), dim3(64), 0, st, P, T, n, Ax);
+    else if (n <= 32)
+        hipLaunchKernelGGL(tiny_dense_kernel<32>, dim3(1), dim3(64), 0, st, P, T, n, Ax);
+    else if (n <= 48)
+        hipLaunchKernelGGL(tiny_dense_kernel<48>, dim3(1), dim3(64), 0, st, P, T, n, Ax);
+    else
+        hipLaunchKernelGGL(tiny_dense_kernel<64>, dim3(1), dim3(64), 0, st, P, T, n, Ax);
+    return hipGetLastError();
+}
+
 // Chain, part 1 (one workgroup per chained front, all in parallel): the packed image
 // of A entries and the children other than the chain child, to HBM.
 __global__ __launch_bounds__(256) void chain_init_kernel(DevPlan P, ChainPlan C, int first,

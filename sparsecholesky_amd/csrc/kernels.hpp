@@ -162,6 +162,13 @@ constexpr int TINY_MAX_FRONTS = 16;
 constexpr int TINY_MAX_LDS = 12288;  // doubles of images + CBs (96 KB)
 constexpr int TINY_PR_LDS = 2048;    // extend-add pairs staged in LDS with the A loads (the rest from HBM)
 hipError_t launch_tiny_tree(const DevPlan& P, const TinyPlan& T, int maxm, const double* Ax, hipStream_t st);
+// Tiny dense (n <= TINY_DENSE_N, one device): the whole matrix as one dense lower
+// triangle in one wave, lane i holding row i in registers, four pivots per step.  The
+// TinyPlan lists are reused: a = (Ax index, dense index r * TINY_DENSE_LD + c), pr =
+// (dense index, panel-pool offset) per stored panel entry; nf, ph unused.
+constexpr int TINY_DENSE_N = 64;
+constexpr int TINY_DENSE_LD = 65;  // padded row stride of the dense image in LDS
+hipError_t launch_tiny_dense(const DevPlan& P, const TinyPlan& T, int n, const double* Ax, hipStream_t st);
 
 hipError_t launch_front_chain(const DevPlan& P, const ChainPlan& C, int first, int count, int maxm,
                               const double* Ax, hipStream_t st);

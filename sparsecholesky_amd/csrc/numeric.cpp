@@ -247,7 +247,7 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
         // a tiny-tree handle is one launch: the kernel owns the status word (initial
         // value, failures, the copy to pinned host memory), so a factorization is one
         // dispatch with no reset / copy around it
-        if (N.sched.size() == 1 && N.sched[0].kind == L_SMALL && N.sched[0].big == 2) {
+        if (N.sched.size() == 1 && N.sched[0].kind == L_SMALL && N.sched[0].big >= 2) {
             void* dp = nullptr;
             if (hipHostGetDevicePointer(&dp, N.h_info, 0) != hipSuccess) {
                 N.err = "hipHostGetDevicePointer failed";
@@ -281,6 +281,7 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
         case L_SMALL:
             if (L.big == 1) return launch_front_chain(N.R[L.vr].P, N.CP, (int)L.off, L.count, L.maxm, d_Ax, N.stream);
             if (L.big == 2) return launch_tiny_tree(N.R[L.vr].P, N.TP, L.maxm, d_Ax, N.stream);
+            if (L.big == 3) return launch_tiny_dense(N.R[L.vr].P, N.TP, L.maxm, d_Ax, N.stream);
             return launch_front_small(N.R[L.vr].P, N.d_small + L.off, L.count, L.maxm, false, d_Ax, N.stream);
         case L_ASM:
             return launch_assemble_large(N.R[L.vr].P, N.d_asm + L.off, L.count, d_Ax, N.stream, L.big != 0);

@@ -827,7 +827,33 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
     // single device, a tiny tree (at most TINY_MAX_FRONTS fronts, all small with m <= 64,
     // every image and CB fitting LDS): the whole factorization as one single-workgroup
     // launch, postorder (the internal numbering), everything in LDS
-    bool tiny = !multi && S.ns > 1 && S.ns <= TINY_MAX_FRONTS;
+    // single device, n <= TINY_DENSE_N (and the tiny_dense option): the whole matrix as
+    // one dense lower triangle in one wave (kernels.hip tiny_dense_kernel); the plan is
+    // the A entries' dense positions and, per supernode panel entry, the dense position
+    // it is gathered from (internal numbering: the factor of the postordered matrix is
+    // the postordered factor, so the dense image is the multifrontal result)
+    const bool dense = !multi && S.opt.tiny_dense && S.n > 0 && S.n <= TINY_DENSE_N && S.nnzA_in <= INT32_MAX;
+    if (dense) {
+        for (int32_t s = 0; s < S.ns; ++s) {
+            const int m = S.sn_m[s], w = S.w(s), c0 = S.sn_start[s];
+            const int32_t* rows = S.rows.data() + S.rows_ptr[s];
+            for (int lc = 0; lc < w; ++lc)
+                for (int64_t q = S.a_ptr[c0 + lc]; q < S.a_ptr[c0 + lc + 1]; ++q)
+                    B.ta.push_back(make_int2((int32_t)S.a_src[q], rows[S.a_pos[q]] * TINY_DENSE_LD + c0 + lc));
+            const int64_t off = N.R[0].panel_off[s];
+            for (int j = 0; j < w; ++j)
+                for (int i = j; i < m; ++i)
+                    B.tpr.push_back(make_int2(rows[i] * TINY_DENSE_LD + c0 + j, (int32_t)(off + (int64_t)j * m + i)));
+        }
+        Launch L {};
+        L.kind = L_SMALL;
+        L.level = 0;
+        L.maxm = (int32_t)S.n;
+        L.big = 3;  // tiny dense
+        L.count = 1;
+        N.sched.push_back(L);
+    }
+    bool tiny = !dense && !multi && S.ns > 1 && S.ns <= TINY_MAX_FRONTS;
     {
         int64_t lds = 0;
         for (int32_t s = 0; tiny && s < S.ns; ++s) {
@@ -884,7 +910,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         L.count = 1;
         N.sched.push_back(L);
     }
-    for (int32_t lev = tiny ? S.nlevels : 0; lev < S.nlevels; ++lev) {
+    for (int32_t lev = (tiny || dense) ? S.nlevels : 0; lev < S.nlevels; ++lev) {
         if (chain_front(lev) && lev + 1 < S.nlevels && chain_front(lev + 1)) {
             Launch L {};
             L.kind = L_SMALL;

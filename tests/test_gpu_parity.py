@@ -72,6 +72,42 @@ def test_reference_matrices_no_relax(gpu, name, mtx):
     check_parity(mtx(name), relax=0)
 
 
+@pytest.mark.parametrize("tiny_dense", [0, 1])
+@pytest.mark.parametrize("case", ["bcsstk01", "readme5", "lap4", "lap4_nd", "random64", "random61_dups"])
+def test_tiny_paths(gpu, mtx, known, case, tiny_dense):
+    # n <= 64 on one device: the one-wave dense launch (tiny_dense=1, default) or the
+    # tiny-tree launch; both must give the oracle's pattern and values
+    if case == "bcsstk01":
+        A, kw = mtx("bcsstk01"), {}
+    elif case == "readme5":
+        g = known["readme5"]
+        A, kw = sc.triplet_to_csc_matrix(g["ti"], g["tj"], g["tx"], 5), {}
+    elif case in ("lap4", "lap4_nd"):
+        A, kw = sc.laplacian3d(4), ({"ordering": 1} if case == "lap4_nd" else {})
+    else:
+        n = 64 if case == "random64" else 61
+        rng = np.random.default_rng(7 + n)
+        M = rng.standard_normal((n, n)) * (rng.random((n, n)) < 0.08)
+        S = np.triu(M + M.T) + np.diag(np.full(n, 2.0 * n))
+        j, i = np.nonzero(S.T)  # upper entries, column-major
+        ti, tj, tx = list(i), list(j), list(S[i, j])
+        if case == "random61_dups":  # duplicates: the last one wins
+            ti += ti[:20]
+            tj += tj[:20]
+            tx += list(np.asarray(tx[:20]) * 0.5)
+        A, kw = sc.triplet_to_csc_matrix(ti, tj, tx, n), {}
+    if kw.get("ordering"):  # parity on the permuted input (as test_nd_ordering_factor_and_solve)
+        s = sc.Symbolic(A, tiny_dense=tiny_dense, **kw)
+        num = sc.Numeric(s)
+        assert num.factor(A.x) == 0
+        _, L = num.export()
+        st, Lp, Li, Lx = oracle.chol(sc.permute_symmetric(A, s.perm()))
+        assert st == 0 and np.array_equal(L.p, Lp) and np.array_equal(L.i, Li)
+        assert rel_fro(L.x, Lx) < TOL
+        return
+    check_parity(A, tiny_dense=tiny_dense, **kw)
+
+
 @pytest.mark.parametrize("k", [8, 16, 24])
 def test_laplacian_nd(gpu, k):
     check_parity(sc.laplacian3d(k))
@@ -116,12 +152,14 @@ def test_not_positive_definite_large_front(gpu):
     assert r.status > 0
 
 
-def test_not_positive_definite_tiny_tree(gpu, mtx):
-    # bcsstk01 runs as one tiny-tree launch that owns the status word (no reset / copy
-    # launches): a broken pivot must still be reported, with the oracle's column, and a
-    # refactorization with good values through the same handle must clear it
+@pytest.mark.parametrize("tiny_dense", [0, 1])
+def test_not_positive_definite_tiny_tree(gpu, mtx, tiny_dense):
+    # bcsstk01 runs as one launch (tiny dense, or the tiny tree) that owns the status
+    # word (no reset / copy launches): a broken pivot must still be reported, with the
+    # oracle's column, and a refactorization with good values through the same handle
+    # must clear it
     A = mtx("bcsstk01")
-    s = sc.Symbolic(A)
+    s = sc.Symbolic(A, tiny_dense=tiny_dense)
     num = sc.Numeric(s)
     assert num.factor(A.x) == 0
     for k in (40, 3):
