@@ -15,6 +15,9 @@ namespace sc {
 
 // CB launches with every K below this use the batched SYRK epilogue (measured per
 // level at 128^3: K <= 121 gains, K = 226 loses)
+#ifndef SC_LA_EPI
+#define SC_LA_EPI 0  // 1: lookahead-stream panel updates with the batched epilogue too
+#endif
 #ifndef SC_EPI_KMAX
 #define SC_EPI_KMAX 192
 #endif

@@ -150,7 +150,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // batched C epilogue on the critical path (main-stream panel updates) and where
         // K is short enough that the epilogue dominates a tile (CB of levels 4-7 at
         // 128^3); deep-K CB updates and the lookahead stream keep the trickle epilogue
-        L.epi = (kind == L_PANEL && strm == 0) || (kind == L_CB && maxK < SC_EPI_KMAX);
+        L.epi = (kind == L_PANEL && (strm == 0 || SC_LA_EPI)) || (kind == L_CB && maxK < SC_EPI_KMAX);
         // (CB launches with K <= 64 -- levels 4-6 at 128^3 -- are gather-bound and lose
         // more to the lean instance's smaller gather batches than they gain in occupancy)
         L.lean = L.bt == SYRK_BT_SMALL && S.opt.syrk_lean_kmax > 0 && maxK <= S.opt.syrk_lean_kmax &&
