@@ -17,6 +17,7 @@ import argparse
 import json
 import os
 import platform
+import re
 import sys
 import time
 
@@ -67,36 +68,75 @@ def cpu_baseline(k=32, reps=2):
     }
 
 
-def cb_syrk_traffic():
-    """HBM bytes per CB SYRK launch from the committed PMC profile
-    (scripts/gpu_pmc.sh: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE
-    doubled per the gfx950 note); None when the profile is absent."""
-    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r03", "pmc_summary.json")
+# The dominant kernel: the CB SYRK on 128 x 128 tiles with the trickle epilogue.  Its
+# kernel-trace name carries one template argument per kernel parameter, and their
+# number grew over the rounds (<128, 2, 4, 1>, <128, 2, 4, 1, 0>, <128, 2, 4, 1, 0, 0>):
+# the profile lookups match the instance on its leading arguments, whatever follows.
+DOMINANT_KERNEL = "syrk_mfma_kernel<128,2,4,1,0,0>"
+_DOMINANT_RE = re.compile(r"syrk_mfma_kernel<128, 2, 4, 1(, 0)*>")
+
+
+def _dominant_entry(table):
+    """The entry of a per-kernel table (kernel name -> stats) that is the dominant
+    kernel instance, or None."""
+    for name, v in table.items():
+        if _DOMINANT_RE.search(name):
+            return name, v
+    return None
+
+
+def _latest_profile(fname):
+    """The newest committed profiles/rNN/<fname> (rounds in descending order)."""
+    pdir = os.path.join(ROOT, "profiles")
+    try:
+        rounds = sorted((d for d in os.listdir(pdir) if re.fullmatch(r"r\d\d", d)), reverse=True)
+    except OSError:
+        return None
+    for d in rounds:
+        p = os.path.join(pdir, d, fname)
+        if os.path.exists(p):
+            return p
+    return None
+
+
+def cb_syrk_traffic(p=None):
+    """HBM bytes per dominant-kernel launch from the newest committed PMC profile (or
+    the summary `p`; scripts/gpu.sh pmc: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes,
+    FETCH_SIZE doubled per the gfx950 note); (None, None) when the profile is absent."""
+    p = p or _latest_profile("pmc_summary.json")
+    if p is None:
+        return None, None
     try:
         with open(p) as f:
-            cb = json.load(f)["cb_syrk_128"]
+            hit = _dominant_entry(json.load(f)["kernels"])
     except (OSError, KeyError, ValueError):
         return None, None
+    if hit is None:
+        return None, None
+    name, cb = hit
     b = cb["fetch_bytes_per_launch"] + cb["write_bytes_per_launch"]
-    return round(b), ("bytes per syrk_mfma_kernel<128,2,4,1> launch (FETCH_SIZE x2 + WRITE_SIZE), "
-                      "profiles/r03/pmc_summary.json; L2-miss bytes incl. Infinity-Cache hits")
+    rel = os.path.relpath(p, ROOT)
+    return round(b), (f"bytes per {DOMINANT_KERNEL} launch (FETCH_SIZE x2 + WRITE_SIZE), {rel} "
+                      f"[{name.split('(')[0]}]; L2-miss bytes incl. Infinity-Cache hits")
 
 
-def cb_syrk_mfma_counters():
-    """MFMA utilisation and clock of the CB SYRK from the committed counter pass
-    (scripts/gpu_mfma_util.sh: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024
-    SIMDs) on an eager bench step); None when the profile is absent."""
-    p = os.path.join(ROOT, "profiles", "r03", "mfma_util.json")
+def cb_syrk_mfma_counters(p=None):
+    """MFMA utilisation and clock of the dominant kernel from the newest committed
+    counter pass (or the summary `p`; scripts/gpu.sh mfma: SQ_VALU_MFMA_BUSY_CYCLES /
+    (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs) on an eager bench step); None when absent."""
+    p = p or _latest_profile("mfma_util.json")
+    if p is None:
+        return None
     try:
         with open(p) as f:
-            ks = json.load(f)["step_kernels"]
+            hit = _dominant_entry(json.load(f)["step_kernels"])
     except (OSError, KeyError, ValueError):
         return None
-    for name, v in ks.items():
-        if "syrk_mfma_kernel<128, 2, 4, 1>" in name or "syrk_mfma_kernel<128, 2, 4, 1, 0>" in name:
-            return {"mfma_busy_frac": v["raw_mfma_ratio"], "clock_GHz": v["clock_GHz"],
-                    "source": "profiles/r03/mfma_util.json (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE)"}
-    return None
+    if hit is None:
+        return None
+    _, v = hit
+    return {"mfma_busy_frac": v["raw_mfma_ratio"], "clock_GHz": v["clock_GHz"],
+            "source": f"{os.path.relpath(p, ROOT)} (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE)"}
 
 
 def backward_error(A, x, b):
@@ -240,10 +280,15 @@ def main():
     if ms > 0 and nl > 0:
         ach = fl / (ms * 1e-3) / 1e12
         traffic, tnote = cb_syrk_traffic()
+        alg = num.syrk_bytes(-2) / nl  # algorithmic bytes per launch of the same launches
         roof = {
             "bound": "mfma", "achieved": round(ach, 3), "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / FP64_MFMA_PEAK_TFLOPS, 4), "traffic": traffic, "traffic_note": tnote,
-            "kernel": "syrk_mfma_kernel<128,2,4,1,0> (CB update)" + (" on rank 0" if world > 1 else ""),
+            "algorithmic_bytes_per_launch": round(alg),
+            "traffic_ratio": round(traffic / alg, 3) if traffic and alg > 0 else None,
+            "traffic_ratio_note": "counter bytes / algorithmic bytes (operand rows once + C written once + "
+                                  "gathered children's CB entries once), per launch",
+            "kernel": f"{DOMINANT_KERNEL} (CB update)" + (" on rank 0" if world > 1 else ""),
             "flops_per_step": fl, "kernel_ms_per_step": round(ms, 3), "launches_per_step": nl,
             "avg_launch_ms": round(ms / nl, 3),
         }

@@ -227,6 +227,12 @@ int64_t sc_numeric_launch_trace(sc_numeric* num, int32_t* kind, int32_t* level, 
  * tiles (one kernel instance, comparable with a kernel trace). */
 int64_t sc_numeric_syrk_stats(sc_numeric* num, int32_t wmin, double* flops, double* ms,
                               int64_t* launches);
+/* Algorithmic HBM bytes of the same launch selection as sc_numeric_syrk_stats: the
+ * operand rows read once (8 M K per task), C written once (gathered CB) or read and
+ * written (assembled C), and every gathered child's CB entries read once.  A launch
+ * whose tail tiles are re-cut into a launch of their own splits its bytes in
+ * proportion to the flops. */
+int64_t sc_numeric_syrk_bytes(sc_numeric* num, int32_t wmin, double* bytes);
 /* Device memory of the handle, bytes: info[0] everything allocated (pools, plan,
  * staging, a gathered factor), info[1] panel arenas (L), info[2] work arenas (the
  * interval-planned contribution blocks), info[3] the work arenas' lower bound (the

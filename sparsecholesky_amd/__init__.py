@@ -121,6 +121,7 @@ _SIGS = [
     ("sc_numeric_level_times", _I64, [_P, _P, _I32]),
     ("sc_numeric_launch_trace", _I64, [_P, _P, _P, _P, _P, _P, _I64]),
     ("sc_numeric_syrk_stats", _I64, [_P, _I32, C.POINTER(_D), C.POINTER(_D), C.POINTER(_I64)]),
+    ("sc_numeric_syrk_bytes", _I64, [_P, _I32, C.POINTER(_D)]),
     ("sc_free_numeric", None, [_P]),
     ("sc_solve_host", _I64, [_P, _P, _P]),
     ("sc_solve_device", _I64, [_P, _P, _P]),
@@ -620,6 +621,13 @@ class Numeric:
         fl, ms, nl = C.c_double(), C.c_double(), C.c_int64()
         _check(lib().sc_numeric_syrk_stats(self.h, wmin, C.byref(fl), C.byref(ms), C.byref(nl)), "syrk_stats")
         return fl.value, ms.value, nl.value
+
+    def syrk_bytes(self, wmin: int = 256) -> float:
+        """Algorithmic HBM bytes of the launches syrk_stats(wmin) selects (C ABI
+        sc_numeric_syrk_bytes)."""
+        b = C.c_double()
+        _check(lib().sc_numeric_syrk_bytes(self.h, wmin, C.byref(b)), "syrk_bytes")
+        return b.value
 
     def memory(self) -> dict:
         """Device memory held, bytes: total, panel arenas, work arenas, work lower bound."""

@@ -325,6 +325,11 @@ int64_t sc_numeric_syrk_stats(sc_numeric* num, int32_t wmin, double* flops, doub
     return sc::numeric_syrk_stats(*num->N, wmin, flops, ms, launches);
 }
 
+int64_t sc_numeric_syrk_bytes(sc_numeric* num, int32_t wmin, double* bytes) {
+    if (!num || !num->N || !bytes) return SC_ERR_ARG;
+    return sc::numeric_syrk_bytes(*num->N, wmin, bytes);
+}
+
 int64_t sc_debug_chain_stamps(sc_numeric* num, int32_t enable, uint64_t* out, int64_t cap) {
     if (!num || !num->N) return SC_ERR_ARG;
     return sc::numeric_chain_stamps(*num->N, enable, out, cap);
@@ -587,7 +592,10 @@ int64_t sc_debug_bench(int32_t which, int32_t M, int32_t K, int32_t reps, int32_
 }
 
 int64_t sc_debug_hwid(int32_t nwg, int32_t threads, int32_t spin_ticks, uint32_t* out) {
-    if (!out || nwg <= 0 || threads <= 0 || threads > 1024) return SC_ERR_ARG;
+    // spin_ticks is compared unsigned in the kernel: a negative value would spin ~forever,
+    // and more than ~1 s (1e8 ticks of the 100 MHz clock) is never a placement probe
+    if (!out || nwg <= 0 || threads <= 0 || threads > 1024 || spin_ticks < 0 || spin_ticks > 100000000)
+        return SC_ERR_ARG;
     void* d = nullptr;
     if (hipMalloc(&d, (size_t)nwg * 8) != hipSuccess) return SC_ERR_DEVMEM;
     hipError_t e = sc::launch_hwid((uint32_t*)d, nwg, threads, spin_ticks, nullptr);

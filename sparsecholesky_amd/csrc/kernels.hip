@@ -753,6 +753,18 @@ hipError_t launch_tiny_tree(const DevPlan& P, const TinyPlan& T, int maxm, const
 #ifndef SC_TD_LA
 #define SC_TD_LA 1  // 1: the next step's D factored under this step's bulk update
 #endif
+#if defined(__AMDGCN_WAVEFRONT_SIZE) && __AMDGCN_WAVEFRONT_SIZE != 64
+#error "tiny_dense_kernel exchanges rows between the lanes of ONE 64-wide wave"
+#endif
+// Cross-lane LDS hand-over inside one wave: the lanes' stores must be ordered before the
+// other lanes' loads (and earlier loads before later stores).  The hardware keeps one
+// wave's LDS operations in issue order; the fence and the wave barrier keep the compiler
+// from moving the lane-indexed stores and the constant-indexed loads across each other
+// (they may alias).  Neither emits an instruction on gfx950.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
 #ifndef SC_TD_PROBE
 #define SC_TD_PROBE 0  // timing probes (scripts/tiny_probe.py): 1 no factorization
 #endif
@@ -805,8 +817,10 @@ __device__ __forceinline__ void td_steps(double (&a)[NP], double (&Ld)[4][4], do
             for (int t = 0; t < k; ++t) x = fma(-l[t], Ld[k][t], x);
             l[k] = x * rc[k];
         }
+        wave_lds_sync();  // the previous step's lv reads are done
         *reinterpret_cast<double2*>(lv + 4 * i) = make_double2(l[0], l[1]);
         *reinterpret_cast<double2*>(lv + 4 * i + 2) = make_double2(l[2], l[3]);
+        wave_lds_sync();  // every lane's l published before update() reads them
         // the step's columns of this row become final: L_D rows (the diagonal block's
         // rows) or l (below it); selects, not branches, so that a[] stays in registers
 #pragma unroll
@@ -829,16 +843,20 @@ __device__ __forceinline__ void td_steps(double (&a)[NP], double (&Ld)[4][4], do
         if constexpr (J + 4 < NP && !SC_TD_LA) {  // no lookahead: the whole update, then the next D
 #pragma unroll
             for (int jj = J + 4; jj < NP; ++jj) update(jj);
+            wave_lds_sync();
             *reinterpret_cast<double2*>(raw + 4 * i) = make_double2(a[J + 4], a[J + 5]);
             *reinterpret_cast<double2*>(raw + 4 * i + 2) = make_double2(a[J + 6], a[J + 7]);
+            wave_lds_sync();
             td_factor_d(raw, J + 4, Ld, rc, bad);
         }
         if constexpr (J + 4 < NP && SC_TD_LA) {
             // the next step's columns first, published, and its D loaded ...
 #pragma unroll
             for (int jj = J + 4; jj < J + 8; ++jj) update(jj);
+            wave_lds_sync();
             *reinterpret_cast<double2*>(raw + 4 * i) = make_double2(a[J + 4], a[J + 5]);
             *reinterpret_cast<double2*>(raw + 4 * i + 2) = make_double2(a[J + 6], a[J + 7]);
+            wave_lds_sync();
             double Dn[4][4], Ln[4][4], rn[4];
             int bn = 4;
 #pragma unroll
@@ -940,6 +958,7 @@ __global__ __launch_bounds__(64) void tiny_dense_kernel(DevPlan P, TinyPlan T, i
     if (SC_TD_PROBE != 1) {
         *reinterpret_cast<double2*>(raw + 4 * i) = make_double2(a[0], a[1]);
         *reinterpret_cast<double2*>(raw + 4 * i + 2) = make_double2(a[2], a[3]);
+        wave_lds_sync();
         td_factor_d(raw, 0, Ld, rc, bad);
     }
     if (SC_TD_PROBE != 1) td_steps<NP, 0>(a, Ld, rc, bad, fail, raw, lv, i);

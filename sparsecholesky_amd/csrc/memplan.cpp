@@ -3,8 +3,10 @@
 // The reference allocates each supernode's update block (UpdateBlock,
 // include/chol.hpp:1161-1169) for the duration of one supernode and scatters it
 // into the working matrix at once (apply_update, :1196-1216).  Here the
-// contribution block (CB) of a front lives from its assembly (level L) until its
-// parent's assembly (level Lp) reads it, and every region's lifetime is a closed
+// contribution block (CB) of a front lives from its assembly (level L) until the last
+// reader at its parent's level Lp -- the parent's assembly, or, when the parent's CB
+// SYRK gathers its children's entries itself (cb_gather, schedule.cpp), that CB SYRK
+// launch, the last launch of level Lp -- and every region's lifetime is a closed
 // interval of assembly-tree levels, fixed by the static schedule.  A sweep over
 // the levels places the regions in one work arena: regions dead before level t are
 // freed before those born at t are placed (best fit, largest first), so offsets
@@ -193,7 +195,10 @@ int64_t plan_rank_memory(const Symbolic& S, const DistPlan* D, int rank, RankMem
 }
 
 // Checks a plan: no two regions of one rank overlap in memory while both are live,
-// and every region lies inside the work arena.  Returns the number of violations.
+// every region lies inside the work arena, and every full-square CB held where its
+// parent runs stays live through the parent's level (its last reader there is the
+// parent's assembly or the parent's gathering CB SYRK, the level's last launch: a
+// region placed at level Lp must never overlap it).  Returns the number of violations.
 int64_t plan_check(const Symbolic& S, int nranks) {
     DistPlan D;
     if (nranks > 1 && dist_plan(S, nranks, D) != SC_OK) return -1;
@@ -202,6 +207,17 @@ int64_t plan_check(const Symbolic& S, int nranks) {
         RankMem R;
         std::vector<PlacedRegion> pl;
         plan_rank_memory(S, nranks > 1 ? &D : nullptr, r, R, &pl);
+        // (offset, birth level) names a region: two regions born at one level at one
+        // offset would overlap, which the sweep below counts anyway
+        std::map<std::pair<int64_t, int32_t>, int32_t> t1_of;
+        for (const PlacedRegion& q : pl) t1_of[{q.off, q.t0}] = q.t1;
+        for (i32 s = 0; s < S.ns; ++s) {
+            if (R.cb_off[s] < 0 || S.mb(s) <= 0) continue;
+            const i32 p = S.sn_parent[s];
+            if (nranks > 1 && D.owner[p] != r) continue;
+            auto it = t1_of.find({R.cb_off[s], S.level[s]});
+            if (it == t1_of.end() || it->second < S.level[p]) ++bad;
+        }
         int32_t tmax = 0;
         for (const PlacedRegion& q : pl) {
             tmax = std::max(tmax, q.t1);

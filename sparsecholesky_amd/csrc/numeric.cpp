@@ -489,20 +489,33 @@ int64_t numeric_timing(Numeric& N, double* t, int nt) {
     return SC_OK;
 }
 
+// CB SYRK launches are split by w >= 256; wmin selects them (0: all CB launches, -1:
+// the panel-update launches instead, -2: the CB launches on 128 x 128 tiles with the
+// trickle epilogue, i.e. exactly the syrk_mfma_kernel<128,2,4,1,0,0> dispatches a kernel
+// trace lists)
+static bool syrk_selected(const Launch& L, int wmin) {
+    if (L.kind != (wmin == -1 ? L_PANEL : L_CB)) return false;
+    if (wmin >= 256 && !L.big) return false;
+    if (wmin == -2 && (L.bt != SYRK_BT_LARGE || L.epi)) return false;
+    return true;
+}
+
+int64_t numeric_syrk_bytes(Numeric& N, int wmin, double* bytes) {
+    double b = 0.0;
+    for (const Launch& L : N.sched)
+        if (syrk_selected(L, wmin)) b += L.bytes;
+    *bytes = b;
+    return SC_OK;
+}
+
 int64_t numeric_syrk_stats(Numeric& N, int wmin, double* flops, double* ms, int64_t* launches) {
-    // CB SYRK launches are split by w >= 256; wmin selects them (0: all CB launches,
-    // -1: the panel-update launches instead, -2: the CB launches on 128 x 128 tiles with
-    // the trickle epilogue, i.e. exactly the syrk_mfma_kernel<128,2,4,1,0> dispatches a
-    // kernel trace lists)
     double fl = 0.0, t = 0.0;
     int64_t cnt = 0;
     bool have_t = N.status_valid && N.profile != 0;
     const std::vector<uint64_t> stamps = read_stamps(N);
     for (size_t i = 0; i < N.sched.size(); ++i) {
         const Launch& L = N.sched[i];
-        if (L.kind != (wmin == -1 ? L_PANEL : L_CB)) continue;
-        if (wmin >= 256 && !L.big) continue;
-        if (wmin == -2 && (L.bt != SYRK_BT_LARGE || L.epi)) continue;
+        if (!syrk_selected(L, wmin)) continue;
         fl += L.flops;
         ++cnt;
         if (have_t) {

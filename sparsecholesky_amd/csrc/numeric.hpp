@@ -158,6 +158,7 @@ struct Launch {
     int32_t strm;     // 0 = main stream, 1 = lookahead stream, 2 = comm stream
     int32_t vr;       // hosted rank whose DevPlan the kernel uses
     double flops;     // algorithmic SYRK flops (CB launches: mb*(mb+1)*w)
+    double bytes;     // algorithmic HBM bytes of a SYRK launch (numeric_syrk_bytes)
     // L_COMM: copy tiles [poff, poff + pcount) pack the sends, [uoff, uoff + ucount)
     // unpack the receives (Numeric::d_ctiles)
     int64_t poff, uoff;
@@ -288,6 +289,7 @@ int64_t numeric_level_times(Numeric& N, double* ms, int nl);
 int64_t numeric_launch_trace(Numeric& N, int32_t* kind, int32_t* level, int32_t* strm, double* ms, double* flops,
                              int64_t cap);
 int64_t numeric_syrk_stats(Numeric& N, int wmin, double* flops, double* ms, int64_t* launches);
+int64_t numeric_syrk_bytes(Numeric& N, int wmin, double* bytes);
 void numeric_free(Numeric* N);
 // x = A^{-1} b with the factor: device vectors of length n (may alias), on the
 // library stream, synchronous.  Multi-rank handles gather the factor first

@@ -130,6 +130,20 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         if (!region_addr(S, Dp, N.R[v], kind, s, row, col, arena, off, ld)) return nullptr;
         return (arena == 0 ? N.R[v].P.panel_pool : N.R[v].P.cb_pool) + off;
     };
+    // algorithmic HBM bytes of one SYRK task: its operand rows once, C written once when
+    // the children are gathered (plus every child's CB entries read once), else C read
+    // and written
+    auto task_bytes = [&](const GemmTask& t) {
+        const double pairs = (double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0;
+        double b = 8.0 * t.M * (double)t.K;
+        if (t.gs < 0) return b + 16.0 * pairs;
+        b += 8.0 * pairs;
+        for (int32_t ci = S.child_ptr[t.gs]; ci < S.child_ptr[t.gs + 1]; ++ci) {
+            const double mbc = S.mb(S.child_list[ci]);
+            b += 8.0 * mbc * (mbc + 1.0) / 2.0;
+        }
+        return b;
+    };
     auto push_gemm_launch = [&](int kind, int level, const std::vector<GemmTask>& tasks, int big,
                                 double flops, int strm = 0) {
         if (tasks.empty()) return;
@@ -156,9 +170,11 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         L.lean = L.bt == SYRK_BT_SMALL && S.opt.syrk_lean_kmax > 0 && maxK <= S.opt.syrk_lean_kmax &&
                  (kind == L_PANEL || maxK > 64);
         L.toff = (int64_t)tiles.size();
+        L.bytes = 0.0;
         for (size_t q = 0; q < tasks.size(); ++q) {
             append_tiles(tiles, (int)q, tasks[q].M, tasks[q].N, L.bt);
             gemm.push_back(tasks[q]);
+            L.bytes += task_bytes(tasks[q]);
         }
         L.count = (int32_t)((int64_t)tiles.size() - L.toff);
         xcd_order_tasks(tiles.data() + L.toff, L.count, tasks.data(), (int)tasks.size());
@@ -202,6 +218,8 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             }
             T.count = (int32_t)((int64_t)tiles.size() - T.toff);
             xcd_order_tasks(tiles.data() + T.toff, T.count, tasks.data(), (int)tasks.size());
+            T.bytes = L.flops > 0.0 ? L.bytes * tfl / L.flops : 0.0;
+            L.bytes -= T.bytes;
             T.flops = tfl;
             L.flops -= tfl;
             N.sched.push_back(L);
