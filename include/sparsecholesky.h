@@ -372,6 +372,14 @@ int64_t sc_debug_bench(int32_t which, int32_t M, int32_t K, int32_t reps, int32_
 /* Placement probe: nwg workgroups of `threads` threads, each spinning spin_ticks of the
  * 100 MHz clock; out[2 i] = HW_ID, out[2 i + 1] = XCC_ID of workgroup i. */
 int64_t sc_debug_hwid(int32_t nwg, int32_t threads, int32_t spin_ticks, uint32_t* out);
+/* Dispatch-contention probe: a panel-update SYRK "hog" (M x M triangle, K deep) on a
+ * low-priority stream against a chain of nchain fused POTRF + TRSM launches (chain_rows
+ * x 64 front) on the high-priority stream.  mode bit 0: hog stream CU-masked (every
+ * mask_stride-th CU off), bit 1: hog replayed from a hipGraph, bit 2: chain from a
+ * hipGraph.  out[8]: chain alone, hog alone, chain under hog, hog under chain, both
+ * (ms), CUs available to the hog. */
+int64_t sc_debug_contention(int32_t M, int32_t K, int32_t chain_rows, int32_t nchain, int32_t mode,
+                            int32_t mask_stride, double* out);
 int64_t sc_device_count(void);
 /* Message of the last failing call on this thread. */
 const char* sc_last_error(void);

@@ -154,6 +154,7 @@ _SIGS = [
     ("sc_debug_time_factor", _I64, [_P, C.c_void_p, _I32, C.POINTER(_D)]),
     ("sc_debug_solve_eager", _I64, [_P, _I32]),
     ("sc_debug_hwid", _I64, [_I32, _I32, _I32, _P]),
+    ("sc_debug_contention", _I64, [_I32, _I32, _I32, _I32, _I32, _I32, _P]),
 ]
 
 _lib: Optional[C.CDLL] = None

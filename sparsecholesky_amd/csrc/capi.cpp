@@ -591,6 +591,12 @@ int64_t sc_debug_bench(int32_t which, int32_t M, int32_t K, int32_t reps, int32_
     return sc::debug_bench(which, M, K, reps, arg, tflops);
 }
 
+int64_t sc_debug_contention(int32_t M, int32_t K, int32_t chain_rows, int32_t nchain, int32_t mode,
+                            int32_t mask_stride, double* out) {
+    if (!out) return SC_ERR_ARG;
+    return sc::debug_contention(M, K, chain_rows, nchain, mode, mask_stride, out);
+}
+
 int64_t sc_debug_hwid(int32_t nwg, int32_t threads, int32_t spin_ticks, uint32_t* out) {
     // spin_ticks is compared unsigned in the kernel: a negative value would spin ~forever,
     // and more than ~1 s (1e8 ticks of the 100 MHz clock) is never a placement probe

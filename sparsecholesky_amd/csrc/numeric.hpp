@@ -299,5 +299,6 @@ int64_t numeric_solve_host(Numeric& N, const double* b, double* x);
 int64_t debug_syrk(double* dC, int ldc, const double* dA, int lda, int M, int N, int K);
 int64_t numeric_chain_stamps(Numeric& N, int enable, uint64_t* out, int64_t cap);
 int64_t debug_bench(int which, int M, int K, int reps, int arg, double* tflops);
+int64_t debug_contention(int M, int K, int chain_rows, int nchain, int mode, int mask_stride, double* out);
 
 }  // namespace sc

@@ -469,6 +469,94 @@ def test_lap64_full_parity(gpu, lap64_oracle, opts):
     assert err < TOL
 
 
+def _root_slab_block(s, nranks):
+    """Slab ranks of the root's distributed panel and its slab block size (dist.cpp:
+    min(dist_slab_block, slabs // group) consecutive slabs per rank)."""
+    sn = s.supernodes()
+    root = int(np.argmax(sn["w"] * (sn["parent"] < 0)))
+    info = s.dist_plan_info(nranks)
+    g = int(info["gsize"][root])
+    nsl = -(-int(sn["w"][root]) // s.opt.panel_nb_outer)
+    return int(info["slab_ranks"][root]), max(1, min(s.opt.dist_slab_block, nsl // g)), info
+
+
+@pytest.mark.parametrize("nranks,rccl", [(2, False), (4, False), (8, False), (2, True), (4, True), (8, True)])
+def test_partitioned_defaults_lap64(gpu, lap64_oracle, nranks, rccl):
+    # VERDICT r3 item 1a: the distributed plan at its default options one size closer to
+    # the bench: at 64^3 the root (4127 wide, five 1024-column slabs) is dealt over up to
+    # 5 ranks (N = 8: 3 distributed fronts, 6 split fronts, 26 comm steps, 88 messages);
+    # at N = 2 the root goes in two-slab blocks.  Every rank emulated with private memory,
+    # messages as device copies or RCCL send / recv to self.
+    A, Lp, Li, Lx = lap64_oracle
+    s = sc.Symbolic(A)
+    assert s.opt.panel_nb_outer == 1024 and s.opt.dist_cbb == 1024 and s.opt.dist_slab_block == 2
+    slab_ranks, blk, info = _root_slab_block(s, nranks)
+    assert slab_ranks == min(nranks, 5)
+    if nranks == 2:
+        assert blk == 2  # two consecutive slabs per rank on the root
+    if nranks == 8:
+        assert (info["slab_ranks"] > 0).sum() == 3 and info["n_msgs"] == 88
+    v = sc.Numeric(s, nranks=nranks, virtual=True, rccl_self=rccl)
+    for _ in range(2):
+        assert v.factor(A.x) == 0
+    _, L = v.export()
+    assert np.array_equal(L.p, Lp) and np.array_equal(L.i, Li)
+    err = rel_fro(L.x, Lx)
+    print(f"lap64 defaults, {nranks} emulated ranks, rccl={rccl}: rel-Fro {err:.3e}, root slab ranks "
+          f"{slab_ranks} (block {blk}), {info['n_steps']} comm steps, {info['n_msgs']} messages")
+    assert err < TOL
+    b = np.random.default_rng(7).standard_normal(A.size())
+    x = v.solve(b)
+    be = _backward_error(A, x, b)
+    print(f"lap64 {nranks} ranks: solve backward error {be:.3e}")
+    assert be < 1e-14
+
+
+def test_partitioned_lap128_emulated8(gpu):
+    # VERDICT r3 item 1b: THE plan the 8-GPU bench runs (128^3, defaults: 7 distributed
+    # fronts, the 16447-wide root over all 8 ranks in two-slab blocks, 6 split fronts, 70
+    # comm steps, 345 messages), every rank emulated on this one GPU with private memory
+    # and every message moved as a device copy.  The whole factor is compared with the
+    # single-GPU factor (itself oracle-checked at 48^3 / 64^3 whole and on 128^3 closed
+    # blocks), column chunk by column chunk; plus the full-size solve backward error.
+    A = sc.laplacian3d(128)
+    n = A.size()
+    s = sc.Symbolic(A)
+    slab_ranks, blk, info = _root_slab_block(s, 8)
+    assert slab_ranks == 8 and blk == 2
+    assert (info["slab_ranks"] > 0).sum() == 7 and (info["split_cb_ranks"] > 0).sum() == 6
+    assert info["n_steps"] == 70 and info["n_msgs"] == 345
+    CH = 1 << 16
+    ref = []
+    one = sc.Numeric(s)
+    assert one.factor(A.x) == 0
+    for j0 in range(0, n, CH):
+        ref.append(one.export_cols(j0, min(n, j0 + CH))[2])
+    del one
+    v = sc.Numeric(s, nranks=8, virtual=True)
+    assert v.factor(A.x) == 0
+    d2 = r2 = 0.0
+    worst = 0.0
+    for q, j0 in enumerate(range(0, n, CH)):
+        cp, ri, rx = v.export_cols(j0, min(n, j0 + CH))
+        assert rx.shape == ref[q].shape
+        dd = float(np.sum((rx - ref[q]) ** 2))
+        rr = float(np.sum(ref[q] ** 2))
+        worst = max(worst, np.sqrt(dd / rr))
+        d2 += dd
+        r2 += rr
+        ref[q] = None
+    err = np.sqrt(d2 / r2)
+    print(f"lap128 8 emulated ranks vs single GPU: rel-Fro {err:.3e} (worst {CH}-column chunk {worst:.3e}); "
+          f"{info['n_steps']} comm steps, {info['n_msgs']} messages")
+    assert err < TOL and worst < TOL
+    b = np.random.default_rng(8).standard_normal(n)
+    x = v.solve(b)
+    be = _backward_error(A, x, b)
+    print(f"lap128 8 emulated ranks: solve backward error {be:.3e}")
+    assert be < 1e-14
+
+
 def test_solve_after_failed_factor(gpu):
     A = sc.laplacian3d(6)
     A.x[A.p[5]:A.p[6]][-1] = -10.0  # diagonal of column 5 (last entry of an upper column)
