@@ -203,11 +203,21 @@ __global__ __launch_bounds__(256) void assemble_tile_kernel(DevPlan P, const int
                     if (rr[q][ch] >= 0) T[tc[q] * ASM_ROWS + rr[q][ch] - r0] += v[q][ch];
         }
     }
-    // own columns: store the lower part once
+    // own columns: store the lower part once.  A front of the tall-TRSM-by-inverse mode
+    // (tall_off >= 0) sends the rows below its first slab's diagonal block, in that
+    // slab's columns, to its staging buffer (ld m - tnb, row tnb first): the tall solve
+    // reads them from there and writes the final L21 into the panel.
+    const int64_t toff = P.tall_off ? P.tall_off[s] : -1;
+    const int tnb = toff >= 0 ? min(w, P.tall_nbo) : 0;
     for (int j = j0 + wid; j < j1; j += 4) {
         double* col = (j < w) ? panel + (int64_t)j * m : cbs + (int64_t)(j - w) * mb - w;
         const double* Tc = T + (j - j0) * ASM_ROWS - r0;
-        for (int r = max(r0, j) + lane; r < r1; r += 64) col[r] = Tc[r];
+        if (j < tnb) {
+            double* tcol = P.tall_pool + toff + (int64_t)j * (m - tnb) - tnb;
+            for (int r = max(r0, j) + lane; r < r1; r += 64) (r < tnb ? col : tcol)[r] = Tc[r];
+        } else {
+            for (int r = max(r0, j) + lane; r < r1; r += 64) col[r] = Tc[r];
+        }
     }
 }
 
@@ -1514,9 +1524,12 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const De
 // each, +128 B row pad: the two k-rows read by a half-wave hit disjoint banks).
 // AGLC: the row0 operand is loaded with glc (L1 bypassed: rows this workgroup
 // itself stored earlier in the same launch).
-template <int BT, int WM, int WN, int AGLC = 0, int BK = 16>
+// SEPB: the col0 operand comes from its own matrix Bm (ld ldb) instead of A (general
+// products, gemm_tile_body); SEPB = 0 compiles to exactly the single-operand loop.
+template <int BT, int WM, int WN, int AGLC = 0, int BK = 16, int SEPB = 0>
 __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t lda, int K, int M, int N, int row0,
-                                           int col0, double4_t (&acc)[BT / WM / 16][BT / WN / 16], double* smem) {
+                                           int col0, double4_t (&acc)[BT / WM / 16][BT / WN / 16], double* smem,
+                                           const double* __restrict__ Bm = nullptr, int64_t ldb = 0) {
     static_assert(BK == 16 || BK == 8, "four-deep k sub-steps of the MFMA");
     constexpr int NT = 64 * WM * WN;
     constexpr int LDT = BT + 16;
@@ -1536,6 +1549,9 @@ __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t
     double ra[PER], rb[PER];
     auto gload = [&](int k0) {
         const __amdgpu_buffer_rsrc_t rs = buf_rsrc(A + (int64_t)k0 * lda, (uint32_t)(min(BK, K - k0) * lda * 8));
+        __amdgpu_buffer_rsrc_t rsb = rs;
+        if constexpr (SEPB) rsb = buf_rsrc(Bm + (int64_t)k0 * ldb, (uint32_t)(min(BK, K - k0) * ldb * 8));
+        const int64_t ldbb = SEPB ? ldb : lda;
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
             const int e = tid + q * NT;
@@ -1546,7 +1562,7 @@ __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t
                 ra[q] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, va, 0, 1));
             else
                 ra[q] = buf_ld(rs, va, 0);
-            rb[q] = buf_ld(rs, gc < N ? (int)((gc + kk * lda) * 8) : BUF_DEAD, 0);
+            rb[q] = buf_ld(rsb, gc < N ? (int)((gc + kk * ldbb) * 8) : BUF_DEAD, 0);
         }
     };
     auto sstore = [&](int buf) {
@@ -1686,6 +1702,133 @@ __global__ __launch_bounds__(64 * WM * WN, LEAN ? (TAG ? 5 : 6) : 1) void syrk_m
                                                                   const int2* __restrict__ tiles,
                                                                   const DevPlan* __restrict__ plans) {
     syrk_tile_body<BT, WM, WN, TAG, EPI, LEAN>(tasks, tiles, blockIdx.x, plans);
+}
+
+// General products of the tall-TRSM-by-inverse panel mode (GemmTask, TAG 2):
+//   the tall solve    L21 = A21 X^T       (A21 staged out of place; X = inv(L11), ktri)
+//   the next slab's   C_out = C_in - L L^T (rows below its diagonal block to the staging
+//   outer update                          buffer the next tall solve reads)
+//   the inverse's     U^T = (B Xa)^T, then E = -Xb U (stored as E and E^T)
+//   doubling steps
+// Same K loop as the SYRK (B from its own matrix); the epilogue reads Cin (if any) for a
+// whole two-MFMA-row chunk before its stores (Cin never aliases C or Ct here).
+template <int BT, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_mfma_kernel(const GemmTask* __restrict__ tasks,
+                                                                  const int2* __restrict__ tiles) {
+    constexpr int BK = 16, LDT = BT + 16;
+    constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
+    __shared__ double smem[2 * 2 * BK * LDT];
+    const int2 tl = tiles[blockIdx.x];
+    const GemmTask T = tasks[tl.x];
+    const int ti = tl.y >> 16, tj = tl.y & 0xffff;
+    const int row0 = ti * BT, col0 = tj * BT;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wr = wid / WN, wc = wid % WN;
+    if (wid >= WM * WN / 2) __builtin_amdgcn_s_setprio(1);
+    double4_t acc[RTM][RTN];
+#pragma unroll
+    for (int a = 0; a < RTM; ++a)
+#pragma unroll
+        for (int b = 0; b < RTN; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
+    const int K = T.ktri ? min(T.K, col0 + BT) : T.K;
+    if (K > 0) mfma_kloop<BT, WM, WN, 0, BK, 1>(T.A, T.lda, K, T.M, T.N, row0, col0, acc, smem, T.B, T.ldb);
+    const double* __restrict__ Cin = T.Cin;
+    double* __restrict__ C = T.C;
+    double* __restrict__ Ct = T.Ct;
+    const double sg = T.sign;
+    constexpr int EA = RTM < 2 ? RTM : 2;  // MFMA tile rows per epilogue chunk
+#pragma unroll
+    for (int a0 = 0; a0 < RTM; a0 += EA) {
+        double v[EA][RTN][4];
+#pragma unroll
+        for (int a = 0; a < EA; ++a)
+#pragma unroll
+            for (int b = 0; b < RTN; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int gi = row0 + wr * (BT / WM) + (a0 + a) * 16 + MFMA_F64_ROW(lane, r);
+                    const int gj = col0 + wc * (BT / WN) + b * 16 + (lane & 15);
+                    const bool live = gi < T.M && gj < T.N && (!T.lower || gi >= gj);
+                    v[a][b][r] = (Cin && live) ? Cin[gi + (int64_t)gj * T.ldin] : 0.0;
+                }
+#pragma unroll
+        for (int a = 0; a < EA; ++a)
+#pragma unroll
+            for (int b = 0; b < RTN; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int gi = row0 + wr * (BT / WM) + (a0 + a) * 16 + MFMA_F64_ROW(lane, r);
+                    const int gj = col0 + wc * (BT / WN) + b * 16 + (lane & 15);
+                    const bool live = gi < T.M && gj < T.N && (!T.lower || gi >= gj);
+                    if (!live) continue;
+                    const double x = fma(sg, acc[a0 + a][b][r], v[a][b][r]);
+                    if (C) C[gi + (int64_t)gj * T.ldc] = x;
+                    if (Ct) Ct[gj + (int64_t)gi * T.ldt] = x;
+                }
+    }
+}
+
+// 64-block inverses of a slab's factored diagonal block into the dense scratch X (and
+// XT = X^T) of the tall-TRSM-by-inverse mode: one wave per 64-column block q, lane j
+// solving e_j L_qq^-T (the generated TRSM code, as solve_inv_kernel) -- column j of
+// inv(L_qq).  The rest of block column q of X (rows above the block; the doubling steps
+// fill the rows below) and block row q of XT are zeroed, so the dense X is exact.
+__global__ __launch_bounds__(64) void xinv64_kernel(DevPlan P, const XinvTask* __restrict__ tasks) {
+    __shared__ double2 S[TRSM64_STREAM / 2];
+    __shared__ double Lc[PNB * (PNB + 2)];
+    __shared__ double invd[PNB];
+    const XinvTask t = tasks[blockIdx.x];
+    const int lane = threadIdx.x;
+    const int m = P.sn_m[t.s];
+    const int k0 = t.c0 + PNB * t.q;               // front column of the block
+    const int nb = min(PNB, t.nbs - PNB * t.q);    // > 0
+    const double* blk = P.panel_pool + P.panel_off[t.s] + (int64_t)k0 * m + k0;
+    double r[PNB];
+#pragma unroll
+    for (int j = 0; j < PNB; ++j) r[j] = (j < nb && lane < nb && lane >= j) ? blk[(int64_t)j * m + lane] : 0.0;
+    if (nb == PNB) {
+        double* Sd = reinterpret_cast<double*>(S);
+#pragma unroll
+        for (int j = 0; j < PNB; ++j)
+            if (lane >= j) Sd[PNB * j - j * (j - 1) / 2 + (lane - j)] = lane == j ? 1.0 / r[j] : r[j];
+    } else {
+        constexpr int LD = PNB + 2;
+#pragma unroll
+        for (int j = 0; j < PNB; ++j) {
+            Lc[j * LD + lane] = r[j];
+            if (lane == j) invd[j] = j < nb ? 1.0 / r[j] : 0.0;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < PNB; ++c) r[c] = c == lane ? 1.0 : 0.0;
+    if (nb == PNB)
+        trsm64_full(r, S);
+    else
+        trsm_steps<0>(r, Lc, invd, nb);
+    // r[c] = inv(L_qq)(c, lane) = X(b0 + c, b0 + lane) = XT(b0 + lane, b0 + c)
+    const int b0 = PNB * t.q;
+#pragma unroll
+    for (int c = 0; c < PNB; ++c)
+        if (c < nb && lane < nb) {
+            const double x = c >= lane ? r[c] : 0.0;
+            t.X[b0 + c + (int64_t)(b0 + lane) * t.ldx] = x;
+            t.XT[b0 + lane + (int64_t)(b0 + c) * t.ldx] = x;  // coalesced across lanes
+        }
+    // zeros, lanes along rows (coalesced): X above the block in its block column (X is
+    // lower triangular) and XT below the block in its block column (XT upper)
+    for (int c = 0; c < nb; ++c) {
+        double* xc = t.X + (int64_t)(b0 + c) * t.ldx;
+        for (int i = lane; i < b0; i += 64) xc[i] = 0.0;
+        double* tc = t.XT + (int64_t)(b0 + c) * t.ldx;
+        for (int i = b0 + PNB + lane; i < t.nbs; i += 64) tc[i] = 0.0;
+    }
+}
+
+hipError_t launch_xinv64(const DevPlan& P, const XinvTask* tasks, int count, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(xinv64_kernel, dim3(count), dim3(64), 0, st, P, tasks);
+    return hipGetLastError();
 }
 
 
@@ -1865,6 +2008,13 @@ static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int b
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
                        int epi, const DevPlan* plans, bool lean) {
     if (total_tiles <= 0) return hipSuccess;
+    if (tag == 2) {
+        if (bt == 128)
+            hipLaunchKernelGGL((gemm_mfma_kernel<128, 2, 4>), dim3(total_tiles), dim3(512), 0, st, tasks, tiles);
+        else
+            hipLaunchKernelGGL((gemm_mfma_kernel<64, 2, 2>), dim3(total_tiles), dim3(256), 0, st, tasks, tiles);
+        return hipGetLastError();
+    }
     if (tag)
         epi ? launch_syrk_t<1, 1>(tasks, tiles, total_tiles, bt, st, plans, lean)
             : launch_syrk_t<1, 0>(tasks, tiles, total_tiles, bt, st, plans, lean);

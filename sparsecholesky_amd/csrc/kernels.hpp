@@ -51,6 +51,12 @@ struct DevPlan {
     double* panel_pool;
     double* cb_pool;
     int32_t* info;              // min failing internal column + 1
+    // tall-TRSM-by-inverse mode (panel_tall = 2): per supernode the staging buffer of its
+    // slabs' rows below the diagonal block in tall_pool (doubles, -1 = not in the mode);
+    // the first slab (tall_nbo columns) is assembled straight into it
+    const int64_t* tall_off;
+    double* tall_pool;
+    int32_t tall_nbo;
 };
 
 // One lower-trapezoid SYRK update: C[i,j] -= sum_k A[i,k] A[j,k], j < N, j <= i < M.
@@ -65,7 +71,33 @@ struct GemmTask {
     int64_t lda;
     int32_t M, N, K;
     int32_t gs = -1, gv = 0;
+    // General products (the TAG 2 launches of the tall-TRSM-by-inverse panel mode,
+    // gemm_tile_body): acc(i, j) = sum_{k < K} A(i, k) B(j, k), A and B column-major
+    // (element (r, k) at base[r + k ld]); out(i, j) = Cin(i, j) + sign acc(i, j) (no Cin:
+    // sign acc), stored at C(i, j) (ld ldc) and / or transposed at Ct(j, i) (ld ldt).
+    // lower: only j <= i (lower-trapezoid tiles), else the full M x N rectangle.  ktri: B
+    // is lower triangular in (j, k) (zero for k > j), so output column block j0 stops at
+    // K = j0 + tile.
+    const double* B = nullptr;
+    int64_t ldb = 0;
+    const double* Cin = nullptr;
+    int64_t ldin = 0;
+    double* Ct = nullptr;
+    int64_t ldt = 0;
+    double sign = -1.0;
+    int32_t lower = 0, ktri = 0;
 };
+// Inverse X = inv(L11) of a slab's factored diagonal block (the tall-TRSM-by-inverse
+// panel mode): 64-block inverses of columns [c0 + 64 q, ...) of front s into the dense
+// scratch X (and its transpose XT), ld ldx, with every other block of their block
+// column zeroed; nbs = the slab width.
+struct XinvTask {
+    double* X;
+    double* XT;
+    int64_t ldx;
+    int32_t s, c0, q, nbs;
+};
+hipError_t launch_xinv64(const DevPlan& P, const XinvTask* tasks, int count, hipStream_t st);
 
 // Strided <-> packed copy of a rows x cols block (pack: a -> b; unpack: b -> a).
 struct Copy2D {
@@ -203,8 +235,11 @@ constexpr int TALL_ROWS = 64;  // rows per tall-TRSM workgroup
 
 // plans: the hosted ranks' DevPlans (CB tasks with gs >= 0 gather their children's entries)
 // lean: 64 x 64 tiles with half the LDS (BK = 8; short-K launches, syrk_lean_kmax)
+// tag 2: general products (GemmTask B / Cin / Ct / sign / lower / ktri)
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
                        int epi = 0, const DevPlan* plans = nullptr, bool lean = false);
+// full rectangle tiles (general products that are not lower trapezoids)
+void append_tiles_full(std::vector<int2>& out, int task, int M, int N, int bt, int G = 8);
 hipError_t launch_stamp(uint64_t* slot, hipStream_t st);
 
 hipError_t launch_hwid(uint32_t* out, int nwg, int threads, int spin, hipStream_t st);

@@ -190,6 +190,21 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
         R.P.cb_off = dp;
     }
     if (!multi || N.emulated) N.gpanel = pbase;  // gathered layout == the arenas
+    {  // tall-TRSM-by-inverse scratch (panel_tall = 2): levels run one after another, so
+       // every hosted rank's fronts of a level share one pool from offset 0
+        int64_t tneed = 0;
+        for (RankMem& R : N.R) tneed = std::max(tneed, plan_tall_scratch(S, multi ? &N.D : nullptr, R.rank, R.tall_off));
+        if (tneed > 0) {
+            if ((rc = dalloc(N, (size_t)tneed * sizeof(double), p))) return fail(rc);
+            for (RankMem& R : N.R) {
+                int64_t* dp = nullptr;
+                if ((rc = upload(N, R.tall_off, dp))) return fail(rc);
+                R.P.tall_off = dp;
+                R.P.tall_pool = (double*)p;
+                R.P.tall_nbo = std::max(PNB, (S.opt.panel_nb_outer / PNB) * PNB);
+            }
+        }
+    }
     {
         std::vector<DevPlan> plans;
         for (const RankMem& R : N.R) plans.push_back(R.P);
@@ -258,7 +273,7 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     }
     if ((rc = upload(N, B.small, N.d_small)) || (rc = upload(N, B.asmv, N.d_asm)) ||
         (rc = upload(N, B.potrf, N.d_potrf)) || (rc = upload(N, B.trsm, N.d_trsm)) ||
-        (rc = upload(N, B.inv, N.d_inv)) || (rc = upload(N, B.tall, N.d_tall)) ||
+        (rc = upload(N, B.inv, N.d_inv)) || (rc = upload(N, B.tall, N.d_tall)) || (rc = upload(N, B.xinv, N.d_xinv)) ||
         (rc = upload(N, std::vector<int32_t>(B.trsm.size() + 1, 0), N.d_arrive)) ||
         (rc = upload(N, B.gemm, N.d_gemm)) || (rc = upload(N, B.tiles, N.d_tiles)))
         return fail(rc);
@@ -300,6 +315,10 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
             return launch_panel_inv(N.R[L.vr].P, N.d_inv + L.off, L.count, N.stream);
         case L_TALL:
             return launch_panel_tall(N.R[L.vr].P, N.d_tall + L.off, L.count, N.stream);
+        case L_XINV:
+            return launch_xinv64(N.R[L.vr].P, N.d_xinv + L.off, L.count, st);
+        case L_GEMM:
+            return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, 2, st);
     }
     return hipErrorInvalidValue;
 }
@@ -422,7 +441,9 @@ int64_t numeric_status(Numeric& N) {
                 case L_POTRF: slot = 4; break;
                 case L_TRSM:
                 case L_INV:
+                case L_XINV:
                 case L_TALL: slot = 5; break;
+                case L_GEMM:
                 case L_PANEL: slot = 6; break;
                 case L_CB: slot = 7; break;
                 case L_COMM: slot = 1; break;

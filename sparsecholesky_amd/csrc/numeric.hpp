@@ -21,9 +21,11 @@ enum LaunchKind : int32_t {
     L_COMM = 6,    // one comm step of the hosted ranks (pack, transfer group, unpack)
     L_INV = 7,     // inverses of a slab's factored 64 x 64 diagonal blocks (tall TRSM)
     L_TALL = 8,    // tall TRSM of a slab's rows below its diagonal block
-    L_RECORD = 9,  // record sync event `count` on stream `strm`
-    L_WAIT = 10,   // stream `strm` waits for sync event `count`
-    L_KINDS = 11
+    L_XINV = 9,    // tall-by-inverse mode: 64-block inverses of slab diagonal blocks into X / XT
+    L_GEMM = 10,   // general MFMA products (GemmTask TAG 2: inverse doubling, tall solve, staged updates)
+    L_RECORD = 11, // record sync event `count` on stream `strm`
+    L_WAIT = 12,   // stream `strm` waits for sync event `count`
+    L_KINDS = 13
 };
 
 // ---------------- multi-GPU plan (dist.cpp) ----------------
@@ -104,6 +106,7 @@ struct RankMem {
     std::vector<int64_t> cb_off;     // per supernode: full-square CB in the work arena, -1
     std::vector<int64_t> land_off;   // per supernode: R_LAND slab (ld = mb) in the work arena, -1
     std::vector<std::vector<int64_t>> blk_off;  // per split front, per column block: compact block, -1
+    std::vector<int64_t> tall_off;   // per supernode: tall-mode scratch in the handle's tall pool, -1
     int64_t panel_total = 0;     // doubles (incl. the PNB tail the TRSM reads past)
     int64_t work_total = 0;      // doubles: high-water mark of the interval plan
     int64_t work_live_max = 0;   // doubles: max over levels of the live region sizes (lower bound)
@@ -188,6 +191,7 @@ struct Numeric {
     TrsmTask* d_trsm = nullptr;
     int2* d_inv = nullptr;   // L_INV tasks (s, k0)
     int4* d_tall = nullptr;  // L_TALL tasks (s, a, r0, b)
+    XinvTask* d_xinv = nullptr;  // L_XINV tasks
     int32_t* d_arrive = nullptr;  // fused POTRF + TRSM: per-block arrival counters
     GemmTask* d_gemm = nullptr;
     int2* d_tiles = nullptr;

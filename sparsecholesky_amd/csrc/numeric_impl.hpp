@@ -85,6 +85,7 @@ struct SchedBuild {
     std::vector<int2> asmv, potrf, inv;
     std::vector<TrsmTask> trsm;
     std::vector<int4> tall;
+    std::vector<XinvTask> xinv;
     std::vector<GemmTask> gemm;
     std::vector<int2> tiles;
     CommBuild cb;
@@ -93,6 +94,25 @@ struct SchedBuild {
 // The static launch schedule of a handle (schedule.cpp): N.sched plus the task arrays
 // in B, final device addresses of the hosted ranks' pools.
 int64_t build_schedule(Numeric& N, SchedBuild& B);
+
+// Tall-TRSM-by-inverse panel mode (panel_tall = 2, schedule.cpp).  A front in the mode
+// factors each slab's diagonal block with the 64-column chain on the block's rows only,
+// forms X = inv(L11) (64-block inverses, then log2 doubling products), and solves the
+// rows below the slab as one MFMA product L21 = A21 X^T, A21 staged out of place.  Per
+// front, in the handle's tall pool (doubles, 64-aligned pieces):
+//   S   (m - nbs0) x nbs0, ld m - nbs0: the current slab's rows below its diagonal block
+//   X, XT  nbs0 x nbs0, ld nbs0: inv(L11) and its transpose
+//   U   nbs0 x nbs0: the doubling steps' intermediate products (transposed)
+struct TallLayout {
+    int32_t nbs0 = 0;     // first slab width = min(w, NBO)
+    int64_t lds = 0;      // ld of S
+    int64_t x = 0, xt = 0, u = 0, total = 0;  // offsets from the front's base, size
+};
+TallLayout tall_layout(const Symbolic& S, int32_t s, int nbo);
+bool tallx_front(const Symbolic& S, const DistPlan* D, int rank, int32_t s);
+// the hosted rank's per-front bases (level-local: fronts of one level side by side,
+// every level from 0); returns the pool size it needs, doubles
+int64_t plan_tall_scratch(const Symbolic& S, const DistPlan* D, int rank, std::vector<int64_t>& off);
 
 // dist.cpp
 hipError_t comm_launch(Numeric& N, const Launch& L);

@@ -27,6 +27,44 @@ static int wbucket_of(int w) {
     return 128;
 }
 
+static int nbo_of(const Symbolic& S) { return std::max(PNB, (S.opt.panel_nb_outer / PNB) * PNB); }
+static int64_t al64(int64_t x) { return (x + 63) / 64 * 64; }
+
+TallLayout tall_layout(const Symbolic& S, int32_t s, int nbo) {
+    TallLayout T;
+    const int w = S.w(s), m = S.sn_m[s];
+    T.nbs0 = std::min(w, nbo);
+    T.lds = std::max<int64_t>(1, m - T.nbs0);
+    const int64_t nn = (int64_t)T.nbs0 * T.nbs0;
+    T.x = al64(T.lds * T.nbs0);
+    T.xt = T.x + al64(nn);
+    T.u = T.xt + al64(nn);
+    T.total = T.u + al64(nn);
+    return T;
+}
+
+bool tallx_front(const Symbolic& S, const DistPlan* D, int rank, int32_t s) {
+    if (S.opt.panel_tall != 2 || S.fclass[s] != FRONT_LARGE) return false;
+    if (D && (D->owner[s] != rank || D->pd[s] >= 0)) return false;
+    const int w = S.w(s), m = S.sn_m[s];
+    return w >= 2 * PNB && m > std::min(w, nbo_of(S));
+}
+
+int64_t plan_tall_scratch(const Symbolic& S, const DistPlan* D, int rank, std::vector<int64_t>& off) {
+    off.assign((size_t)S.ns, -1);
+    std::vector<int64_t> used((size_t)std::max(S.nlevels, 1), 0);
+    const int nbo = nbo_of(S);
+    int64_t peak = 0;
+    for (int32_t s = 0; s < S.ns; ++s) {
+        if (!tallx_front(S, D, rank, s)) continue;
+        int64_t& u = used[S.level[s]];
+        off[s] = u;
+        u += tall_layout(S, s, nbo).total;
+        peak = std::max(peak, u);
+    }
+    return peak;
+}
+
 // Build the static launch schedule (host).  Task pointers into the pools are
 // final device addresses, so the schedule can be replayed or graph-captured.
 void append_tiles(std::vector<int2>& out, int task, int M, int N, int bt, int G) {
@@ -36,6 +74,14 @@ void append_tiles(std::vector<int2>& out, int task, int M, int N, int bt, int G)
             for (int tj = sj; tj < std::min(TN, sj + G); ++tj)
                 for (int ti = std::max(si, tj); ti < std::min(TM, si + G); ++ti)
                     out.push_back(make_int2(task, (ti << 16) | tj));
+}
+
+void append_tiles_full(std::vector<int2>& out, int task, int M, int N, int bt, int G) {
+    const int TM = (M + bt - 1) / bt, TN = (N + bt - 1) / bt;
+    for (int sj = 0; sj < TN; sj += G)
+        for (int si = 0; si < TM; si += G)
+            for (int tj = sj; tj < std::min(TN, sj + G); ++tj)
+                for (int ti = si; ti < std::min(TM, si + G); ++ti) out.push_back(make_int2(task, (ti << 16) | tj));
 }
 
 void xcd_order(int2* tiles, int64_t n) {
@@ -135,6 +181,10 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
     // and written
     auto task_bytes = [&](const GemmTask& t) {
         const double pairs = (double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0;
+        if (t.B) {  // general product: both operands once, the output (and Cin) once
+            const double outs = t.lower ? pairs : (double)t.M * t.N;
+            return 8.0 * (t.M + (double)t.N) * t.K + 8.0 * outs * ((t.C ? 1 : 0) + (t.Ct ? 1 : 0) + (t.Cin ? 1 : 0));
+        }
         double b = 8.0 * t.M * (double)t.K;
         if (t.gs < 0) return b + 16.0 * pairs;
         b += 8.0 * pairs;
@@ -169,10 +219,20 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // more to the lean instance's smaller gather batches than they gain in occupancy)
         L.lean = L.bt == SYRK_BT_SMALL && S.opt.syrk_lean_kmax > 0 && maxK <= S.opt.syrk_lean_kmax &&
                  (kind == L_PANEL || maxK > 64);
+        if (kind == L_GEMM) {  // general products: tile by the smaller output edge
+            int minMN = INT32_MAX;
+            for (auto& t : tasks) minMN = std::min(minMN, std::min((int)t.M, (int)t.N));
+            L.bt = minMN >= 256 ? SYRK_BT_LARGE : SYRK_BT_SMALL;
+            L.epi = 0;
+            L.lean = 0;
+        }
         L.toff = (int64_t)tiles.size();
         L.bytes = 0.0;
         for (size_t q = 0; q < tasks.size(); ++q) {
-            append_tiles(tiles, (int)q, tasks[q].M, tasks[q].N, L.bt);
+            if (kind == L_GEMM && !tasks[q].lower)
+                append_tiles_full(tiles, (int)q, tasks[q].M, tasks[q].N, L.bt);
+            else
+                append_tiles(tiles, (int)q, tasks[q].M, tasks[q].N, L.bt);
             gemm.push_back(tasks[q]);
             L.bytes += task_bytes(tasks[q]);
         }
@@ -377,6 +437,136 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             push_gemm_launch(L_CB, lev, cbt, w >= 256 ? 1 : 0, fl);
         }
     };
+    // general product task (L_GEMM): out(i, j) = Cin(i, j) - sum_k A(i, k) B(j, k), i < M,
+    // j < N (lower: j <= i only), stored at C
+    auto gen_update = [&](std::vector<GemmTask>& vec, double& fl, double* C, int64_t ldc, const double* Cin,
+                          int64_t ldin, const double* A, int64_t lda, const double* Bm, int64_t ldb, int M, int Nn,
+                          int K, bool lower) {
+        if (M <= 0 || Nn <= 0 || K <= 0) return;
+        GemmTask t {};
+        t.C = C;
+        t.ldc = ldc;
+        t.Cin = Cin;
+        t.ldin = ldin;
+        t.A = A;
+        t.lda = lda;
+        t.B = Bm;
+        t.ldb = ldb;
+        t.M = M;
+        t.N = Nn;
+        t.K = K;
+        t.lower = lower ? 1 : 0;
+        t.sign = -1.0;
+        vec.push_back(t);
+        fl += 2.0 * K * (lower ? ((double)Nn * M - (double)Nn * (Nn - 1) / 2.0) : (double)Nn * M);
+    };
+    // Slab end of tall-by-inverse fronts tx = (s, slab0) on hosted rank v, after the
+    // chain has factored the slabs' diagonal blocks (the reference's cblas_dtrsm,
+    // chol.hpp:1292, for the rows below them, as products):
+    //   1. xinv64: the 64-block inverses of each diagonal block into X / XT
+    //   2. per doubling width b = 64, 128, ...: X = [Xa 0; E Xb] for every pair of
+    //      b-blocks, E = -Xb (B Xa), B = L(c-block rows, a-block columns), as two general
+    //      products (U^T = (B Xa)^T, then E and E^T)
+    //   3. the tall solve L21 = A21 X^T (K trimmed to the triangle), A21 from the staging
+    //      buffer, L21 written into the panel
+    auto emit_tallx = [&](int32_t lev, int v, const std::vector<int2>& tx) {
+        const RankMem& R = N.R[v];
+        struct F {
+            int32_t s, c0, nbs, m;
+            double *pan, *base, *X, *XT, *U;
+            int64_t ldx, lds;
+        };
+        std::vector<F> fr;
+        int maxnb = 0;
+        for (const int2& e : tx) {
+            F f {};
+            f.s = e.x;
+            f.c0 = e.y;
+            f.nbs = std::min(S.w(f.s), f.c0 + NBO) - f.c0;
+            f.m = S.sn_m[f.s];
+            const TallLayout TL = tall_layout(S, f.s, NBO);
+            f.pan = R.P.panel_pool + R.panel_off[f.s];
+            f.base = R.P.tall_pool + R.tall_off[f.s];
+            f.X = f.base + TL.x;
+            f.XT = f.base + TL.xt;
+            f.U = f.base + TL.u;
+            f.ldx = TL.nbs0;
+            f.lds = TL.lds;
+            fr.push_back(f);
+            maxnb = std::max(maxnb, f.nbs);
+        }
+        Launch Lx {};
+        Lx.kind = L_XINV;
+        Lx.level = lev;
+        Lx.vr = v;
+        Lx.off = (int64_t)B.xinv.size();
+        for (const F& f : fr)
+            for (int q = 0; q * PNB < f.nbs; ++q)
+                B.xinv.push_back(XinvTask {f.X, f.XT, f.ldx, f.s, f.c0, q, f.nbs});
+        Lx.count = (int32_t)((int64_t)B.xinv.size() - Lx.off);
+        N.sched.push_back(Lx);
+        for (int b = PNB; b < maxnb; b *= 2) {
+            std::vector<GemmTask> ut, et;
+            double fu = 0.0, fe = 0.0;
+            for (const F& f : fr)
+                for (int pb = 0, pi = 0; pb + b < f.nbs; pb += 2 * b, ++pi) {
+                    const int valid = std::min(b, f.nbs - pb - b);
+                    double* Ui = f.U + (int64_t)pi * b * b;
+                    GemmTask u {};
+                    u.A = f.pan + (int64_t)(f.c0 + pb) * f.m + (f.c0 + pb + b);  // B = L(c rows, a columns)
+                    u.lda = f.m;
+                    u.B = f.XT + pb + (int64_t)pb * f.ldx;  // Xa(k, j) = XT(pb + j, pb + k)
+                    u.ldb = f.ldx;
+                    u.M = valid;
+                    u.N = b;
+                    u.K = b;
+                    u.C = nullptr;
+                    u.Ct = Ui;  // U(i, j) at Ui[j + i b]
+                    u.ldt = b;
+                    u.sign = 1.0;
+                    ut.push_back(u);
+                    fu += 2.0 * valid * (double)b * b;
+                    GemmTask q {};
+                    q.A = f.X + (pb + b) + (int64_t)(pb + b) * f.ldx;  // Xb
+                    q.lda = f.ldx;
+                    q.B = Ui;  // U(k, j) = Ui[j + k b]
+                    q.ldb = b;
+                    q.M = valid;
+                    q.N = b;
+                    q.K = valid;
+                    q.C = f.X + (pb + b) + (int64_t)pb * f.ldx;     // E into X
+                    q.ldc = f.ldx;
+                    q.Ct = f.XT + pb + (int64_t)(pb + b) * f.ldx;   // and E^T into XT
+                    q.ldt = f.ldx;
+                    q.sign = -1.0;
+                    et.push_back(q);
+                    fe += 2.0 * valid * (double)b * valid;
+                }
+            push_gemm_launch(L_GEMM, lev, ut, 0, fu);
+            push_gemm_launch(L_GEMM, lev, et, 0, fe);
+        }
+        std::vector<GemmTask> tt;
+        double ft = 0.0;
+        for (const F& f : fr) {
+            const int c1 = f.c0 + f.nbs;
+            if (f.m <= c1) continue;
+            GemmTask t {};
+            t.A = f.base;  // S: rows [c1, m) of the slab's columns
+            t.lda = f.lds;
+            t.B = f.X;
+            t.ldb = f.ldx;
+            t.M = f.m - c1;
+            t.N = f.nbs;
+            t.K = f.nbs;
+            t.C = f.pan + (int64_t)f.c0 * f.m + c1;
+            t.ldc = f.m;
+            t.sign = 1.0;
+            t.ktri = 1;
+            tt.push_back(t);
+            ft += (double)(f.m - c1) * f.nbs * (double)f.nbs;
+        }
+        push_gemm_launch(L_GEMM, lev, tt, 0, ft);
+    };
     // one level's fronts of hosted rank v
     auto emit_level = [&](int32_t lev, const std::vector<int32_t>& nodes, int v) {
         double* panel_pool = N.R[v].P.panel_pool;
@@ -420,6 +610,9 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // columns, 256-row tile), write-once (big = 1); smaller fronts one workgroup per
         // (front, 16 columns) streaming child columns (measured faster below ~8k rows)
         const int tile_min_m = S.opt.asm_tile_min_m > 0 ? S.opt.asm_tile_min_m : ASM_TILE_MIN_M;
+        // tall-by-inverse fronts (tall_layout): the tile assembly stages their first slab's
+        // rows below its diagonal block in the scratch the slab's tall solve reads
+        auto tallx = [&](int32_t s) { return N.R[v].tall_off.size() > (size_t)s && N.R[v].tall_off[s] >= 0; };
         for (int tiled = 1; tiled >= 0; --tiled) {
             Launch L {};
             L.kind = L_ASM;
@@ -429,7 +622,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             L.off = (int64_t)asmv.size();
             for (int32_t s : large) {
                 const int m = S.sn_m[s];
-                if ((m >= tile_min_m) != (tiled == 1)) continue;
+                if ((m >= tile_min_m || tallx(s)) != (tiled == 1)) continue;
                 const int ncol = gather(s) ? S.w(s) : m;  // assembled columns
                 for (int cb = 0; cb * ASM_COLS < ncol; ++cb) {
                     if (!tiled) {
@@ -467,11 +660,13 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             vec.push_back(t);
             fl += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
         };
-        // tall mode (a front of more than one 64-column block): the 64-column chain
+        // tall modes (a front of more than one 64-column block): the 64-column chain
         // (POTRF / TRSM / inner updates) runs on the slab's diagonal-block rows only; at
-        // the slab end the block inverses and one tall-TRSM launch solve every row below
-        // the slab (panel_tall_kernel), then the outer updates as before
-        auto tall = [&](int32_t s) { return S.opt.panel_tall && S.w(s) > PNB; };
+        // the slab end every row below the slab is solved -- panel_tall = 1: block
+        // inverses and one row-blocked tall-TRSM launch (panel_tall_kernel); panel_tall =
+        // 2 (tallx fronts): X = inv(L11) and one MFMA product L21 = A21 X^T -- then the
+        // outer updates as before
+        auto tall = [&](int32_t s) { return (S.opt.panel_tall == 1 && S.w(s) > PNB) || tallx(s); };
         // fronts whose next TRSM launch folds in the pending span-64 inner update (recursive
         // order, an even block of the slab followed by a full block): the update launch of
         // that step is dropped, one dispatch fewer on the chain per two steps
@@ -506,6 +701,8 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             const bool split_step = S.opt.trsm_split_wg > 0 && step_wg > S.opt.trsm_split_wg;
             std::vector<int2> inv_t;           // tall mode, slab end: diagonal-block inverses
             std::vector<int4> tall_t;          // ... and the tall TRSM of the rows below
+            std::vector<int2> tx;              // tall-by-inverse fronts at a slab end: (s, slab0)
+            std::vector<GemmTask> outer_a2;    // ... their next-slab updates (general products)
             double uflops = 0.0, afl = 0.0, bfl = 0.0;
             for (int32_t s : large) {
                 const int w = S.w(s), m = S.sn_m[s];
@@ -543,15 +740,35 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 } else if (k1 < slab1) {
                     add_update(upd, uflops, pan, m, rend, k1, slab1, k0, k1);
                 }
-                if (k1 == slab1 && tall(s)) {
+                if (k1 == slab1 && tall(s) && !tallx(s)) {
                     for (int kb = slab0; kb < slab1; kb += PNB) inv_t.push_back(make_int2(s, kb));
                     for (int r0 = slab1; r0 < m; r0 += TALL_ROWS) tall_t.push_back(make_int4(s, slab0, r0, slab1));
                 }
+                if (k1 == slab1 && tallx(s)) tx.push_back(make_int2(s, slab0));
                 if (k1 == slab1 && slab1 < w) {
                     // outer_a is the last update of block slab1: a pending stream-1 outer
                     // update of those columns is waited for before outer_a runs
                     const int nxt = S.opt.lookahead ? std::min(w, slab1 + NBO) : w;
-                    add_update(outer_a, afl, pan, m, m, slab1, nxt, slab0, slab1);
+                    if (tallx(s)) {
+                        // the next slab's columns: its diagonal block in place, its rows below
+                        // (final after this update) to the staging buffer its tall solve reads
+                        const int n1 = std::min(w, slab1 + NBO);
+                        const TallLayout TL = tall_layout(S, s, NBO);
+                        double* Sb = N.R[v].P.tall_pool + N.R[v].tall_off[s];
+                        const int K = slab1 - slab0;
+                        gen_update(outer_a2, afl, pan + (int64_t)slab1 * m + slab1, m, pan + (int64_t)slab1 * m + slab1,
+                                   m, pan + (int64_t)slab0 * m + slab1, m, pan + (int64_t)slab0 * m + slab1, m,
+                                   n1 - slab1, n1 - slab1, K, true);
+                        gen_update(outer_a2, afl, Sb, TL.lds, pan + (int64_t)slab1 * m + n1, m,
+                                   pan + (int64_t)slab0 * m + n1, m, pan + (int64_t)slab0 * m + slab1, m, m - n1,
+                                   n1 - slab1, K, false);
+                        if (nxt > n1)  // no lookahead: the rest of the trailing columns, in place
+                            gen_update(outer_a2, afl, pan + (int64_t)n1 * m + n1, m, pan + (int64_t)n1 * m + n1, m,
+                                       pan + (int64_t)slab0 * m + n1, m, pan + (int64_t)slab0 * m + n1, m, m - n1,
+                                       nxt - n1, K, true);
+                    } else {
+                        add_update(outer_a, afl, pan, m, m, slab1, nxt, slab0, slab1);
+                    }
                     add_update(outer_b, bfl, pan, m, m, nxt, w, slab0, slab1);
                 }
             }
@@ -584,6 +801,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 N.sched.push_back(Lq);
             }
             push_gemm_launch(L_PANEL, lev, upd, 0, uflops);
+            if (!tx.empty()) emit_tallx(lev, v, tx);
             if (!tall_t.empty() || !inv_t.empty()) {
                 Launch Li {};
                 Li.kind = L_INV;
@@ -612,12 +830,16 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             }
             int e_trsm = -1;
             if (!outer_b.empty()) e_trsm = push_record(0);
-            if (!outer_a.empty()) {
+            if (!outer_a.empty() || !outer_a2.empty()) {
                 if (b_pending >= 0) {
                     push_wait(0, b_pending);
                     b_pending = -1;
                 }
-                push_gemm_launch(L_PANEL, lev, outer_a, 0, afl);
+                double fa = 0.0, fa2 = 0.0;
+                for (const GemmTask& t : outer_a) fa += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
+                fa2 = afl - fa;
+                push_gemm_launch(L_PANEL, lev, outer_a, 0, fa);
+                push_gemm_launch(L_GEMM, lev, outer_a2, 0, fa2);
             }
             if (!outer_b.empty()) {
                 push_wait(1, e_trsm);
