@@ -233,6 +233,13 @@ int64_t sc_numeric_syrk_stats(sc_numeric* num, int32_t wmin, double* flops, doub
  * whose tail tiles are re-cut into a launch of their own splits its bytes in
  * proportion to the flops. */
 int64_t sc_numeric_syrk_bytes(sc_numeric* num, int32_t wmin, double* bytes);
+/* Timeline of the last profiled (sc_numeric_set_profile(num, 1)) factorization: per
+ * launch its start and end (ms from the first main-stream launch), its kind (the
+ * launch-trace kinds; 6 = a comm step), for comm steps the step index of the plan
+ * (sc_dist_steps, else -1) and its stream (0 main, 1 lookahead, 2 comm).  Returns the
+ * number of launches (t0 == NULL: count only). */
+int64_t sc_numeric_launch_times(sc_numeric* num, double* t0, double* t1, int32_t* kind, int32_t* step,
+                                int32_t* stream, int64_t cap);
 /* Device memory of the handle, bytes: info[0] everything allocated (pools, plan,
  * staging, a gathered factor), info[1] panel arenas (L), info[2] work arenas (the
  * interval-planned contribution blocks), info[3] the work arenas' lower bound (the

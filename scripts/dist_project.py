@@ -10,10 +10,23 @@ Communication term (host-only, from the plan's message list, sc_dist_schedule): 
 comm step a rank's exchange with each peer runs on that pair's own xGMI link, so the
 step takes max over peers of max(bytes sent, bytes received) / link_GBs plus a
 per-message latency.  comm_ms = the sum over the rank's steps, i.e. every transfer
-serialised behind the rank's compute (nothing overlapped): rank_ms + comm_ms is an
-upper-bound projection, rank_ms alone the lower bound.
+serialised behind the rank's compute (nothing overlapped): rank_ms + comm_ms is the
+"serialised-comm estimate" -- NOT an upper bound: it leaves out the time a rank waits
+for another rank's compute.
 
-  python scripts/dist_project.py [--k 128] [--n 2,4,8] [--opt key=value ...]
+Critical-path estimate (--timeline, one extra eager profiled factorization per rank):
+each rank's dry timeline gives, per comm step, the time its comm stream posts the step
+(sends: when the data is computed) and the time its main stream needs the step (the
+start of its next main-stream launch).  A discrete-event replay over the plan's global
+step order then moves every message over its link (link_GBs per direction, msg_us each,
+one transfer at a time per directed link), starts a step on a rank no earlier than the
+rank's previous step (one in-order comm stream), and delays a receiving rank's compute
+from the need point until its data has arrived -- so waiting on other ranks' compute
+and on the links is on the critical path, while transfers that overlap compute are
+not.  Assumed, not measured: link_GBs (default 50 GB/s per direction of one xGMI
+link; 153 GB/s spec) and msg_us.
+
+  python scripts/dist_project.py [--k 128] [--n 2,4,8] [--opt key=value ...] [--timeline] [--graph]
   python scripts/dist_project.py --comm-only      (no GPU: the communication term alone)
 """
 import argparse
@@ -51,6 +64,59 @@ def comm_model(symb, n, link_gbs, msg_us):
     return out
 
 
+def rank_timeline(num):
+    """From one eager profiled factorization of a dry handle: (total ms, post[step],
+    need[step]) -- the step's comm-stream start, and the start of the first main-stream
+    launch after it in schedule order (the point the main stream waits for the step)."""
+    tl = num.launch_times()
+    t0, t1, kind, step, strm = tl["t0"], tl["t1"], tl["kind"], tl["step"], tl["stream"]
+    total = float(max(t1.max(), 0.0)) if len(t1) else 0.0
+    post, need = {}, {}
+    for i in range(len(t0)):
+        if kind[i] != 6:
+            continue
+        st = int(step[i])
+        post[st] = float(t0[i])
+        nxt = next((float(t0[j]) for j in range(i + 1, len(t0)) if strm[j] == 0), total)
+        need[st] = max(nxt, float(t1[i]))
+    return total, post, need
+
+
+def critical_path(symb, n, timelines, link_gbs, msg_us):
+    """Discrete-event replay of the plan's comm steps over the ranks' dry timelines (see
+    the module docstring).  Returns per-rank finish times (ms)."""
+    sends = {}  # step -> [(src, dst, bytes)] in plan order
+    for r in range(n):
+        step, peer, nb, snd = symb.dist_schedule(n, r)
+        for st, p, b, s in zip(step, peer, nb, snd):
+            if s:
+                sends.setdefault(int(st), []).append((r, int(p), int(b)))
+    delay = [0.0] * n      # accumulated wait of each rank's main stream
+    comm_free = [0.0] * n  # each rank's comm stream
+    link_free = {}
+    for st in sorted(sends):
+        msgs = sends[st]
+        parts = sorted({m[0] for m in msgs} | {m[1] for m in msgs})
+        start = {}
+        for r in parts:
+            _, post, _ = timelines[r]
+            start[r] = max(post.get(st, 0.0) + delay[r], comm_free[r])
+        done = dict(start)
+        for src, dst, b in msgs:
+            t = max(start[src], start[dst], link_free.get((src, dst), 0.0))
+            t += b / (link_gbs * 1e9) * 1e3 + msg_us * 1e-3
+            link_free[(src, dst)] = t
+            done[src] = max(done[src], t)
+            done[dst] = max(done[dst], t)
+        for r in parts:
+            comm_free[r] = done[r]
+            if any(m[1] == r for m in msgs):  # a receiver waits at its need point
+                _, _, need = timelines[r]
+                nd = need.get(st, 0.0)
+                delay[r] = max(delay[r], done[r] - nd)
+    return [round(max(timelines[r][0] + delay[r], comm_free[r]), 2) for r in range(n)]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--k", type=int, default=128)
@@ -61,6 +127,10 @@ def main():
                     help="achievable GB/s per direction of one xGMI link (spec 153 per link)")
     ap.add_argument("--msg-us", type=float, default=10.0, help="per-message latency, us")
     ap.add_argument("--comm-only", action="store_true")
+    ap.add_argument("--timeline", action="store_true",
+                    help="also the critical-path estimate (one eager profiled factorization per rank)")
+    ap.add_argument("--graph", action="store_true",
+                    help="also time every rank's dry schedule replayed as one hipGraph (eager vs graph gap)")
     args = ap.parse_args()
     import sparsecholesky_amd as sc
 
@@ -82,38 +152,68 @@ def main():
         kw[key] = int(val)
     A = sc.laplacian3d(args.k)
     symb = sc.Symbolic(A, **kw)
+    symb_g = sc.Symbolic(A, use_graph=1, **kw) if args.graph else None
     F = symb.stats()["flops"]
     d_Ax = torch.from_numpy(A.x).to("cuda:0")
+
+    def timed(num):
+        num.factor_device(d_Ax.data_ptr(), sync=True)
+        best = None
+        for _ in range(args.reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            num.factor_device(d_Ax.data_ptr(), sync=False)
+            num.status()
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) * 1e3
+            best = dt if best is None else min(best, dt)
+        return round(best, 2)
+
     for n in [int(x) for x in args.n.split(",")]:
         info = symb.dist_plan_info(n)
         _, work = symb.owner_map(n)
-        per = []
+        per, per_g, tls = [], [], []
         for r in range(n):
             num = sc.Numeric(symb, device=0, rank=r, nranks=n, transport="dry")
-            num.factor_device(d_Ax.data_ptr(), sync=True)
-            best = None
-            for _ in range(args.reps):
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                num.factor_device(d_Ax.data_ptr(), sync=False)
-                num.status()
-                torch.cuda.synchronize()
-                dt = (time.perf_counter() - t0) * 1e3
-                best = dt if best is None else min(best, dt)
-            per.append(round(best, 2))
+            best = timed(num)
+            per.append(best)
+            if args.timeline:
+                num.set_profile(1)
+                num.factor_device(d_Ax.data_ptr(), sync=True)
+                tot, post, need = rank_timeline(num)
+                f = best / tot if tot > 0 else 1.0  # the event-bracketed run is slower: rescale
+                tls.append((best, {k: v * f for k, v in post.items()}, {k: v * f for k, v in need.items()}))
             del num
             gc.collect()
-            print(f"  n={n} rank {r}: {best:.1f} ms", flush=True)
+            msg = f"  n={n} rank {r}: {best:.1f} ms"
+            if symb_g is not None:
+                num = sc.Numeric(symb_g, device=0, rank=r, nranks=n, transport="dry")
+                per_g.append(timed(num))
+                del num
+                gc.collect()
+                msg += f" (graph {per_g[-1]:.1f} ms)"
+            print(msg, flush=True)
         mx = max(per)
         cm = comm_model(symb, n, args.link_gbs, args.msg_us)
         with_comm = [round(a + b, 2) for a, b in zip(per, cm["comm_ms"])]
-        print(json.dumps({"k": args.k, "n": n, "opts": kw, "rank_ms": per, "max_rank_ms": mx,
-                          "projected_gflops_upper": round(F / (mx * 1e-3) / 1e9, 1),
-                          "rank_ms_with_comm_serial": with_comm, "max_rank_ms_with_comm_serial": max(with_comm),
-                          "projected_gflops_with_comm_serial": round(F / (max(with_comm) * 1e-3) / 1e9, 1),
-                          "link_GBs": args.link_gbs, **cm,
-                          "work_share": [round(float(x) / float(work.sum()), 3) for x in work],
-                          "comm_steps": info["n_steps"], "messages": info["n_msgs"]}), flush=True)
+        rec = {"k": args.k, "n": n, "opts": kw, "rank_ms": per, "max_rank_ms": mx,
+               "projected_gflops_no_comm": round(F / (mx * 1e-3) / 1e9, 1),
+               "rank_ms_with_comm_serial": with_comm, "max_rank_ms_with_comm_serial": max(with_comm),
+               "projected_gflops_with_comm_serial": round(F / (max(with_comm) * 1e-3) / 1e9, 1),
+               "link_GBs": args.link_gbs, "msg_us": args.msg_us, **cm,
+               "work_share": [round(float(x) / float(work.sum()), 3) for x in work],
+               "comm_steps": info["n_steps"], "messages": info["n_msgs"]}
+        if per_g:
+            rec["rank_ms_graph"] = per_g
+            rec["max_rank_ms_graph"] = max(per_g)
+        if tls:
+            for gbs in sorted({args.link_gbs, 100.0}):
+                cp = critical_path(symb, n, tls, gbs, args.msg_us)
+                rec[f"critical_path_ms_{int(gbs)}GBs"] = cp
+                rec[f"max_critical_path_ms_{int(gbs)}GBs"] = max(cp)
+                rec[f"projected_gflops_critical_path_{int(gbs)}GBs"] = round(F / (max(cp) * 1e-3) / 1e9, 1)
+            rec["timeline_total_ms"] = [round(t[0], 2) for t in tls]
+        print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":

@@ -122,6 +122,7 @@ _SIGS = [
     ("sc_numeric_launch_trace", _I64, [_P, _P, _P, _P, _P, _P, _I64]),
     ("sc_numeric_syrk_stats", _I64, [_P, _I32, C.POINTER(_D), C.POINTER(_D), C.POINTER(_I64)]),
     ("sc_numeric_syrk_bytes", _I64, [_P, _I32, C.POINTER(_D)]),
+    ("sc_numeric_launch_times", _I64, [_P, _P, _P, _P, _P, _P, _I64]),
     ("sc_free_numeric", None, [_P]),
     ("sc_solve_host", _I64, [_P, _P, _P]),
     ("sc_solve_device", _I64, [_P, _P, _P]),
@@ -622,6 +623,16 @@ class Numeric:
         fl, ms, nl = C.c_double(), C.c_double(), C.c_int64()
         _check(lib().sc_numeric_syrk_stats(self.h, wmin, C.byref(fl), C.byref(ms), C.byref(nl)), "syrk_stats")
         return fl.value, ms.value, nl.value
+
+    def launch_times(self) -> dict:
+        """Per launch of the last profiled factorization: start / end ms (from the first
+        main-stream launch), kind, comm step index (-1 if not a comm launch)."""
+        n = _check(lib().sc_numeric_launch_times(self.h, None, None, None, None, None, 0), "launch_times")
+        t0, t1 = np.zeros(max(n, 1)), np.zeros(max(n, 1))
+        k, st, sm = (np.zeros(max(n, 1), dtype=np.int32) for _ in range(3))
+        _check(lib().sc_numeric_launch_times(self.h, _ptr(t0), _ptr(t1), _ptr(k), _ptr(st), _ptr(sm), n),
+               "launch_times")
+        return dict(t0=t0[:n], t1=t1[:n], kind=k[:n], step=st[:n], stream=sm[:n])
 
     def syrk_bytes(self, wmin: int = 256) -> float:
         """Algorithmic HBM bytes of the launches syrk_stats(wmin) selects (C ABI

@@ -325,6 +325,13 @@ int64_t sc_numeric_syrk_stats(sc_numeric* num, int32_t wmin, double* flops, doub
     return sc::numeric_syrk_stats(*num->N, wmin, flops, ms, launches);
 }
 
+int64_t sc_numeric_launch_times(sc_numeric* num, double* t0, double* t1, int32_t* kind, int32_t* step,
+                                int32_t* stream, int64_t cap) {
+    if (!num || !num->N) return SC_ERR_ARG;
+    if (t0 && (!t1 || !kind || !step || !stream)) return SC_ERR_ARG;
+    return sc::numeric_launch_times(*num->N, t0, t1, kind, step, stream, cap);
+}
+
 int64_t sc_numeric_syrk_bytes(sc_numeric* num, int32_t wmin, double* bytes) {
     if (!num || !num->N || !bytes) return SC_ERR_ARG;
     return sc::numeric_syrk_bytes(*num->N, wmin, bytes);

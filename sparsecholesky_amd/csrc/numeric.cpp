@@ -504,6 +504,33 @@ int64_t numeric_launch_trace(Numeric& N, int32_t* kind, int32_t* level, int32_t*
     return n;
 }
 
+// Start / end (ms from the first main-stream launch) of every launch of the last
+// profiled factorization, the launch kind and, for comm launches, the comm step.
+int64_t numeric_launch_times(Numeric& N, double* t0, double* t1, int32_t* kind, int32_t* step, int32_t* strm,
+                             int64_t cap) {
+    if (N.profile != 1 || !N.status_valid) return SC_ERR_STATE;
+    hipEvent_t origin = nullptr;
+    for (size_t i = 0; i < N.sched.size() && !origin; ++i)
+        if (N.sched[i].kind < L_RECORD && N.sched[i].strm == 0) origin = N.ev[2 * i];
+    int64_t n = 0;
+    for (size_t i = 0; i < N.sched.size(); ++i) {
+        const Launch& l = N.sched[i];
+        if (l.kind >= L_RECORD) continue;
+        if (n < cap && t0) {
+            float a = 0.f, b = 0.f;
+            HIP_TRY(hipEventElapsedTime(&a, origin, N.ev[2 * i]));
+            HIP_TRY(hipEventElapsedTime(&b, origin, N.ev[2 * i + 1]));
+            t0[n] = a;
+            t1[n] = b;
+            kind[n] = l.kind;
+            step[n] = l.kind == L_COMM ? l.step : -1;
+            strm[n] = l.strm;
+        }
+        ++n;
+    }
+    return n;
+}
+
 int64_t numeric_timing(Numeric& N, double* t, int nt) {
     if (N.profile != 1 || !N.status_valid) return SC_ERR_STATE;
     for (int i = 0; i < nt && i < 8; ++i) t[i] = N.phase_ms[i];

@@ -294,6 +294,8 @@ int64_t numeric_launch_trace(Numeric& N, int32_t* kind, int32_t* level, int32_t*
                              int64_t cap);
 int64_t numeric_syrk_stats(Numeric& N, int wmin, double* flops, double* ms, int64_t* launches);
 int64_t numeric_syrk_bytes(Numeric& N, int wmin, double* bytes);
+int64_t numeric_launch_times(Numeric& N, double* t0, double* t1, int32_t* kind, int32_t* step, int32_t* strm,
+                             int64_t cap);
 void numeric_free(Numeric* N);
 // x = A^{-1} b with the factor: device vectors of length n (may alias), on the
 // library stream, synchronous.  Multi-rank handles gather the factor first
