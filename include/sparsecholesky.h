@@ -113,6 +113,10 @@ typedef struct sc_options {
     int32_t tiny_dense;      /* 1 (default): on one device, a matrix with n <= 64 factors as one dense n x n
                                 lower triangle in a single wave (the symbolic pattern is exact: entries outside
                                 it come out as exact zeros and are not exported); 0: the tiny-tree launch */
+    int32_t dist_asm;        /* multi-GPU: 1 (default): a shared front with a distributed panel or split CB is
+                                assembled where its columns live (each rank its own slabs / CB blocks; child CB
+                                columns go straight to the rank owning the parent columns they map into, no
+                                assembled-front hand-out); 0: its owner assembles it and sends the pieces */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

@@ -72,6 +72,31 @@ bool DistPlan::holds(int32_t s, int r) const {
     return std::binary_search(h.begin(), h.end(), r);
 }
 
+int DistPlan::col_owner(const Symbolic& S, int32_t p, int col) const {
+    const int w = S.w(p);
+    if (col < w) return pd[p] >= 0 ? slab_rank[pd[p]][col / nbo] : owner[p];
+    return split[p] >= 0 ? cb_rank[split[p]][(col - w) / cbb] : owner[p];
+}
+
+bool DistPlan::receives(const Symbolic& S, int32_t c, int r) const {
+    const int32_t p = S.sn_parent[c];
+    if (p < 0) return false;
+    if (!dasm[p]) return owner[p] == r;
+    const int32_t* rel = S.relind.data() + S.rel_ptr[c];
+    for (int j = 0; j < S.mb(c); ++j)
+        if (col_owner(S, p, rel[j]) == r) return true;
+    return false;
+}
+
+bool DistPlan::produces_cb(const Symbolic& S, int32_t s, int r) const {
+    if (S.mb(s) <= 0) return false;
+    if (split[s] < 0) return owner[s] == r;
+    if (owner[s] == r && !dasm[s]) return true;  // assembles the whole CB, sends its blocks (STEP_INIT)
+    for (int32_t q : cb_rank[split[s]])
+        if (q == r) return true;
+    return false;
+}
+
 int DistPlan::need_row(const Symbolic& S, int32_t s, int k, int r) const {
     const int m = S.sn_m[s];
     const std::vector<int32_t>& sr = slab_rank[pd[s]];
@@ -218,6 +243,9 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
         D.holders[q] = std::move(h);
     }
 
+    D.dasm.assign((size_t)ns, 0);
+    for (i32 s = 0; s < ns; ++s)
+        D.dasm[s] = S.opt.dist_asm != 0 && shared[s] && (D.pd[s] >= 0 || D.split[s] >= 0);
     D.early_gw = 4 * D.cbb;
     D.early.assign((size_t)ns, 0);
     for (i32 c = 0; c < ns; ++c) {
@@ -264,11 +292,12 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
             if (D.pd[s] < 0) continue;
             const std::vector<i32>& sr = D.slab_rank[D.pd[s]];
             const int own = D.owner[s], w = S.w(s), nsl = (int)sr.size();
-            // INIT: assembled slab columns to their owners, CB blocks to the CB ranks
+            // INIT (owner-assembled fronts only): assembled slab columns to their owners,
+            // CB blocks to the CB ranks
             int32_t id = open_step(STEP_INIT, lev, s, 0);
-            for (int k = 1; k < nsl; ++k)
+            for (int k = 1; k < nsl && !D.dasm[s]; ++k)
                 if (sr[k] != own) panel_msg(id, s, own, sr[k], k * D.nbo, k * D.nbo, std::min(w, (k + 1) * D.nbo));
-            if (D.split[s] >= 0) {
+            if (D.split[s] >= 0 && !D.dasm[s]) {
                 const std::vector<i32>& cbr = D.cb_rank[D.split[s]];
                 for (int jb = 0; jb < (int)cbr.size(); ++jb) {
                     if (cbr[jb] == own) continue;  // computed in place in the owner's CB
@@ -302,7 +331,7 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
             const std::vector<i32>& cbr = D.cb_rank[D.split[s]];
             const int own = D.owner[s], m = S.sn_m[s], w = S.w(s), mb = m - w;
             int32_t id = open_step(STEP_INIT, lev, s, 0);
-            for (int jb = 0; jb < (int)cbr.size(); ++jb) {
+            for (int jb = 0; jb < (int)cbr.size() && !D.dasm[s]; ++jb) {
                 DistMsg g {};
                 g.step = id;
                 g.src = own;
@@ -336,19 +365,41 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
                 close_step(id);
             }
         }
+        // child c's CB columns [j0, j1) (computed on src) to the ranks that assemble the
+        // parent columns they map into: the parent's owner, or, distributed assembly,
+        // each run of consecutive columns to the owner of its parent slab / CB block
+        // (rows from the run's first column down; a run on src itself stays put)
+        auto deliver_cols = [&](int32_t id, i32 c, int src, int j0, int j1) {
+            const i32 p = S.sn_parent[c];
+            const int mbc = S.mb(c);
+            const int32_t* rel = S.relind.data() + S.rel_ptr[c];
+            auto dst_of = [&](int j) { return D.dasm[p] ? D.col_owner(S, p, rel[j]) : D.owner[p]; };
+            for (int a = j0; a < j1;) {
+                const int r = dst_of(a);
+                int b = a + 1;
+                while (b < j1 && dst_of(b) == r) ++b;
+                if (r != src) {
+                    DistMsg g {};
+                    g.step = id;
+                    g.src = src;
+                    g.dst = r;
+                    g.skind = g.dkind = R_CB;
+                    g.srow = g.scol = g.drow = g.dcol = a;
+                    g.rows = mbc - a;
+                    g.cols = b - a;
+                    g.s = c;
+                    D.msgs.push_back(g);
+                }
+                a = b;
+            }
+        };
         for (i32 c : by_level[lev]) {  // early children: one sub-step per column group
             if (!D.early[c]) continue;
             const int mbc = S.mb(c), per = D.early_gw / D.cbb;
             for (int g = 0; g * D.early_gw < mbc; ++g) {
                 const int32_t id = open_step(STEP_DELIVER, lev, c, g);
-                for (int jb = g * per; jb < (g + 1) * per && jb * D.cbb < mbc; ++jb) {
-                    DistMsg m {};
-                    m.step = id;
-                    m.src = D.owner[c];
-                    m.dst = D.owner[S.sn_parent[c]];
-                    cb_block(m, c, jb);
-                    D.msgs.push_back(m);
-                }
+                for (int jb = g * per; jb < (g + 1) * per && jb * D.cbb < mbc; ++jb)
+                    deliver_cols(id, c, D.owner[c], jb * D.cbb, std::min(mbc, (jb + 1) * D.cbb));
                 close_step(id);
             }
         }
@@ -357,16 +408,9 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
             const i32 p = S.sn_parent[c];
             const int mbc = S.mb(c);
             if (p < 0 || mbc <= 0 || D.early[c]) continue;
-            const int dst = D.owner[p];
             for (int jb = 0; jb * D.cbb < mbc; ++jb) {
                 const int src = D.split[c] >= 0 ? D.cb_rank[D.split[c]][jb] : D.owner[c];
-                if (src == dst) continue;
-                DistMsg g {};
-                g.step = id;
-                g.src = src;
-                g.dst = dst;
-                cb_block(g, c, jb);
-                D.msgs.push_back(g);
+                deliver_cols(id, c, src, jb * D.cbb, std::min(mbc, (jb + 1) * D.cbb));
             }
         }
         close_step(id);

@@ -152,7 +152,6 @@ int64_t plan_rank_memory(const Symbolic& S, const DistPlan* D, int rank, RankMem
     R.panel_off.assign((size_t)ns, -1);
     R.cb_off.assign((size_t)ns, -1);
     R.land_off.assign((size_t)ns, -1);
-    R.blk_off.assign(D ? D->split_s.size() : 0, std::vector<int64_t>());
     auto owner = [&](i32 s) { return D ? D->owner[s] : 0; };
     R.panel_total = plan_rank_panels(S, D, rank, R.panel_off);
     std::vector<Req> reqs;
@@ -161,32 +160,23 @@ int64_t plan_rank_memory(const Symbolic& S, const DistPlan* D, int rank, RankMem
         const int64_t mb = S.mb(s);
         if (mb <= 0) continue;
         const i32 L = S.level[s], p = S.sn_parent[s], Lp = S.level[p];
-        const bool mine = owner(s) == rank, here = owner(p) == rank;
         const int64_t sq = mb * mb;
-        if (!D || D->split[s] < 0) {
-            if (mine)
-                req(sq, L, here ? Lp : L + 1, &R.cb_off[s]);
-            else if (here)
-                req(sq, L, Lp, &R.cb_off[s]);
+        if (!D) {
+            req(sq, L, Lp, &R.cb_off[s]);
             continue;
         }
-        const int sp = D->split[s];
-        const std::vector<i32>& cbr = D->cb_rank[sp];
-        bool cbrank = false;
-        for (i32 r : cbr) cbrank |= r == rank;
-        if (here)  // the parent's owner keeps the whole CB (its blocks computed in place)
+        // a full-square CB(s) wherever part of it is computed (until it is sent after
+        // level L) or received for the parent's assembly (until level Lp)
+        const bool prod = D->produces_cb(S, s, rank), recv = D->receives(S, s, rank);
+        if (recv)
             req(sq, L, Lp, &R.cb_off[s]);
-        else if (mine)  // assembled, then sent to the CB ranks (STEP_INIT)
+        else if (prod)
             req(sq, L, L + 1, &R.cb_off[s]);
-        else if (cbrank) {
-            R.blk_off[sp].assign(cbr.size(), -1);
-            for (size_t jb = 0; jb < cbr.size(); ++jb) {
-                if (cbr[jb] != rank) continue;
-                const int64_t rows = mb - (int64_t)jb * D->cbb, cols = std::min<int64_t>(D->cbb, rows);
-                req(rows * cols, L, L + 1, &R.blk_off[sp][jb]);
-            }
-        }
-        if (cbrank && D->pd[s] < 0) req(mb * S.w(s), L, L + 1, &R.land_off[s]);  // else its panel copy
+        bool cbrank = false;
+        if (D->split[s] >= 0)
+            for (i32 r : D->cb_rank[D->split[s]]) cbrank |= r == rank;
+        if (cbrank && D->pd[s] < 0 && owner(s) != rank)  // L21 slabs (a distributed panel: its copy)
+            req(mb * S.w(s), L, L + 1, &R.land_off[s]);
     }
     R.work_total = place(reqs, &R.work_live_max);
     if (placed)
@@ -214,7 +204,7 @@ int64_t plan_check(const Symbolic& S, int nranks) {
         for (i32 s = 0; s < S.ns; ++s) {
             if (R.cb_off[s] < 0 || S.mb(s) <= 0) continue;
             const i32 p = S.sn_parent[s];
-            if (nranks > 1 && D.owner[p] != r) continue;
+            if (nranks > 1 && !D.receives(S, s, r)) continue;
             auto it = t1_of.find({R.cb_off[s], S.level[s]});
             if (it == t1_of.end() || it->second < S.level[p]) ++bad;
         }
@@ -250,23 +240,14 @@ bool region_addr(const Symbolic& S, const DistPlan* D, const RankMem& R, int kin
             ld = S.mb(s);
             off = R.land_off[s] + (int64_t)col * ld + row;
             return true;
-        case R_CB: {
+        case R_CB:
+            if (R.cb_off[s] < 0) return false;
             arena = 1;
-            if (R.cb_off[s] >= 0) {
-                ld = S.mb(s);
-                off = R.cb_off[s] + (int64_t)col * ld + row;
-                return true;
-            }
-            if (!D || D->split[s] < 0) return false;
-            const std::vector<int64_t>& bo = R.blk_off[D->split[s]];
-            const int jb = col / D->cbb;
-            if (jb >= (int)bo.size() || bo[jb] < 0) return false;
-            const int r0 = jb * D->cbb;
-            ld = S.mb(s) - r0;
-            off = bo[jb] + (int64_t)(col - r0) * ld + (row - r0);
-            return row >= r0;
-        }
+            ld = S.mb(s);
+            off = R.cb_off[s] + (int64_t)col * ld + row;
+            return true;
     }
+    (void)D;
     return false;
 }
 

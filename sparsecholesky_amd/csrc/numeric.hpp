@@ -48,9 +48,9 @@ struct DistStep {
 // by kind, supernode and LOGICAL coordinates; every rank maps them to its own
 // physical layout, so sender and receiver may store a block differently.
 //   R_PANEL  the L panel of s: m x w, row = front row (owner only; permanent)
-//   R_CB     the contribution block of s: mb x mb, row/col = front row - w.  Held as a
-//            full square (ld = mb) or, on a rank computing only some of a split
-//            front's column blocks, as compact blocks (ld = rows of the block)
+//   R_CB     the contribution block of s: mb x mb, row/col = front row - w, held as a
+//            full square (ld = mb) on every rank that computes or receives part of it
+//            (only those parts are valid there)
 //   R_LAND   a split front's L21 (rows [w, m) of its panel) on a CB rank: mb x w
 enum RegionKind : int32_t { R_PANEL = 0, R_CB = 1, R_LAND = 2 };
 
@@ -85,6 +85,16 @@ struct DistPlan {
     // its first own slab after k, or w for a CB rank; m = not needed
     int need_row(const Symbolic& S, int32_t s, int k, int r) const;
     bool holds(int32_t s, int r) const;  // r keeps a panel copy of s (owner included)
+    // distributed assembly (dist_asm): a shared front with a distributed panel or a split
+    // CB is assembled where its columns live -- every rank assembles the panel slabs and
+    // CB column blocks it owns, and each child's CB columns go straight to the rank
+    // owning the parent columns they map into (no STEP_INIT)
+    std::vector<char> dasm;
+    int col_owner(const Symbolic& S, int32_t p, int col) const;  // rank assembling front column col of p
+    // rank r assembles a parent column that child c's CB maps into (holds CB(c) until then)
+    bool receives(const Symbolic& S, int32_t c, int r) const;
+    // rank r computes column blocks of s's CB (holds the full-square CB(s) from level(s))
+    bool produces_cb(const Symbolic& S, int32_t s, int r) const;
     // early delivery: a large, unsplit child whose parent runs on another rank has its
     // CB SYRK in column groups of early_gw, each group sent as soon as it is computed
     int early_gw = 4096;
@@ -105,7 +115,6 @@ struct RankMem {
     std::vector<int64_t> panel_off;  // per supernode: doubles into the panel arena, -1 = not here
     std::vector<int64_t> cb_off;     // per supernode: full-square CB in the work arena, -1
     std::vector<int64_t> land_off;   // per supernode: R_LAND slab (ld = mb) in the work arena, -1
-    std::vector<std::vector<int64_t>> blk_off;  // per split front, per column block: compact block, -1
     std::vector<int64_t> tall_off;   // per supernode: tall-mode scratch in the handle's tall pool, -1
     int64_t panel_total = 0;     // doubles (incl. the PNB tail the TRSM reads past)
     int64_t work_total = 0;      // doubles: high-water mark of the interval plan

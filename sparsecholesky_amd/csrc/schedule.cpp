@@ -407,13 +407,39 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
     auto is_early_sender = [&](int32_t s, int v) {
         return multi && D.early[s] && D.owner[s] == N.R[v].rank;
     };
+    auto is_dasm = [&](int32_t s) { return multi && D.dasm[s]; };
+    // distributed assembly: one write-once tile-assembly launch of the front columns of
+    // s that hosted rank v owns (its panel slabs and CB column blocks, D.col_owner), in
+    // 16-column blocks; a block straddling another rank's columns computes those too,
+    // into this rank's private copy, where nothing reads them
+    auto emit_region_asm = [&](int32_t lev, int32_t s, int v) {
+        const int who = N.R[v].rank, m = S.sn_m[s];
+        Launch L {};
+        L.kind = L_ASM;
+        L.level = lev;
+        L.vr = v;
+        L.big = 1;
+        L.off = (int64_t)asmv.size();
+        for (int cb = 0; cb * ASM_COLS < m; ++cb) {
+            bool mine = false;
+            for (int c = cb * ASM_COLS; c < std::min(m, (cb + 1) * ASM_COLS) && !mine; ++c)
+                mine = D.col_owner(S, s, c) == who;
+            if (!mine) continue;
+            for (int k = cb * ASM_COLS / ASM_ROWS; k * ASM_ROWS < m; ++k) asmv.push_back(make_int2(s, (k << 16) | cb));
+        }
+        L.count = (int32_t)((int64_t)asmv.size() - L.off);
+        if (L.count > 0) N.sched.push_back(L);
+    };
     // CB rank (hosted index v) of split front s: per final panel slab, CB -= L21_k
     // L21_k^T on the column blocks it owns (K = slab width), from its R_LAND copy
     auto emit_cb_rank = [&](int32_t lev, int32_t s, int v) {
         const int who = N.R[v].rank;
         const std::vector<int32_t>& cbr = D.cb_rank[D.split[s]];
         const int w = S.w(s), m = S.sn_m[s], mb = m - w;
-        emit_step(init_step[s]);
+        if (is_dasm(s))
+            emit_region_asm(lev, s, v);  // its own CB blocks, from the children's columns it received
+        else
+            emit_step(init_step[s]);
         for (int k0 = 0, k = 0; k0 < w; k0 += D.nbo, ++k) {
             const int k1 = std::min(w, k0 + D.nbo);
             emit_step(slab_step0[s] < 0 ? -1 : slab_step0[s] + k);
@@ -623,7 +649,9 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             for (int32_t s : large) {
                 const int m = S.sn_m[s];
                 if ((m >= tile_min_m || tallx(s)) != (tiled == 1)) continue;
-                const int ncol = gather(s) ? S.w(s) : m;  // assembled columns
+                // assembled columns (a distributed-assembly split front: its panel only,
+                // the CB ranks assemble their blocks)
+                const int ncol = (gather(s) || is_dasm(s)) ? S.w(s) : m;
                 for (int cb = 0; cb * ASM_COLS < ncol; ++cb) {
                     if (!tiled) {
                         asmv.push_back(make_int2(s, cb));
@@ -915,7 +943,9 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         auto slab_c0 = [&](int k) { return k * D.nbo; };
         auto slab_c1 = [&](int k) { return std::min(w, (k + 1) * D.nbo); };
         const int vo = hosted_of[own];
-        if (vo >= 0) {  // the owner assembles the whole front (tiled or column-streaming)
+        if (is_dasm(s)) {  // every holder assembles its own slabs and CB blocks
+            for (int v : vs) emit_region_asm(lev, s, v);
+        } else if (vo >= 0) {  // the owner assembles the whole front (tiled or column-streaming)
             const int tile_min_m = S.opt.asm_tile_min_m > 0 ? S.opt.asm_tile_min_m : ASM_TILE_MIN_M;
             Launch L {};
             L.kind = L_ASM;

@@ -67,7 +67,9 @@ def _worker(rank, world, port, k, opts, out):
                                           (4, 20, dict(panel_nb_outer=128, dist_cbb=64, small_front_max=32)),
                                           (3, 24, dict(dist_cbb=128)), (4, 20, dict(dist_split=0)),
                                           (8, 24, dict(panel_nb_outer=128, dist_cbb=64)),
-                                          (4, 20, dict(panel_nb_outer=128, dist_panel=0))])
+                                          (4, 20, dict(panel_nb_outer=128, dist_panel=0)),
+                                          (8, 24, dict(panel_nb_outer=128, dist_cbb=64, dist_asm=0)),
+                                          (3, 24, dict(dist_cbb=128, dist_asm=0))])
 def test_message_schedule_matches_across_ranks(world, k, opts):
     import random
 
@@ -78,6 +80,33 @@ def test_message_schedule_matches_across_ranks(world, k, opts):
     res = [out[r] for r in range(world)]
     assert all(ok for ok, _ in res), res
     assert res[0][1] > 0  # some contribution blocks do cross ranks
+
+
+@pytest.mark.parametrize("k,nranks,opts", [(128, 8, {}), (128, 4, {}), (24, 8, dict(panel_nb_outer=128, dist_cbb=64))])
+def test_distributed_assembly_plan(k, nranks, opts):
+    # dist_asm (default): no STEP_INIT (the owner no longer hands out assembled slabs and
+    # CB blocks); every child CB column still reaches exactly the rank that assembles the
+    # parent column it maps into, so the total volume drops by the INIT bytes and the
+    # DELIVER bytes grow by at most the rows above each run's first column
+    def volume(s):
+        st = s.dist_steps(nranks)
+        by_kind = np.zeros(3)
+        for r in range(nranks):
+            step, peer, nb, snd = s.dist_schedule(nranks, r)
+            for a, b in zip(step[snd == 1], nb[snd == 1]):
+                by_kind[st["kind"][a]] += b
+        return st, by_kind
+
+    s1 = sc.Symbolic(sc.laplacian3d(k), **opts)
+    s0 = sc.Symbolic(sc.laplacian3d(k), dist_asm=0, **opts)
+    st1, v1 = volume(s1)
+    st0, v0 = volume(s0)
+    assert (st1["kind"] != 0).all() and (st0["kind"] == 0).any()  # INIT gone
+    assert v1[0] == 0 and v0[0] > 0
+    assert v1[1] == v0[1]  # SLAB traffic unchanged
+    assert v1.sum() < v0.sum()
+    print(f"k={k} n={nranks}: INIT {v0[0] / 1e9:.2f} GB -> 0, DELIVER {v0[2] / 1e9:.2f} -> {v1[2] / 1e9:.2f} GB, "
+          f"total {v0.sum() / 1e9:.2f} -> {v1.sum() / 1e9:.2f} GB")
 
 
 @pytest.mark.parametrize("k,nranks", [(20, 4), (24, 8), (24, 3)])

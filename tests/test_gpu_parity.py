@@ -414,7 +414,8 @@ def test_lap48_full_parity(gpu, lap48_oracle, opts):
 
 @pytest.mark.parametrize("nranks,rccl,opts", [(2, False, {}), (4, False, {}), (8, False, {}), (2, True, {}),
                                                (4, True, {}), (8, True, {}), (8, False, dict(panel_tall=1)),
-                                               (8, False, dict(panel_tall=2)), (2, True, dict(panel_tall=2))])
+                                               (8, False, dict(panel_tall=2)), (2, True, dict(panel_tall=2)),
+                                               (8, False, dict(dist_asm=0)), (4, True, dict(dist_asm=0))])
 def test_partitioned_defaults_lap48(gpu, lap48_oracle, nranks, rccl, opts):
     # the distributed plan at the DEFAULT options the N-GPU bench runs (panel_nb_outer
     # 1024, dist_cbb 1024, small_front_max 128): the 2327-wide root factored 1D
@@ -621,7 +622,8 @@ def test_partitioned_schedule_bitwise_equal(gpu, nranks):
 @pytest.mark.parametrize("nranks,rccl,opts", [
     (2, False, {}), (3, False, {}), (4, False, {}), (8, False, {}), (2, True, {}), (4, True, {}), (8, True, {}),
     (4, False, dict(dist_panel=0)), (3, False, dict(dist_split=0)), (8, True, dict(dist_split=0)),
-    (4, False, dict(lookahead=0, inner_order=0))])
+    (4, False, dict(lookahead=0, inner_order=0)), (4, False, dict(dist_asm=0)), (8, True, dict(dist_asm=0)),
+    (3, False, dict(dist_panel=0, dist_asm=0))])
 def test_partitioned_split_fronts_emulated(gpu, nranks, rccl, opts):
     # split top fronts (CB column blocks updated per slab by the ranks of the group)
     # and distributed panels (slabs factored 1D slab-cyclic over the group, the root
