@@ -113,7 +113,8 @@ static int64_t bench_panel(int which, int M, int reps, double* out) {
 // on a low-priority stream -- and a "chain" of nchain dependent fused POTRF + TRSM
 // launches on a chain_rows x 64 front, on the high-priority stream.  mode bit 0: the hog
 // stream is CU-masked (every mask_stride-th CU off); bit 1: the hog is replayed from a
-// captured hipGraph; bit 2: the chain too (its own graph).  out[0] chain alone, out[1] hog
+// captured hipGraph; bit 2: the chain too (its own graph); bit 3: the hog is a resident
+// grid of mask_stride workgroups walking its tiles (no CU mask).  out[0] chain alone, out[1] hog
 // alone, out[2] chain under the hog (first chain start -> last chain end), out[3] hog
 // under the chain, out[4] both (wall), all ms; out[5] CUs the hog may use.
 int64_t debug_contention(int M, int K, int chain_rows, int nchain, int mode, int mask_stride, double* out) {
@@ -128,7 +129,7 @@ int64_t debug_contention(int M, int K, int chain_rows, int nchain, int mode, int
     const int ncu = prop.multiProcessorCount;
     int used = ncu;
     if (hipStreamCreateWithPriority(&s_chain, hipStreamNonBlocking, prio_hi) != hipSuccess) return SC_ERR_HIP;
-    if (mode & 1) {
+    if ((mode & 1) && !(mode & 8)) {
         std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
         used = 0;
         for (int c = 0; c < ncu; ++c)
@@ -156,9 +157,15 @@ int64_t debug_contention(int M, int K, int chain_rows, int nchain, int mode, int
     hipGraph_t g_hog = nullptr, g_chain = nullptr;
     hipGraphExec_t x_hog = nullptr, x_chain = nullptr;
     DevPlan P {};
+    const int resident = (mode & 8) ? mask_stride : 0;  // bit 3: the hog as a resident grid of this size
+    auto hog_direct = [&]() {
+        if (resident > 0)
+            return launch_syrk_resident((GemmTask*)bt, (int2*)bl, ntiles, SYRK_BT_LARGE, 0, s_hog, 0, nullptr, resident);
+        return launch_syrk((GemmTask*)bt, (int2*)bl, ntiles, SYRK_BT_LARGE, 0, s_hog);
+    };
     auto hog = [&]() {
         if (x_hog) return hipGraphLaunch(x_hog, s_hog);
-        return launch_syrk((GemmTask*)bt, (int2*)bl, ntiles, SYRK_BT_LARGE, 0, s_hog);
+        return hog_direct();
     };
     auto chain_direct = [&]() {
         hipError_t e = hipSuccess;
@@ -219,7 +226,7 @@ int64_t debug_contention(int M, int K, int chain_rows, int nchain, int mode, int
         (void)hipDeviceSynchronize();
         if (mode & 2) {  // the hog as a captured graph
             (void)hipStreamBeginCapture(s_hog, hipStreamCaptureModeThreadLocal);
-            (void)launch_syrk((GemmTask*)bt, (int2*)bl, ntiles, SYRK_BT_LARGE, 0, s_hog);
+            (void)hog_direct();
             (void)hipStreamEndCapture(s_hog, &g_hog);
             if (!g_hog || hipGraphInstantiate(&x_hog, g_hog, nullptr, nullptr, 0) != hipSuccess) rc = SC_ERR_HIP;
         }

@@ -1704,6 +1704,21 @@ __global__ __launch_bounds__(64 * WM * WN, LEAN ? (TAG ? 5 : 6) : 1) void syrk_m
     syrk_tile_body<BT, WM, WN, TAG, EPI, LEAN>(tasks, tiles, blockIdx.x, plans);
 }
 
+// Resident-grid instance: a grid smaller than the GPU's workgroup slots walks the tile
+// list with stride gridDim.x (a multiple of 8, so workgroup b keeps XCD b % 8's tiles).
+// Every workgroup is dispatched at once and nothing stays queued behind it: a queued
+// grid holds the dispatcher, and a small critical-path launch on another stream waits
+// for all of it (the contention probe); with slots left free, it does not.
+template <int BT, int WM, int WN, int TAG, int EPI>
+__global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_resident_kernel(const GemmTask* __restrict__ tasks,
+                                                                           const int2* __restrict__ tiles, int ntiles,
+                                                                           const DevPlan* __restrict__ plans) {
+    for (int b = blockIdx.x; b < ntiles; b += gridDim.x) {
+        if (b != (int)blockIdx.x) __syncthreads();  // the previous tile's LDS reads are done
+        syrk_tile_body<BT, WM, WN, TAG, EPI, 0>(tasks, tiles, b, plans);
+    }
+}
+
 // General products of the tall-TRSM-by-inverse panel mode (GemmTask, TAG 2):
 //   the tall solve    L21 = A21 X^T       (A21 staged out of place; X = inv(L11), ktri)
 //   the next slab's   C_out = C_in - L L^T (rows below its diagonal block to the staging
@@ -2003,6 +2018,31 @@ static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int b
         hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, EPI>), dim3(n), dim3(512), 0, st, tasks, tiles, plans);
     else
         hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG, EPI>), dim3(n), dim3(256), 0, st, tasks, tiles, plans);
+}
+
+hipError_t launch_syrk_resident(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag,
+                                hipStream_t st, int epi, const DevPlan* plans, int grid) {
+    if (total_tiles <= 0) return hipSuccess;
+    grid = std::max(8, std::min(grid, (total_tiles + 7) / 8 * 8));
+    const dim3 g(grid);
+#define SC_RES(BT_, WM_, WN_, TAG_, EPI_)                                                                          \
+    hipLaunchKernelGGL((syrk_mfma_resident_kernel<BT_, WM_, WN_, TAG_, EPI_>), g, dim3(64 * WM_ * WN_), 0, st, tasks, \
+                       tiles, total_tiles, plans)
+    if (bt == 128) {
+        if (tag) {
+            if (epi) SC_RES(128, 2, 4, 1, 1); else SC_RES(128, 2, 4, 1, 0);
+        } else {
+            if (epi) SC_RES(128, 2, 4, 0, 1); else SC_RES(128, 2, 4, 0, 0);
+        }
+    } else {
+        if (tag) {
+            if (epi) SC_RES(64, 2, 2, 1, 1); else SC_RES(64, 2, 2, 1, 0);
+        } else {
+            if (epi) SC_RES(64, 2, 2, 0, 1); else SC_RES(64, 2, 2, 0, 0);
+        }
+    }
+#undef SC_RES
+    return hipGetLastError();
 }
 
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,

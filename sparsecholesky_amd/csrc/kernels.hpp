@@ -238,6 +238,11 @@ constexpr int TALL_ROWS = 64;  // rows per tall-TRSM workgroup
 // tag 2: general products (GemmTask B / Cin / Ct / sign / lower / ktri)
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
                        int epi = 0, const DevPlan* plans = nullptr, bool lean = false);
+// the same SYRK as a resident grid of `grid` workgroups (a multiple of 8) walking the
+// tile list: dispatched at once, so a critical-path launch on another stream finds the
+// slots the grid leaves free instead of queueing behind it
+hipError_t launch_syrk_resident(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag,
+                                hipStream_t st, int epi, const DevPlan* plans, int grid);
 // full rectangle tiles (general products that are not lower trapezoids)
 void append_tiles_full(std::vector<int2>& out, int task, int M, int N, int bt, int G = 8);
 hipError_t launch_stamp(uint64_t* slot, hipStream_t st);
