@@ -117,6 +117,9 @@ typedef struct sc_options {
                                 assembled where its columns live (each rank its own slabs / CB blocks; child CB
                                 columns go straight to the rank owning the parent columns they map into, no
                                 assembled-front hand-out); 0: its owner assembles it and sends the pieces */
+    int32_t la_grid;         /* > 0: the lookahead stream's panel updates run as a resident grid of this many
+                                workgroups walking their tiles (dispatched at once, so the 64-column chain on the
+                                main stream finds the slots it leaves free); 0: one workgroup per tile */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

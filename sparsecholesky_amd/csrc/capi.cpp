@@ -95,6 +95,7 @@ void sc_default_options(sc_options* opt) {
     opt->cb_tail_split = 1;
     opt->tiny_dense = 1;
     opt->dist_asm = 1;
+    opt->la_grid = 0;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,

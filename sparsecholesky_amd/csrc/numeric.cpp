@@ -307,6 +307,9 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
                                      L.epi);
         case L_PANEL:
         case L_CB:
+            if (L.res > 0)
+                return launch_syrk_resident(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0,
+                                            st, L.epi, N.d_plans, L.res);
             return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st, L.epi,
                                N.d_plans, L.lean != 0);
         case L_COMM:

@@ -167,6 +167,7 @@ struct Launch {
     int32_t bt;       // SYRK tile edge (64 or 128)
     int32_t epi;      // SYRK epilogue with its C loads batched (short-K and critical-path launches)
     int32_t lean;     // SYRK on 64 x 64 tiles with half the LDS (deepest K <= syrk_lean_kmax)
+    int32_t res;      // > 0: SYRK as a resident grid of this many workgroups (launch_syrk_resident)
     int32_t strm;     // 0 = main stream, 1 = lookahead stream, 2 = comm stream
     int32_t vr;       // hosted rank whose DevPlan the kernel uses
     double flops;     // algorithmic SYRK flops (CB launches: mb*(mb+1)*w)

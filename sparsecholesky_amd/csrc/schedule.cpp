@@ -219,6 +219,11 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // more to the lean instance's smaller gather batches than they gain in occupancy)
         L.lean = L.bt == SYRK_BT_SMALL && S.opt.syrk_lean_kmax > 0 && maxK <= S.opt.syrk_lean_kmax &&
                  (kind == L_PANEL || maxK > 64);
+        // lookahead-stream updates as a resident grid (la_grid): all its workgroups are
+        // dispatched at once, so the chain's launches on the main stream are not queued
+        // behind the rest of the grid
+        L.res = (kind == L_PANEL && strm == 1 && S.opt.la_grid > 0) ? S.opt.la_grid : 0;
+        if (L.res) L.lean = 0;
         if (kind == L_GEMM) {  // general products: tile by the smaller output edge
             int minMN = INT32_MAX;
             for (auto& t : tasks) minMN = std::min(minMN, std::min((int)t.M, (int)t.N));
