@@ -108,8 +108,12 @@ __global__ __launch_bounds__(256) void assemble_cols_kernel(DevPlan P, const int
 // entries for a wave's columns (<= 4 columns x 256 rows) are loaded with all
 // loads in flight before the adds (the kernel is latency-bound otherwise).
 constexpr int ASM_CCH = 32;  // children staged per prologue
+// lim (distributed assembly, or null): per task the front columns [x, y) this rank
+// assembles; the tile's other columns are neither gathered nor stored (their children's
+// columns went to another rank, and this rank may hold no copy of them)
 __global__ __launch_bounds__(256) void assemble_tile_kernel(DevPlan P, const int2* __restrict__ tasks,
-                                                             const double* __restrict__ Ax) {
+                                                             const double* __restrict__ Ax,
+                                                             const int2* __restrict__ lim) {
     __shared__ double T[ASM_COLS * ASM_ROWS];  // T[(j - j0) * ASM_ROWS + (r - r0)]
     __shared__ const double* s_src[ASM_CCH];
     __shared__ const int32_t* s_rel[ASM_CCH];
@@ -128,6 +132,7 @@ __global__ __launch_bounds__(256) void assemble_tile_kernel(DevPlan P, const int
     const int j0 = jb * ASM_COLS;
     const int j1 = min(m, j0 + ASM_COLS);
     const int r0 = k * ASM_ROWS, r1 = min(m, r0 + ASM_ROWS);
+    const int2 cl = lim ? lim[blockIdx.x] : make_int2(0, m);  // owned front columns
     double* panel = P.panel_pool + P.panel_off[s];
     double* cbs = P.cb_pool + P.cb_off[s];
     const int cp0 = P.child_ptr[s], cp1 = P.child_ptr[s + 1];
@@ -156,7 +161,10 @@ __global__ __launch_bounds__(256) void assemble_tile_kernel(DevPlan P, const int
             const int jlo = bnd_at(cbnd, jb, mbc), jhi = bnd_at(cbnd, jb + 1, mbc);
             int pj[ASM_COLS];
 #pragma unroll
-            for (int l = 0; l < ASM_COLS; ++l) pj[l] = (jlo + l < jhi && ilo < ihi) ? rel[jlo + l] - j0 : -1;
+            for (int l = 0; l < ASM_COLS; ++l) {
+                const int pc = (jlo + l < jhi && ilo < ihi) ? rel[jlo + l] : -1;
+                pj[l] = (pc >= cl.x && pc < cl.y) ? pc - j0 : -1;
+            }
 #pragma unroll
             for (int l = 0; l < ASM_COLS; ++l) s_pj[tid][l] = (int8_t)pj[l];
             s_src[tid] = P.cb_pool + P.cb_off[c];
@@ -210,6 +218,7 @@ __global__ __launch_bounds__(256) void assemble_tile_kernel(DevPlan P, const int
     const int64_t toff = P.tall_off ? P.tall_off[s] : -1;
     const int tnb = toff >= 0 ? min(w, P.tall_nbo) : 0;
     for (int j = j0 + wid; j < j1; j += 4) {
+        if (j < cl.x || j >= cl.y) continue;
         double* col = (j < w) ? panel + (int64_t)j * m : cbs + (int64_t)(j - w) * mb - w;
         const double* Tc = T + (j - j0) * ASM_ROWS - r0;
         if (j < tnb) {
@@ -1788,61 +1797,69 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mfma_kernel(const GemmTask*
 // solving e_j L_qq^-T (the generated TRSM code, as solve_inv_kernel) -- column j of
 // inv(L_qq).  The rest of block column q of X (rows above the block; the doubling steps
 // fill the rows below) and block row q of XT are zeroed, so the dense X is exact.
-__global__ __launch_bounds__(64) void xinv64_kernel(DevPlan P, const XinvTask* __restrict__ tasks) {
+// Wave 0 solves; waves 1-3 write the zeros meanwhile (up to 2 x 1024 x 64 doubles per
+// block: one wave alone took 0.27 ms per launch at 128^3 level 17).
+__global__ __launch_bounds__(256) void xinv64_kernel(DevPlan P, const XinvTask* __restrict__ tasks) {
     __shared__ double2 S[TRSM64_STREAM / 2];
     __shared__ double Lc[PNB * (PNB + 2)];
     __shared__ double invd[PNB];
     const XinvTask t = tasks[blockIdx.x];
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int m = P.sn_m[t.s];
     const int k0 = t.c0 + PNB * t.q;               // front column of the block
     const int nb = min(PNB, t.nbs - PNB * t.q);    // > 0
+    const int b0 = PNB * t.q;
     const double* blk = P.panel_pool + P.panel_off[t.s] + (int64_t)k0 * m + k0;
     double r[PNB];
+    if (wid == 0) {
 #pragma unroll
-    for (int j = 0; j < PNB; ++j) r[j] = (j < nb && lane < nb && lane >= j) ? blk[(int64_t)j * m + lane] : 0.0;
-    if (nb == PNB) {
-        double* Sd = reinterpret_cast<double*>(S);
+        for (int j = 0; j < PNB; ++j) r[j] = (j < nb && lane < nb && lane >= j) ? blk[(int64_t)j * m + lane] : 0.0;
+        if (nb == PNB) {
+            double* Sd = reinterpret_cast<double*>(S);
 #pragma unroll
-        for (int j = 0; j < PNB; ++j)
-            if (lane >= j) Sd[PNB * j - j * (j - 1) / 2 + (lane - j)] = lane == j ? 1.0 / r[j] : r[j];
-    } else {
-        constexpr int LD = PNB + 2;
+            for (int j = 0; j < PNB; ++j)
+                if (lane >= j) Sd[PNB * j - j * (j - 1) / 2 + (lane - j)] = lane == j ? 1.0 / r[j] : r[j];
+        } else {
+            constexpr int LD = PNB + 2;
 #pragma unroll
-        for (int j = 0; j < PNB; ++j) {
-            Lc[j * LD + lane] = r[j];
-            if (lane == j) invd[j] = j < nb ? 1.0 / r[j] : 0.0;
+            for (int j = 0; j < PNB; ++j) {
+                Lc[j * LD + lane] = r[j];
+                if (lane == j) invd[j] = j < nb ? 1.0 / r[j] : 0.0;
+            }
         }
     }
     __syncthreads();
+    if (wid == 0) {
 #pragma unroll
-    for (int c = 0; c < PNB; ++c) r[c] = c == lane ? 1.0 : 0.0;
-    if (nb == PNB)
-        trsm64_full(r, S);
-    else
-        trsm_steps<0>(r, Lc, invd, nb);
-    // r[c] = inv(L_qq)(c, lane) = X(b0 + c, b0 + lane) = XT(b0 + lane, b0 + c)
-    const int b0 = PNB * t.q;
+        for (int c = 0; c < PNB; ++c) r[c] = c == lane ? 1.0 : 0.0;
+        if (nb == PNB)
+            trsm64_full(r, S);
+        else
+            trsm_steps<0>(r, Lc, invd, nb);
+        // r[c] = inv(L_qq)(c, lane) = X(b0 + c, b0 + lane) = XT(b0 + lane, b0 + c)
 #pragma unroll
-    for (int c = 0; c < PNB; ++c)
-        if (c < nb && lane < nb) {
-            const double x = c >= lane ? r[c] : 0.0;
-            t.X[b0 + c + (int64_t)(b0 + lane) * t.ldx] = x;
-            t.XT[b0 + lane + (int64_t)(b0 + c) * t.ldx] = x;  // coalesced across lanes
+        for (int c = 0; c < PNB; ++c)
+            if (c < nb && lane < nb) {
+                const double x = c >= lane ? r[c] : 0.0;
+                t.X[b0 + c + (int64_t)(b0 + lane) * t.ldx] = x;
+                t.XT[b0 + lane + (int64_t)(b0 + c) * t.ldx] = x;  // coalesced across lanes
+            }
+    } else {
+        // zeros, threads along rows (coalesced): X above the block in its block column
+        // (X is lower triangular) and XT below the block in its block column (XT upper)
+        const int z = tid - 64;
+        for (int c = 0; c < nb; ++c) {
+            double* xc = t.X + (int64_t)(b0 + c) * t.ldx;
+            for (int i = z; i < b0; i += 192) xc[i] = 0.0;
+            double* tc = t.XT + (int64_t)(b0 + c) * t.ldx;
+            for (int i = b0 + PNB + z; i < t.nbs; i += 192) tc[i] = 0.0;
         }
-    // zeros, lanes along rows (coalesced): X above the block in its block column (X is
-    // lower triangular) and XT below the block in its block column (XT upper)
-    for (int c = 0; c < nb; ++c) {
-        double* xc = t.X + (int64_t)(b0 + c) * t.ldx;
-        for (int i = lane; i < b0; i += 64) xc[i] = 0.0;
-        double* tc = t.XT + (int64_t)(b0 + c) * t.ldx;
-        for (int i = b0 + PNB + lane; i < t.nbs; i += 64) tc[i] = 0.0;
     }
 }
 
 hipError_t launch_xinv64(const DevPlan& P, const XinvTask* tasks, int count, hipStream_t st) {
     if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(xinv64_kernel, dim3(count), dim3(64), 0, st, P, tasks);
+    hipLaunchKernelGGL(xinv64_kernel, dim3(count), dim3(256), 0, st, P, tasks);
     return hipGetLastError();
 }
 
@@ -1977,10 +1994,10 @@ hipError_t launch_front_chain(const DevPlan& P, const ChainPlan& C, int first, i
 }
 
 hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count, const double* Ax,
-                                 hipStream_t st, bool tiled) {
+                                 hipStream_t st, bool tiled, const int2* lim) {
     if (count <= 0) return hipSuccess;
     if (tiled)
-        hipLaunchKernelGGL(assemble_tile_kernel, dim3(count), dim3(256), 0, st, P, tasks, Ax);
+        hipLaunchKernelGGL(assemble_tile_kernel, dim3(count), dim3(256), 0, st, P, tasks, Ax, lim);
     else
         hipLaunchKernelGGL(assemble_cols_kernel, dim3(count), dim3(256), 0, st, P, tasks, Ax);
     return hipGetLastError();

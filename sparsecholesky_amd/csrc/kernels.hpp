@@ -205,9 +205,10 @@ hipError_t launch_tiny_dense(const DevPlan& P, const TinyPlan& T, int n, const d
 hipError_t launch_front_chain(const DevPlan& P, const ChainPlan& C, int first, int count, int maxm,
                               const double* Ax, hipStream_t st);
 // tiled: tasks are (front, (row tile << 16) | 16-column block) for the write-once
-// tile kernel (fronts with m >= ASM_TILE_MIN_M), else (front, column block)
+// tile kernel (fronts with m >= ASM_TILE_MIN_M), else (front, column block); lim (tiled
+// only, may be null): per task the front columns [x, y) to assemble (distributed assembly)
 hipError_t launch_assemble_large(const DevPlan& P, const int2* tasks, int count, const double* Ax,
-                                 hipStream_t st, bool tiled);
+                                 hipStream_t st, bool tiled, const int2* lim = nullptr);
 // Large-front panel kernels (generated straight-line code, panel_gen.inc): the
 // 64 x 64 diagonal POTRF (one wave per block) and the TRSM of the rows below it
 // (TRSM_ROWS rows per task).  partial: every task is a partial last block (nb < 64).

@@ -271,7 +271,8 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
             N.TP.host_info = (int32_t*)dp;
         }
     }
-    if ((rc = upload(N, B.small, N.d_small)) || (rc = upload(N, B.asmv, N.d_asm)) ||
+    B.asml.resize(B.asmv.size(), make_int2(0, INT32_MAX));
+    if ((rc = upload(N, B.small, N.d_small)) || (rc = upload(N, B.asmv, N.d_asm)) || (rc = upload(N, B.asml, N.d_asml)) ||
         (rc = upload(N, B.potrf, N.d_potrf)) || (rc = upload(N, B.trsm, N.d_trsm)) ||
         (rc = upload(N, B.inv, N.d_inv)) || (rc = upload(N, B.tall, N.d_tall)) || (rc = upload(N, B.xinv, N.d_xinv)) ||
         (rc = upload(N, std::vector<int32_t>(B.trsm.size() + 1, 0), N.d_arrive)) ||
@@ -299,7 +300,9 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
             if (L.big == 3) return launch_tiny_dense(N.R[L.vr].P, N.TP, L.maxm, d_Ax, N.stream);
             return launch_front_small(N.R[L.vr].P, N.d_small + L.off, L.count, L.maxm, false, d_Ax, N.stream);
         case L_ASM:
-            return launch_assemble_large(N.R[L.vr].P, N.d_asm + L.off, L.count, d_Ax, N.stream, L.big != 0);
+            // epi = 1: distributed-assembly launch, column limits parallel to the tasks
+            return launch_assemble_large(N.R[L.vr].P, N.d_asm + L.off, L.count, d_Ax, N.stream, L.big != 0,
+                                         L.epi ? N.d_asml + L.off : nullptr);
         case L_POTRF:
             return launch_potrf_diag(N.R[L.vr].P, N.d_potrf + L.off, L.count, N.stream);
         case L_TRSM:

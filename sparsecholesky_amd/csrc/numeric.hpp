@@ -197,6 +197,7 @@ struct Numeric {
     TinyPlan TP {};                  // tiny trees: the whole factorization in one workgroup
     int64_t n_chain = 0;             // chained fronts (descriptors)
     int2* d_asm = nullptr;
+    int2* d_asml = nullptr;  // per assembly task: owned front columns (distributed-assembly launches)
     int2* d_potrf = nullptr;
     TrsmTask* d_trsm = nullptr;
     int2* d_inv = nullptr;   // L_INV tasks (s, k0)

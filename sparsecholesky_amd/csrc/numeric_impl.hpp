@@ -83,6 +83,7 @@ struct SchedBuild {
     int32_t tiny_lds = 0;
     std::vector<int32_t> small;
     std::vector<int2> asmv, potrf, inv;
+    std::vector<int2> asml;  // parallel to asmv: owned front columns [x, y) of a task
     std::vector<TrsmTask> trsm;
     std::vector<int4> tall;
     std::vector<XinvTask> xinv;

@@ -424,13 +424,24 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         L.level = lev;
         L.vr = v;
         L.big = 1;
+        L.epi = 1;  // the tasks carry column limits (B.asml)
         L.off = (int64_t)asmv.size();
         for (int cb = 0; cb * ASM_COLS < m; ++cb) {
-            bool mine = false;
-            for (int c = cb * ASM_COLS; c < std::min(m, (cb + 1) * ASM_COLS) && !mine; ++c)
-                mine = D.col_owner(S, s, c) == who;
-            if (!mine) continue;
-            for (int k = cb * ASM_COLS / ASM_ROWS; k * ASM_ROWS < m; ++k) asmv.push_back(make_int2(s, (k << 16) | cb));
+            const int c1 = std::min(m, (cb + 1) * ASM_COLS);
+            for (int a = cb * ASM_COLS; a < c1;) {  // each run of owned columns of the block
+                if (D.col_owner(S, s, a) != who) {
+                    ++a;
+                    continue;
+                }
+                int b = a + 1;
+                while (b < c1 && D.col_owner(S, s, b) == who) ++b;
+                for (int k = cb * ASM_COLS / ASM_ROWS; k * ASM_ROWS < m; ++k) {
+                    asmv.push_back(make_int2(s, (k << 16) | cb));
+                    B.asml.resize(asmv.size(), make_int2(0, INT32_MAX));
+                    B.asml.back() = make_int2(a, b);
+                }
+                a = b;
+            }
         }
         L.count = (int32_t)((int64_t)asmv.size() - L.off);
         if (L.count > 0) N.sched.push_back(L);
@@ -653,10 +664,8 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             L.off = (int64_t)asmv.size();
             for (int32_t s : large) {
                 const int m = S.sn_m[s];
-                if ((m >= tile_min_m || tallx(s)) != (tiled == 1)) continue;
-                // assembled columns (a distributed-assembly split front: its panel only,
-                // the CB ranks assemble their blocks)
-                const int ncol = (gather(s) || is_dasm(s)) ? S.w(s) : m;
+                if ((m >= tile_min_m || tallx(s)) != (tiled == 1) || is_dasm(s)) continue;
+                const int ncol = gather(s) ? S.w(s) : m;  // assembled columns
                 for (int cb = 0; cb * ASM_COLS < ncol; ++cb) {
                     if (!tiled) {
                         asmv.push_back(make_int2(s, cb));
@@ -669,6 +678,10 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             L.count = (int32_t)((int64_t)asmv.size() - L.off);
             if (L.count > 0) N.sched.push_back(L);
         }
+        // distributed assembly of a split front: the owner assembles its panel columns,
+        // the CB ranks their blocks (emit_cb_rank)
+        for (int32_t s : large)
+            if (is_dasm(s)) emit_region_asm(lev, s, v);
         for (int32_t s : large)
             if (is_split(s)) emit_step(init_step[s]);
         int maxw = 0;
