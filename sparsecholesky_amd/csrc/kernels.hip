@@ -217,13 +217,14 @@ __global__ __launch_bounds__(256) void assemble_tile_kernel(DevPlan P, const int
     // reads them from there and writes the final L21 into the panel.
     const int64_t toff = P.tall_off ? P.tall_off[s] : -1;
     const int tnb = toff >= 0 ? min(w, P.tall_nbo) : 0;
+    const int trow = tnb + (toff >= 0 ? P.tall_skip : 0);  // first staged row (ld m - trow)
     for (int j = j0 + wid; j < j1; j += 4) {
         if (j < cl.x || j >= cl.y) continue;
         double* col = (j < w) ? panel + (int64_t)j * m : cbs + (int64_t)(j - w) * mb - w;
         const double* Tc = T + (j - j0) * ASM_ROWS - r0;
         if (j < tnb) {
-            double* tcol = P.tall_pool + toff + (int64_t)j * (m - tnb) - tnb;
-            for (int r = max(r0, j) + lane; r < r1; r += 64) (r < tnb ? col : tcol)[r] = Tc[r];
+            double* tcol = P.tall_pool + toff + (int64_t)j * (m - trow) - trow;
+            for (int r = max(r0, j) + lane; r < r1; r += 64) (r < trow ? col : tcol)[r] = Tc[r];
         } else {
             for (int r = max(r0, j) + lane; r < r1; r += 64) col[r] = Tc[r];
         }
@@ -1737,12 +1738,12 @@ __global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_resident_kernel(const 
 // Same K loop as the SYRK (B from its own matrix); the epilogue reads Cin (if any) for a
 // whole two-MFMA-row chunk before its stores (Cin never aliases C or Ct here).
 template <int BT, int WM, int WN>
-__global__ __launch_bounds__(64 * WM * WN) void gemm_mfma_kernel(const GemmTask* __restrict__ tasks,
-                                                                  const int2* __restrict__ tiles) {
+__device__ __forceinline__ void gemm_tile_body(const GemmTask* __restrict__ tasks, const int2* __restrict__ tiles,
+                                               int bidx) {
     constexpr int BK = 16, LDT = BT + 16;
     constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
     __shared__ double smem[2 * 2 * BK * LDT];
-    const int2 tl = tiles[blockIdx.x];
+    const int2 tl = tiles[bidx];
     const GemmTask T = tasks[tl.x];
     const int ti = tl.y >> 16, tj = tl.y & 0xffff;
     const int row0 = ti * BT, col0 = tj * BT;
@@ -1789,6 +1790,22 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_mfma_kernel(const GemmTask*
                     if (C) C[gi + (int64_t)gj * T.ldc] = x;
                     if (Ct) Ct[gj + (int64_t)gi * T.ldt] = x;
                 }
+    }
+}
+
+template <int BT, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_mfma_kernel(const GemmTask* __restrict__ tasks,
+                                                                  const int2* __restrict__ tiles) {
+    gemm_tile_body<BT, WM, WN>(tasks, tiles, blockIdx.x);
+}
+
+// resident-grid instance (see syrk_mfma_resident_kernel)
+template <int BT, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_mfma_resident_kernel(const GemmTask* __restrict__ tasks,
+                                                                           const int2* __restrict__ tiles, int ntiles) {
+    for (int b = blockIdx.x; b < ntiles; b += gridDim.x) {
+        if (b != (int)blockIdx.x) __syncthreads();
+        gemm_tile_body<BT, WM, WN>(tasks, tiles, b);
     }
 }
 
@@ -2042,6 +2059,13 @@ hipError_t launch_syrk_resident(const GemmTask* tasks, const int2* tiles, int to
     if (total_tiles <= 0) return hipSuccess;
     grid = std::max(8, std::min(grid, (total_tiles + 7) / 8 * 8));
     const dim3 g(grid);
+    if (tag == 2) {
+        if (bt == 128)
+            hipLaunchKernelGGL((gemm_mfma_resident_kernel<128, 2, 4>), g, dim3(512), 0, st, tasks, tiles, total_tiles);
+        else
+            hipLaunchKernelGGL((gemm_mfma_resident_kernel<64, 2, 2>), g, dim3(256), 0, st, tasks, tiles, total_tiles);
+        return hipGetLastError();
+    }
 #define SC_RES(BT_, WM_, WN_, TAG_, EPI_)                                                                          \
     hipLaunchKernelGGL((syrk_mfma_resident_kernel<BT_, WM_, WN_, TAG_, EPI_>), g, dim3(64 * WM_ * WN_), 0, st, tasks, \
                        tiles, total_tiles, plans)

@@ -57,6 +57,7 @@ struct DevPlan {
     const int64_t* tall_off;
     double* tall_pool;
     int32_t tall_nbo;
+    int32_t tall_skip;  // rows right below the first slab that stay in the panel (panel_tall = 3)
 };
 
 // One lower-trapezoid SYRK update: C[i,j] -= sum_k A[i,k] A[j,k], j < N, j <= i < M.

@@ -202,6 +202,7 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
                 R.P.tall_off = dp;
                 R.P.tall_pool = (double*)p;
                 R.P.tall_nbo = std::max(PNB, (S.opt.panel_nb_outer / PNB) * PNB);
+                R.P.tall_skip = S.opt.panel_tall == 3 ? R.P.tall_nbo : 0;
             }
         }
     }
@@ -324,6 +325,8 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
         case L_XINV:
             return launch_xinv64(N.R[L.vr].P, N.d_xinv + L.off, L.count, st);
         case L_GEMM:
+            if (L.res > 0) return launch_syrk_resident(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, 2, st, 0,
+                                                       nullptr, L.res);
             return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, 2, st);
     }
     return hipErrorInvalidValue;

@@ -101,11 +101,14 @@ int64_t build_schedule(Numeric& N, SchedBuild& B);
 // forms X = inv(L11) (64-block inverses, then log2 doubling products), and solves the
 // rows below the slab as one MFMA product L21 = A21 X^T, A21 staged out of place.  Per
 // front, in the handle's tall pool (doubles, 64-aligned pieces):
-//   S   (m - nbs0) x nbs0, ld m - nbs0: the current slab's rows below its diagonal block
+//   S   (m - nbs0 - skip) x nbs0, ld m - nbs0 - skip: the current slab's rows below its
+//       diagonal block (panel_tall = 3: below its near rows)
 //   X, XT  nbs0 x nbs0, ld nbs0: inv(L11) and its transpose
 //   U   nbs0 x nbs0: the doubling steps' intermediate products (transposed)
 struct TallLayout {
     int32_t nbs0 = 0;     // first slab width = min(w, NBO)
+    int32_t skip = 0;     // panel_tall = 3: the NBO "near" rows below each slab stay in the panel (S holds
+                          // the rows from slab end + skip on)
     int64_t lds = 0;      // ld of S
     int64_t x = 0, xt = 0, u = 0, total = 0;  // offsets from the front's base, size
 };

@@ -34,7 +34,8 @@ TallLayout tall_layout(const Symbolic& S, int32_t s, int nbo) {
     TallLayout T;
     const int w = S.w(s), m = S.sn_m[s];
     T.nbs0 = std::min(w, nbo);
-    T.lds = std::max<int64_t>(1, m - T.nbs0);
+    T.skip = S.opt.panel_tall == 3 ? nbo : 0;  // near rows solved in place on the main stream
+    T.lds = std::max<int64_t>(1, m - T.nbs0 - T.skip);
     const int64_t nn = (int64_t)T.nbs0 * T.nbs0;
     T.x = al64(T.lds * T.nbs0);
     T.xt = T.x + al64(nn);
@@ -44,8 +45,11 @@ TallLayout tall_layout(const Symbolic& S, int32_t s, int nbo) {
 }
 
 bool tallx_front(const Symbolic& S, const DistPlan* D, int rank, int32_t s) {
-    if (S.opt.panel_tall != 2 || S.fclass[s] != FRONT_LARGE) return false;
+    if ((S.opt.panel_tall != 2 && S.opt.panel_tall != 3) || S.fclass[s] != FRONT_LARGE) return false;
     if (D && (D->owner[s] != rank || D->pd[s] >= 0)) return false;
+    // panel_tall = 3 solves the far rows on the lookahead stream: a split front sends its
+    // final slabs from the main stream's point of view (STEP_SLAB): it keeps the default path
+    if (D && S.opt.panel_tall == 3 && D->split[s] >= 0) return false;
     const int w = S.w(s), m = S.sn_m[s];
     return w >= 2 * PNB && m > std::min(w, nbo_of(S));
 }
@@ -222,7 +226,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // lookahead-stream updates as a resident grid (la_grid): all its workgroups are
         // dispatched at once, so the chain's launches on the main stream are not queued
         // behind the rest of the grid
-        L.res = (kind == L_PANEL && strm == 1 && S.opt.la_grid > 0) ? S.opt.la_grid : 0;
+        L.res = ((kind == L_PANEL || kind == L_GEMM) && strm == 1 && S.opt.la_grid > 0) ? S.opt.la_grid : 0;
         if (L.res) L.lean = 0;
         if (kind == L_GEMM) {  // general products: tile by the smaller output edge
             int minMN = INT32_MAX;
@@ -511,10 +515,12 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
     //      products (U^T = (B Xa)^T, then E and E^T)
     //   3. the tall solve L21 = A21 X^T (K trimmed to the triangle), A21 from the staging
     //      buffer, L21 written into the panel
-    auto emit_tallx = [&](int32_t lev, int v, const std::vector<int2>& tx) {
+    //   (panel_tall = 3: on stream strm, and the tall solve covers only the rows from
+    //   slab end + skip on -- the near rows were solved in place on the main stream)
+    auto emit_tallx = [&](int32_t lev, int v, const std::vector<int2>& tx, int strm) {
         const RankMem& R = N.R[v];
         struct F {
-            int32_t s, c0, nbs, m;
+            int32_t s, c0, nbs, m, skip;
             double *pan, *base, *X, *XT, *U;
             int64_t ldx, lds;
         };
@@ -534,6 +540,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             f.U = f.base + TL.u;
             f.ldx = TL.nbs0;
             f.lds = TL.lds;
+            f.skip = TL.skip;
             fr.push_back(f);
             maxnb = std::max(maxnb, f.nbs);
         }
@@ -541,6 +548,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         Lx.kind = L_XINV;
         Lx.level = lev;
         Lx.vr = v;
+        Lx.strm = strm;
         Lx.off = (int64_t)B.xinv.size();
         for (const F& f : fr)
             for (int q = 0; q * PNB < f.nbs; ++q)
@@ -584,30 +592,30 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     et.push_back(q);
                     fe += 2.0 * valid * (double)b * valid;
                 }
-            push_gemm_launch(L_GEMM, lev, ut, 0, fu);
-            push_gemm_launch(L_GEMM, lev, et, 0, fe);
+            push_gemm_launch(L_GEMM, lev, ut, 0, fu, strm);
+            push_gemm_launch(L_GEMM, lev, et, 0, fe, strm);
         }
         std::vector<GemmTask> tt;
         double ft = 0.0;
         for (const F& f : fr) {
-            const int c1 = f.c0 + f.nbs;
-            if (f.m <= c1) continue;
+            const int r0 = f.c0 + f.nbs + f.skip;  // first row of the tall solve
+            if (f.m <= r0) continue;
             GemmTask t {};
-            t.A = f.base;  // S: rows [c1, m) of the slab's columns
+            t.A = f.base;  // S: rows [r0, m) of the slab's columns
             t.lda = f.lds;
             t.B = f.X;
             t.ldb = f.ldx;
-            t.M = f.m - c1;
+            t.M = f.m - r0;
             t.N = f.nbs;
             t.K = f.nbs;
-            t.C = f.pan + (int64_t)f.c0 * f.m + c1;
+            t.C = f.pan + (int64_t)f.c0 * f.m + r0;
             t.ldc = f.m;
             t.sign = 1.0;
             t.ktri = 1;
             tt.push_back(t);
-            ft += (double)(f.m - c1) * f.nbs * (double)f.nbs;
+            ft += (double)(f.m - r0) * f.nbs * (double)f.nbs;
         }
-        push_gemm_launch(L_GEMM, lev, tt, 0, ft);
+        push_gemm_launch(L_GEMM, lev, tt, 0, ft, strm);
     };
     // one level's fronts of hosted rank v
     auto emit_level = [&](int32_t lev, const std::vector<int32_t>& nodes, int v) {
@@ -718,6 +726,8 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // that step is dropped, one dispatch fewer on the chain per two steps
         std::vector<char> pre_next((size_t)S.ns, 0);
         auto fold = [&](int32_t s) { return S.opt.trsm_fold && S.opt.inner_order == 1 && !tall(s); };
+        const bool tall3 = S.opt.panel_tall == 3;
+        int a3_ev = -1, b3_ev = -1;  // lookahead-stream events of the last slab end (panel_tall = 3)
         for (int k0 = 0; k0 < maxw; k0 += PNB) {
             Launch Lp {};
             Lp.kind = L_POTRF;
@@ -749,7 +759,8 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             std::vector<int4> tall_t;          // ... and the tall TRSM of the rows below
             std::vector<int2> tx;              // tall-by-inverse fronts at a slab end: (s, slab0)
             std::vector<GemmTask> outer_a2;    // ... their next-slab updates (general products)
-            double uflops = 0.0, afl = 0.0, bfl = 0.0;
+            std::vector<GemmTask> d3, a3, b3;  // panel_tall = 3: next diagonal block, next slab, the rest
+            double uflops = 0.0, afl = 0.0, bfl = 0.0, d3fl = 0.0, a3fl = 0.0, b3fl = 0.0;
             for (int32_t s : large) {
                 const int w = S.w(s), m = S.sn_m[s];
                 if (w <= k0) continue;
@@ -789,6 +800,34 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 if (k1 == slab1 && tall(s) && !tallx(s)) {
                     for (int kb = slab0; kb < slab1; kb += PNB) inv_t.push_back(make_int2(s, kb));
                     for (int r0 = slab1; r0 < m; r0 += TALL_ROWS) tall_t.push_back(make_int4(s, slab0, r0, slab1));
+                }
+                if (k1 == slab1 && tallx(s) && tall3) {
+                    // panel_tall = 3 (see below): the near rows [slab1, slab1 + NBO) on the main
+                    // stream by the row-blocked tall TRSM; X, the far rows and the updates on
+                    // the lookahead stream
+                    const int ne = std::min(m, slab1 + NBO);
+                    for (int kb = slab0; kb < slab1 && ne > slab1; kb += PNB) inv_t.push_back(make_int2(s, kb));
+                    for (int r0 = slab1; r0 < ne; r0 += TALL_ROWS) tall_t.push_back(make_int4(s, slab0, r0, slab1));
+                    tx.push_back(make_int2(s, slab0));
+                    if (slab1 < w) {
+                        const int n1 = std::min(w, slab1 + NBO), nf = std::min(m, n1 + NBO);
+                        const int K = slab1 - slab0;
+                        // the next slab's diagonal block (main stream, critical path)
+                        add_update(d3, d3fl, pan, m, n1, slab1, n1, slab0, slab1);
+                        // the next slab's near rows in place, its far rows to the staging buffer
+                        gen_update(a3, a3fl, pan + (int64_t)slab1 * m + n1, m, pan + (int64_t)slab1 * m + n1, m,
+                                   pan + (int64_t)slab0 * m + n1, m, pan + (int64_t)slab0 * m + slab1, m, nf - n1,
+                                   n1 - slab1, K, false);
+                        if (m > nf) {
+                            const TallLayout TL = tall_layout(S, s, NBO);
+                            gen_update(a3, a3fl, N.R[v].P.tall_pool + N.R[v].tall_off[s], TL.lds,
+                                       pan + (int64_t)slab1 * m + nf, m, pan + (int64_t)slab0 * m + nf, m,
+                                       pan + (int64_t)slab0 * m + slab1, m, m - nf, n1 - slab1, K, false);
+                        }
+                        // every later column, in place
+                        add_update(b3, b3fl, pan, m, m, n1, w, slab0, slab1);
+                    }
+                    continue;
                 }
                 if (k1 == slab1 && tallx(s)) tx.push_back(make_int2(s, slab0));
                 if (k1 == slab1 && slab1 < w) {
@@ -847,7 +886,23 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 N.sched.push_back(Lq);
             }
             push_gemm_launch(L_PANEL, lev, upd, 0, uflops);
-            if (!tx.empty()) emit_tallx(lev, v, tx);
+            // panel_tall = 3, a slab end (two lookahead levels, every big product on the
+            // lookahead stream, as resident grids with la_grid):
+            //   main      [wait A(j-1)] near rows of slab j (row-blocked tall TRSM, 16
+            //             workgroups per 1024 rows) -> [wait B(j-1)] slab j+1's diagonal
+            //             block -= its product (K = NBO) -> the chain of slab j+1
+            //   lookahead X = inv(L_jj), the far rows L = S X^T, then slab j+1's near rows
+            //             (in place) and far rows (into S) -= their products -> A(j), then
+            //             every later column -> B(j)
+            // so the main stream carries only small launches (the chain and its near rows)
+            // and never waits for a big product of the slab it follows.
+            int e_chain = -1;
+            if (tall3 && !tx.empty()) {
+                e_chain = push_record(0);  // slab j's diagonal blocks factored
+                if (a3_ev >= 0) push_wait(0, a3_ev);
+            } else if (!tx.empty()) {
+                emit_tallx(lev, v, tx, 0);
+            }
             if (!tall_t.empty() || !inv_t.empty()) {
                 Launch Li {};
                 Li.kind = L_INV;
@@ -865,6 +920,21 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 Lt2.count = (int32_t)tall_t.size();
                 B.tall.insert(B.tall.end(), tall_t.begin(), tall_t.end());
                 if (Lt2.count > 0) N.sched.push_back(Lt2);
+            }
+            if (tall3 && !tx.empty()) {
+                const int e_near = push_record(0);  // slab j's near rows solved
+                push_wait(1, e_chain);
+                emit_tallx(lev, v, tx, 1);  // X and the far rows
+                push_wait(1, e_near);
+                push_gemm_launch(L_GEMM, lev, a3, 0, a3fl, 1);
+                if (!a3.empty()) a3_ev = push_record(1);
+                const int b_prev = b3_ev;
+                push_gemm_launch(L_PANEL, lev, b3, 0, b3fl, 1);
+                b3_ev = push_record(1);
+                if (!d3.empty()) {
+                    if (b_prev >= 0) push_wait(0, b_prev);
+                    push_gemm_launch(L_PANEL, lev, d3, 0, d3fl);
+                }
             }
             // split fronts: a slab is final after the TRSM of its last block (tall mode:
             // after the slab's tall TRSM); at a slab end no inner update is pending
@@ -894,6 +964,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             }
         }
         if (b_pending >= 0) push_wait(0, b_pending);
+        if (b3_ev >= 0) push_wait(0, b3_ev);  // panel_tall = 3: the lookahead stream's last far rows
         // early-delivery children: the CB SYRK in column groups, an event after each
         // (the group's comm sub-step waits for exactly that event)
         for (int32_t s : large) {
