@@ -202,7 +202,7 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
                 R.P.tall_off = dp;
                 R.P.tall_pool = (double*)p;
                 R.P.tall_nbo = std::max(PNB, (S.opt.panel_nb_outer / PNB) * PNB);
-                R.P.tall_skip = S.opt.panel_tall == 3 ? R.P.tall_nbo : 0;
+                R.P.tall_skip = S.opt.panel_tall >= 3 ? R.P.tall_nbo : 0;
             }
         }
     }

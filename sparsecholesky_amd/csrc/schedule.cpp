@@ -34,7 +34,7 @@ TallLayout tall_layout(const Symbolic& S, int32_t s, int nbo) {
     TallLayout T;
     const int w = S.w(s), m = S.sn_m[s];
     T.nbs0 = std::min(w, nbo);
-    T.skip = S.opt.panel_tall == 3 ? nbo : 0;  // near rows solved in place on the main stream
+    T.skip = S.opt.panel_tall >= 3 ? nbo : 0;  // near rows solved in place on the main stream
     T.lds = std::max<int64_t>(1, m - T.nbs0 - T.skip);
     const int64_t nn = (int64_t)T.nbs0 * T.nbs0;
     T.x = al64(T.lds * T.nbs0);
@@ -45,11 +45,11 @@ TallLayout tall_layout(const Symbolic& S, int32_t s, int nbo) {
 }
 
 bool tallx_front(const Symbolic& S, const DistPlan* D, int rank, int32_t s) {
-    if ((S.opt.panel_tall != 2 && S.opt.panel_tall != 3) || S.fclass[s] != FRONT_LARGE) return false;
+    if ((S.opt.panel_tall < 2 || S.opt.panel_tall > 4) || S.fclass[s] != FRONT_LARGE) return false;
     if (D && (D->owner[s] != rank || D->pd[s] >= 0)) return false;
     // panel_tall = 3 solves the far rows on the lookahead stream: a split front sends its
     // final slabs from the main stream's point of view (STEP_SLAB): it keeps the default path
-    if (D && S.opt.panel_tall == 3 && D->split[s] >= 0) return false;
+    if (D && S.opt.panel_tall >= 3 && D->split[s] >= 0) return false;
     const int w = S.w(s), m = S.sn_m[s];
     return w >= 2 * PNB && m > std::min(w, nbo_of(S));
 }
@@ -726,7 +726,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // that step is dropped, one dispatch fewer on the chain per two steps
         std::vector<char> pre_next((size_t)S.ns, 0);
         auto fold = [&](int32_t s) { return S.opt.trsm_fold && S.opt.inner_order == 1 && !tall(s); };
-        const bool tall3 = S.opt.panel_tall == 3;
+        const bool tall3 = S.opt.panel_tall >= 3;
         int a3_ev = -1, b3_ev = -1;  // lookahead-stream events of the last slab end (panel_tall = 3)
         for (int k0 = 0; k0 < maxw; k0 += PNB) {
             Launch Lp {};
@@ -824,8 +824,13 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                                        pan + (int64_t)slab1 * m + nf, m, pan + (int64_t)slab0 * m + nf, m,
                                        pan + (int64_t)slab0 * m + slab1, m, m - nf, n1 - slab1, K, false);
                         }
-                        // every later column, in place
-                        add_update(b3, b3fl, pan, m, m, n1, w, slab0, slab1);
+                        // every later column, in place (panel_tall = 4, left-looking: only the
+                        // slab after next, from every slab so far -- one deep-K product per
+                        // slab instead of a rank-NBO pass over every later column)
+                        if (S.opt.panel_tall == 4)
+                            add_update(b3, b3fl, pan, m, m, n1, std::min(w, n1 + NBO), 0, slab1);
+                        else
+                            add_update(b3, b3fl, pan, m, m, n1, w, slab0, slab1);
                     }
                     continue;
                 }
