@@ -1720,7 +1720,7 @@ __global__ __launch_bounds__(64 * WM * WN, LEAN ? (TAG ? 5 : 6) : 1) void syrk_m
 // grid holds the dispatcher, and a small critical-path launch on another stream waits
 // for all of it (the contention probe); with slots left free, it does not.
 template <int BT, int WM, int WN, int TAG, int EPI>
-__global__ __launch_bounds__(64 * WM * WN) void syrk_mfma_resident_kernel(const GemmTask* __restrict__ tasks,
+__global__ __launch_bounds__(64 * WM * WN, 4) void syrk_mfma_resident_kernel(const GemmTask* __restrict__ tasks,
                                                                            const int2* __restrict__ tiles, int ntiles,
                                                                            const DevPlan* __restrict__ plans) {
     for (int b = blockIdx.x; b < ntiles; b += gridDim.x) {
@@ -1761,6 +1761,24 @@ __device__ __forceinline__ void gemm_tile_body(const GemmTask* __restrict__ task
     double* __restrict__ C = T.C;
     double* __restrict__ Ct = T.Ct;
     const double sg = T.sign;
+    if (!Cin && !Ct && !T.lower) {
+        // plain store (the tall solve): through a buffer resource over the tile's columns,
+        // dead elements masked by range, no branches
+        const __amdgpu_buffer_rsrc_t rc =
+            buf_rsrc(C + (int64_t)col0 * T.ldc, (uint32_t)(min(BT, T.N - col0) * T.ldc * 8));
+#pragma unroll
+        for (int a = 0; a < RTM; ++a)
+#pragma unroll
+            for (int b = 0; b < RTN; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int gi = row0 + wr * (BT / WM) + a * 16 + MFMA_F64_ROW(lane, r);
+                    const int gj = col0 + wc * (BT / WN) + b * 16 + (lane & 15);
+                    const int off = gi < T.M ? (int)((gi + (int64_t)(gj - col0) * T.ldc) * 8) : BUF_DEAD;
+                    buf_st(sg * acc[a][b][r], rc, off, 0);
+                }
+        return;
+    }
     constexpr int EA = RTM < 2 ? RTM : 2;  // MFMA tile rows per epilogue chunk
 #pragma unroll
     for (int a0 = 0; a0 < RTM; a0 += EA) {
@@ -1794,14 +1812,14 @@ __device__ __forceinline__ void gemm_tile_body(const GemmTask* __restrict__ task
 }
 
 template <int BT, int WM, int WN>
-__global__ __launch_bounds__(64 * WM * WN) void gemm_mfma_kernel(const GemmTask* __restrict__ tasks,
+__global__ __launch_bounds__(64 * WM * WN, 4) void gemm_mfma_kernel(const GemmTask* __restrict__ tasks,
                                                                   const int2* __restrict__ tiles) {
     gemm_tile_body<BT, WM, WN>(tasks, tiles, blockIdx.x);
 }
 
 // resident-grid instance (see syrk_mfma_resident_kernel)
 template <int BT, int WM, int WN>
-__global__ __launch_bounds__(64 * WM * WN) void gemm_mfma_resident_kernel(const GemmTask* __restrict__ tasks,
+__global__ __launch_bounds__(64 * WM * WN, 4) void gemm_mfma_resident_kernel(const GemmTask* __restrict__ tasks,
                                                                            const int2* __restrict__ tiles, int ntiles) {
     for (int b = blockIdx.x; b < ntiles; b += gridDim.x) {
         if (b != (int)blockIdx.x) __syncthreads();
