@@ -1779,7 +1779,7 @@ __device__ __forceinline__ void gemm_tile_body(const GemmTask* __restrict__ task
                 }
         return;
     }
-    constexpr int EA = RTM < 2 ? RTM : 2;  // MFMA tile rows per epilogue chunk
+    constexpr int EA = 1;  // MFMA tile rows per epilogue chunk (2 spills in the resident instance)
 #pragma unroll
     for (int a0 = 0; a0 < RTM; a0 += EA) {
         double v[EA][RTN][4];
