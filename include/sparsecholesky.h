@@ -120,6 +120,9 @@ typedef struct sc_options {
     int32_t la_grid;         /* > 0: the lookahead stream's panel updates run as a resident grid of this many
                                 workgroups walking their tiles (dispatched at once, so the 64-column chain on the
                                 main stream finds the slots it leaves free); 0: one workgroup per tile */
+    int32_t dist_pieces;     /* multi-GPU distributed panels: each final slab is handed over in this many column
+                                pieces (default 4: 256 of a 1024-column slab), each sent as soon as the chain has
+                                finished it, so the next slab's owner starts updating before the slab is done */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

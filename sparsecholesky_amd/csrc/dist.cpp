@@ -117,6 +117,10 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
     D.nranks = nranks;
     D.cbb = std::max(64, S.opt.dist_cbb > 0 ? S.opt.dist_cbb : 1024);
     D.nbo = std::max(PNB, (S.opt.panel_nb_outer / PNB) * PNB);
+    {
+        const int np = std::max(1, S.opt.dist_pieces);
+        D.pw = std::max(PNB, (D.nbo / np + PNB - 1) / PNB * PNB);
+    }
     const i32 ns = S.ns;
     D.owner.assign((size_t)ns, 0);
     D.gsize.assign((size_t)ns, 1);
@@ -266,8 +270,8 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
         g.cols = std::min(D.cbb, g.rows);
         g.s = c;
     };
-    auto open_step = [&](int kind, int lev, int s, int k) {
-        D.steps.push_back({kind, lev, s, k});
+    auto open_step = [&](int kind, int lev, int s, int k, int p = 0) {
+        D.steps.push_back({kind, lev, s, k, p});
         return (int32_t)D.steps.size() - 1;
     };
     auto close_step = [&](int32_t id) {  // drop a step without messages
@@ -311,19 +315,23 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
             }
             close_step(id);
             // SLAB k: rows [need, m) of the final slab to every holder that uses them,
-            // the next slab's owner first (its update is on the critical path)
+            // the next slab's owner first (its update is on the critical path), in column
+            // pieces of pw (dist_pieces): a piece leaves as soon as the chain has finished
+            // its columns, and the next owner applies it while the rest is computed
             for (int k = 0; k < nsl; ++k) {
                 const int k0 = k * D.nbo, k1 = std::min(w, k0 + D.nbo);
-                id = open_step(STEP_SLAB, lev, s, k);
                 std::vector<i32> dsts;
                 if (k + 1 < nsl && sr[k + 1] != sr[k]) dsts.push_back(sr[k + 1]);
                 for (i32 r : D.holders[D.pd[s]])
                     if (r != sr[k] && (k + 1 >= nsl || r != sr[k + 1])) dsts.push_back(r);
-                for (i32 r : dsts) {
-                    const int need = D.need_row(S, s, k, r);
-                    if (need < S.sn_m[s]) panel_msg(id, s, sr[k], r, std::max(need, k1), k0, k1);
+                for (int p = 0, c0 = k0; c0 < k1; ++p, c0 += D.pw) {
+                    id = open_step(STEP_SLAB, lev, s, k, p);
+                    for (i32 r : dsts) {
+                        const int need = D.need_row(S, s, k, r);
+                        if (need < S.sn_m[s]) panel_msg(id, s, sr[k], r, std::max(need, k1), c0, std::min(k1, c0 + D.pw));
+                    }
+                    close_step(id);
                 }
-                close_step(id);
             }
         }
         for (i32 s : by_level[lev]) {

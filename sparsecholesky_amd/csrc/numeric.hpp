@@ -42,6 +42,7 @@ enum LaunchKind : int32_t {
 enum StepKind : int32_t { STEP_INIT = 0, STEP_SLAB = 1, STEP_DELIVER = 2 };
 struct DistStep {
     int32_t kind, level, s, k;
+    int32_t p = 0;  // STEP_SLAB of a distributed panel: the column piece of slab k (dist_pieces)
 };
 
 // Device memory regions of a rank (memplan.cpp).  Messages and tasks name a region
@@ -68,6 +69,7 @@ struct DistPlan {
     int nranks = 1;
     int cbb = 1024;  // CB column-block width
     int nbo = 1024;  // panel slab width (panel_nb_outer)
+    int pw = 1024;   // distributed panels: columns per STEP_SLAB piece (nbo / dist_pieces, 64-aligned)
     std::vector<int32_t> owner;    // rank executing each supernode's assembly + panel
     std::vector<int32_t> gsize;    // rank-group size of each supernode (1 = inside a subtree)
     std::vector<int32_t> split;    // index into split_s / cb_rank, or -1

@@ -149,22 +149,25 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
     auto is_dpanel = [&](int32_t s) { return multi && D.pd[s] >= 0; };
     std::vector<int32_t> hosted_of((size_t)std::max(N.nranks, 1), -1);  // rank -> index into N.R
     for (size_t v = 0; v < N.R.size(); ++v) hosted_of[N.R[v].rank] = (int32_t)v;
-    std::vector<int32_t> init_step, slab_step0, early_step0, deliver_step((size_t)S.nlevels, -1);
-    std::vector<std::vector<int32_t>> slab_step;  // distributed panels: step of slab k, -1 = none
+    std::vector<int32_t> init_step, early_step0, deliver_step((size_t)S.nlevels, -1);
+    // split fronts / distributed panels: slab_step[s][k] = the steps of slab k's pieces (dist_pieces)
+    std::vector<std::vector<std::vector<int32_t>>> slab_step;
     std::vector<std::vector<int>> early_ev((size_t)S.ns);  // sender: event after each CB column group
     std::vector<int64_t> step_beg;
     std::vector<char> emitted;
     if (multi) {
         init_step.assign((size_t)S.ns, -1);
-        slab_step0.assign((size_t)S.ns, -1);
-        slab_step.assign((size_t)S.ns, std::vector<int32_t>());
-        for (size_t q = 0; q < D.pd_s.size(); ++q) slab_step[D.pd_s[q]].assign(D.slab_rank[q].size(), -1);
+        slab_step.assign((size_t)S.ns, {});
         early_step0.assign((size_t)S.ns, -1);
         for (int32_t id = 0; id < (int32_t)D.steps.size(); ++id) {
             const DistStep& t = D.steps[id];
             if (t.kind == STEP_INIT) init_step[t.s] = id;
-            if (t.kind == STEP_SLAB && t.k == 0) slab_step0[t.s] = id;
-            if (t.kind == STEP_SLAB && D.pd[t.s] >= 0) slab_step[t.s][t.k] = id;
+            if (t.kind == STEP_SLAB) {
+                auto& ks = slab_step[t.s];
+                if ((int)ks.size() <= t.k) ks.resize((size_t)t.k + 1);
+                if ((int)ks[t.k].size() <= t.p) ks[t.k].resize((size_t)t.p + 1, -1);
+                ks[t.k][t.p] = id;
+            }
             if (t.kind == STEP_DELIVER && t.s < 0) deliver_step[t.level] = id;
             if (t.kind == STEP_DELIVER && t.s >= 0 && t.k == 0) early_step0[t.s] = id;
         }
@@ -413,6 +416,15 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         N.sched.push_back(L);
         if (any_recv) push_wait(0, push_record(2));
     };
+    // the step of piece p of slab k of front s (-1: none), and all pieces of slab k
+    auto slab_piece = [&](int32_t s, int k, int p) -> int32_t {
+        if (!multi || k >= (int)slab_step[s].size() || p >= (int)slab_step[s][k].size()) return -1;
+        return slab_step[s][k][p];
+    };
+    auto emit_slab = [&](int32_t s, int k) {
+        if (!multi || k >= (int)slab_step[s].size()) return;
+        for (int32_t id : slab_step[s][k]) emit_step(id);
+    };
     auto is_early_sender = [&](int32_t s, int v) {
         return multi && D.early[s] && D.owner[s] == N.R[v].rank;
     };
@@ -462,7 +474,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             emit_step(init_step[s]);
         for (int k0 = 0, k = 0; k0 < w; k0 += D.nbo, ++k) {
             const int k1 = std::min(w, k0 + D.nbo);
-            emit_step(slab_step0[s] < 0 ? -1 : slab_step0[s] + k);
+            emit_slab(s, k);
             std::vector<GemmTask> cbt;
             double fl = 0.0;
             for (int jb = 0; jb < (int)cbr.size(); ++jb) {
@@ -945,9 +957,9 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             // after the slab's tall TRSM); at a slab end no inner update is pending
             for (int32_t s : large) {
                 const int w = S.w(s);
-                if (!is_split(s) || w <= k0 || slab_step0[s] < 0) continue;
+                if (!is_split(s) || w <= k0) continue;
                 const int k1 = std::min(w, k0 + PNB);
-                if (k1 == w || k1 % D.nbo == 0) emit_step(slab_step0[s] + k0 / D.nbo);
+                if (k1 == w || k1 % D.nbo == 0) emit_slab(s, k0 / D.nbo);
             }
             int e_trsm = -1;
             if (!outer_b.empty()) e_trsm = push_record(0);
@@ -1111,6 +1123,8 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                         trsm.push_back(TrsmTask {s, k0, r0, m, ctr});
                     Lt.count = (int32_t)((int64_t)trsm.size() - Lt.off);
                     if (Lt.count > 0) N.sched.push_back(Lt);
+                    // a finished piece of the slab leaves now (dist_pieces)
+                    if (k1 == k1s || (k1 - k0s) % D.pw == 0) emit_step(slab_piece(s, k, (k1 - 1 - k0s) / D.pw));
                     if (k1 < k1s) {
                         std::vector<GemmTask> upd;
                         double fl = 0.0;
@@ -1128,7 +1142,6 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     }
                 }
             }
-            if (slab_step[s].size() > (size_t)k) emit_step(slab_step[s][k]);
             // slab k's update on every hosted rank that needs it
             for (int v : vs) {
                 const int r = N.R[v].rank;
@@ -1136,15 +1149,20 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 double* pan = pan_of(v);
                 const double* Lk = pan + (int64_t)k0s * m;  // column k0s of the slab, row 0
                 const int K = k1s - k0s;
-                if (k + 1 < nsl && sr[k + 1] == r) {  // the next slab: critical path
+                if (k + 1 < nsl && sr[k + 1] == r) {  // the next slab: critical path, piece by piece
                     const int e = last_ev1(v, k - 1);
                     if (e >= 0) push_wait(0, e);
                     const int j0 = slab_c0(k + 1), j1 = slab_c1(k + 1);
-                    std::vector<GemmTask> t0;
-                    double fl = 0.0;
-                    upd_task(t0, fl, pan + (int64_t)j0 * m + j0, m, Lk + j0, m, m - j0, j1 - j0, K);
-                    push_gemm_launch(L_PANEL, lev, t0, 0, fl);
+                    for (int p = 0, c0 = k0s; c0 < k1s; ++p, c0 += D.pw) {
+                        emit_step(slab_piece(s, k, p));
+                        std::vector<GemmTask> t0;
+                        double fl = 0.0;
+                        upd_task(t0, fl, pan + (int64_t)j0 * m + j0, m, pan + (int64_t)c0 * m + j0, m, m - j0,
+                                 j1 - j0, std::min(k1s, c0 + D.pw) - c0);
+                        push_gemm_launch(L_PANEL, lev, t0, 0, fl);
+                    }
                 }
+                emit_slab(s, k);
                 std::vector<GemmTask> t1;
                 double fl = 0.0;
                 for (int j = k + 2; j < nsl; ++j) {

@@ -69,7 +69,9 @@ def _worker(rank, world, port, k, opts, out):
                                           (8, 24, dict(panel_nb_outer=128, dist_cbb=64)),
                                           (4, 20, dict(panel_nb_outer=128, dist_panel=0)),
                                           (8, 24, dict(panel_nb_outer=128, dist_cbb=64, dist_asm=0)),
-                                          (3, 24, dict(dist_cbb=128, dist_asm=0))])
+                                          (3, 24, dict(dist_cbb=128, dist_asm=0)),
+                                          (4, 24, dict(panel_nb_outer=256, dist_pieces=1)),
+                                          (4, 24, dict(panel_nb_outer=256, dist_pieces=3))])
 def test_message_schedule_matches_across_ranks(world, k, opts):
     import random
 
@@ -107,6 +109,30 @@ def test_distributed_assembly_plan(k, nranks, opts):
     assert v1.sum() < v0.sum()
     print(f"k={k} n={nranks}: INIT {v0[0] / 1e9:.2f} GB -> 0, DELIVER {v0[2] / 1e9:.2f} -> {v1[2] / 1e9:.2f} GB, "
           f"total {v0.sum() / 1e9:.2f} -> {v1.sum() / 1e9:.2f} GB")
+
+
+@pytest.mark.parametrize("k,nranks,pieces", [(64, 8, 4), (48, 4, 3), (128, 8, 16)])
+def test_slab_pieces_plan(k, nranks, pieces):
+    # dist_pieces: each distributed-panel slab hand-over splits into column pieces of
+    # ceil(1024 / pieces) rounded up to 64; the bytes moved per step kind are unchanged,
+    # only the SLAB step count grows (one step per piece that carries a message)
+    def per_kind(s):
+        st = s.dist_steps(nranks)
+        v = np.zeros(3)
+        for r in range(nranks):
+            step, peer, nb, snd = s.dist_schedule(nranks, r)
+            for a, b in zip(step[snd == 1], nb[snd == 1]):
+                v[st["kind"][a]] += b
+        return st, v
+
+    A = sc.laplacian3d(k)
+    st1, v1 = per_kind(sc.Symbolic(A, dist_pieces=1))
+    stp, vp = per_kind(sc.Symbolic(A, dist_pieces=pieces))
+    assert np.array_equal(v1, vp)
+    pw = -(-(1024 // pieces) // 64) * 64
+    n1, npc = (st1["kind"] == 1).sum(), (stp["kind"] == 1).sum()
+    assert n1 < npc <= n1 * -(-1024 // pw)
+    print(f"k={k} n={nranks}: {n1} slab steps -> {npc} pieces of {pw} columns")
 
 
 @pytest.mark.parametrize("k,nranks", [(20, 4), (24, 8), (24, 3)])

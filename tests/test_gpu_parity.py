@@ -419,7 +419,9 @@ def test_lap48_full_parity(gpu, lap48_oracle, opts):
                                                (4, True, {}), (8, True, {}), (8, False, dict(panel_tall=1)),
                                                (8, False, dict(panel_tall=2)), (2, True, dict(panel_tall=2)),
                                                (8, False, dict(dist_asm=0)), (4, True, dict(dist_asm=0)),
-                                               (8, False, dict(panel_tall=3, la_grid=448))])
+                                               (8, False, dict(panel_tall=3, la_grid=448)),
+                                               (4, False, dict(dist_pieces=1)), (8, True, dict(dist_pieces=16)),
+                                               (4, True, dict(dist_pieces=3))])
 def test_partitioned_defaults_lap48(gpu, lap48_oracle, nranks, rccl, opts):
     # the distributed plan at the DEFAULT options the N-GPU bench runs (panel_nb_outer
     # 1024, dist_cbb 1024, small_front_max 128): the 2327-wide root factored 1D
@@ -504,7 +506,8 @@ def test_partitioned_defaults_lap64(gpu, lap64_oracle, nranks, rccl):
     if nranks == 2:
         assert blk == 2  # two consecutive slabs per rank on the root
     if nranks == 8:  # 88 messages with owner assembly (dist_asm=0), 69 with distributed assembly
-        assert (info["slab_ranks"] > 0).sum() == 3 and info["n_msgs"] == 69
+        # and whole-slab hand-over, 135 with the slabs handed over in 256-column pieces
+        assert (info["slab_ranks"] > 0).sum() == 3 and info["n_msgs"] == 135
     v = sc.Numeric(s, nranks=nranks, virtual=True, rccl_self=rccl)
     for _ in range(2):
         assert v.factor(A.x) == 0
@@ -535,8 +538,9 @@ def test_partitioned_lap128_emulated8(gpu):
     assert slab_ranks == 8 and blk == 2
     assert (info["slab_ranks"] > 0).sum() == 7 and (info["split_cb_ranks"] > 0).sum() == 6
     # 70 steps / 345 messages with owner assembly (dist_asm=0, round 3); 64 / 306 with the
-    # distributed assembly (no STEP_INIT)
-    assert info["n_steps"] == 64 and info["n_msgs"] == 306
+    # distributed assembly (no STEP_INIT); 208 / 708 with every distributed-panel slab
+    # handed over in four 256-column pieces (dist_pieces)
+    assert info["n_steps"] == 208 and info["n_msgs"] == 708
     CH = 1 << 16
     ref = []
     one = sc.Numeric(s)
@@ -630,7 +634,7 @@ def test_partitioned_schedule_bitwise_equal(gpu, nranks):
     (2, False, {}), (3, False, {}), (4, False, {}), (8, False, {}), (2, True, {}), (4, True, {}), (8, True, {}),
     (4, False, dict(dist_panel=0)), (3, False, dict(dist_split=0)), (8, True, dict(dist_split=0)),
     (4, False, dict(lookahead=0, inner_order=0)), (4, False, dict(dist_asm=0)), (8, True, dict(dist_asm=0)),
-    (3, False, dict(dist_panel=0, dist_asm=0))])
+    (3, False, dict(dist_panel=0, dist_asm=0)), (4, False, dict(dist_pieces=1)), (8, True, dict(dist_pieces=8))])
 def test_partitioned_split_fronts_emulated(gpu, nranks, rccl, opts):
     # split top fronts (CB column blocks updated per slab by the ranks of the group)
     # and distributed panels (slabs factored 1D slab-cyclic over the group, the root
