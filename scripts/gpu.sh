@@ -101,6 +101,25 @@ case "$task" in
     # kernel durations of the same runs (tiny tree, small-front levels)
     timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_small -o small -- \
       python3 scripts/small_configs.py > /dev/null 2> gpurun_out/small_prof.err ;;
+  tiny)  # tiny-path parity, small configs, and the tiny kernel's duration per variant
+    timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "tiny or not_positive" -x -q --timeout 120 \
+      --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_tiny.log 2>&1
+    rc=$?; echo "pytest tiny rc=$rc"; tail -3 gpurun_out/pytest_tiny.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 300 python3 scripts/small_configs.py > gpurun_out/small_configs.jsonl 2> gpurun_out/small_configs.err
+    rc=$?; cat gpurun_out/small_configs.jsonl; [ $rc -eq 0 ] || exit $rc
+    for v in main "$@"; do
+      pkg=.; [ "$v" != main ] && pkg=gpurun_var/$v
+      timeout -k 10 120 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_tiny_$v -o tiny -- \
+        python3 scripts/tiny_probe.py $pkg > gpurun_out/tiny_$v.log 2>&1 || { tail -3 gpurun_out/tiny_$v.log; exit 1; }
+      python3 - "$v" <<'EOF'
+import csv, glob, sys
+for f in glob.glob(f"gpurun_out/prof_tiny_{sys.argv[1]}/**/*kernel_stats.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "tiny" in r["Name"]:
+            print(sys.argv[1], r["Name"][:40], "calls", r["Calls"], "avg_us", round(float(r["AverageNs"]) / 1e3, 2),
+                  "min_us", round(float(r["MinNs"]) / 1e3, 2))
+EOF
+    done ;;
   solve)
     timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -k "solve" -x -v --timeout 240 \
       --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_solve.log 2>&1

@@ -744,6 +744,7 @@ __global__ __launch_bounds__(256) void tiny_tree_kernel(DevPlan P, TinyPlan T, c
         }
         lds_barrier();
     }
+    if (T.host_info) __syncthreads();  // every wave's panel stores done before the status word
     if (T.host_info && tid == 0) {  // the status word straight to the pinned host copy
         P.info[0] = s_info;
         __hip_atomic_store(T.host_info, s_info, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -768,8 +769,8 @@ hipError_t launch_tiny_tree(const DevPlan& P, const TinyPlan& T, int maxm, const
 // then applies the rest of the rank-4 update -- so the next step's serial chain (LDS
 // round trip, four pivots) overlaps this step's bulk FMAs.  Entries outside the
 // symbolic pattern come out as exact zeros (every product of the update has a
-// structurally zero factor) and are not stored: the panel entries of every supernode
-// are gathered from the dense image by a host-built list.  Status as tiny_tree_kernel.
+// structurally zero factor) and are not stored: a host-built lane map names, per dense
+// entry, its A value and its panel-pool offset.  Status as tiny_tree_kernel.
 #ifndef SC_TD_LA
 #define SC_TD_LA 1  // 1: the next step's D factored under this step's bulk update
 #endif
@@ -786,7 +787,7 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 #ifndef SC_TD_PROBE
-#define SC_TD_PROBE 0  // timing probes (scripts/tiny_probe.py): 1 no factorization
+#define SC_TD_PROBE 0  // timing probes (scripts/tiny_probe.py): 1 no factorization, 2 factor twice
 #endif
 // raw[4 * r .. 4 * r + 3] = step columns of row r (published) -> D and its factor
 __device__ __forceinline__ void td_factor_d(const double* raw, int J, double (&Ld)[4][4], double (&rc)[4], int& bad) {
@@ -933,70 +934,49 @@ __device__ __forceinline__ void td_steps(double (&a)[NP], double (&Ld)[4][4], do
 
 template <int NP>
 __global__ __launch_bounds__(64) void tiny_dense_kernel(DevPlan P, TinyPlan T, int n, const double* __restrict__ Ax) {
-    constexpr int LD = TINY_DENSE_LD, U = 8, UP = 8;
-    __shared__ double Dm[NP * LD];
     __shared__ __attribute__((aligned(16))) double raw[NP * 4];
     __shared__ __attribute__((aligned(16))) double lv[NP * 4];
-    __shared__ int2 prl[UP * 64];  // the first UP * 64 panel entries of the plan, staged at the start
+    __shared__ int po[NP * 64];  // the panel offsets of the lane map, parked for the end
     const int i = threadIdx.x;
-    // the first U * 64 A entries and UP * 64 panel entries of the plan in flight while
-    // the image is zeroed (the panel entries wait in LDS for the end)
-    int2 ae[U], pe[UP];
-    double av[U];
+    // the lane map: entry (row i, column j) comes from Ax[q[j].x] and goes to panel
+    // offset q[j].y (-1: none) -- one coalesced 512-byte load per column, then every A
+    // value straight into its register (no LDS image, no barriers); the panel offsets
+    // wait in LDS (lane-private slots) for the stores at the end
+    int2 q[NP];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int e = u * 64 + i;
-        ae[u] = e < T.na ? T.a[e] : make_int2(-1, 0);
-    }
+    for (int j = 0; j < NP; ++j) q[j] = T.a[j * 64 + i];
 #pragma unroll
-    for (int u = 0; u < UP; ++u) {
-        const int e = u * 64 + i;
-        pe[u] = e < T.npr ? T.pr[e] : make_int2(-1, 0);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) av[u] = ae[u].x >= 0 ? Ax[ae[u].x] : 0.0;
-    for (int e = i; e < NP * LD; e += 64) Dm[e] = 0.0;
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-        if (ae[u].x >= 0) Dm[ae[u].y] = av[u];
-#pragma unroll
-    for (int u = 0; u < UP; ++u) prl[u * 64 + i] = pe[u];
-    for (int e = U * 64 + i; e < T.na; e += 64) {  // rare: more than U * 64 entries
-        const int2 q = T.a[e];
-        Dm[q.y] = Ax[q.x];
-    }
-    __syncthreads();
+    for (int j = 0; j < NP; ++j) po[j * 64 + i] = q[j].y;
     double a[NP];
-#pragma unroll
-    for (int j = 0; j < NP; ++j) a[j] = j <= i ? Dm[i * LD + j] : 0.0;
-#pragma unroll
-    for (int j = 0; j < NP; ++j) a[j] = (i == j && i >= n) ? 1.0 : a[j];  // identity padding
     int fail = n;
     double Ld[4][4], rc[4];
     int bad;
-    if (SC_TD_PROBE != 1) {
-        *reinterpret_cast<double2*>(raw + 4 * i) = make_double2(a[0], a[1]);
-        *reinterpret_cast<double2*>(raw + 4 * i + 2) = make_double2(a[2], a[3]);
-        wave_lds_sync();
-        td_factor_d(raw, 0, Ld, rc, bad);
+    // probe 2: the same factorization twice through the same code (the second pass with
+    // the instruction cache warm)
+#pragma nounroll
+    for (int pass = 0; pass < (SC_TD_PROBE == 2 ? 2 : 1); ++pass) {
+#pragma unroll
+        for (int j = 0; j < NP; ++j) a[j] = q[j].x >= 0 ? Ax[q[j].x] : 0.0;
+#pragma unroll
+        for (int j = 0; j < NP; ++j) a[j] = (i == j && i >= n) ? 1.0 : a[j];  // identity padding
+        fail = n;
+        if (SC_TD_PROBE != 1) {
+            wave_lds_sync();
+            *reinterpret_cast<double2*>(raw + 4 * i) = make_double2(a[0], a[1]);
+            *reinterpret_cast<double2*>(raw + 4 * i + 2) = make_double2(a[2], a[3]);
+            wave_lds_sync();
+            td_factor_d(raw, 0, Ld, rc, bad);
+            td_steps<NP, 0>(a, Ld, rc, bad, fail, raw, lv, i);
+        }
     }
-    if (SC_TD_PROBE != 1) td_steps<NP, 0>(a, Ld, rc, bad, fail, raw, lv, i);
     if (fail > n) fail = n;  // padding pivots never fail; a failure at or past n is none
 #pragma unroll
-    for (int j = 0; j < NP; ++j)
-        if (j <= i && i < n) Dm[i * LD + j] = a[j];
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < UP; ++u) {
-        const int2 q = prl[u * 64 + i];
-        if (q.x >= 0) P.panel_pool[q.y] = Dm[q.x];
+    for (int j = 0; j < NP; ++j) {
+        const int o = po[j * 64 + i];
+        if (o >= 0) P.panel_pool[o] = a[j];
     }
-    for (int e = UP * 64 + i; e < T.npr; e += 64) {  // the rest of the panel entries
-        const int2 q = T.pr[e];
-        P.panel_pool[q.y] = Dm[q.x];
-    }
-    __syncthreads();
+    // one wave: lane 0's system-scope release store below waits for the wave's panel
+    // stores, so the status word is seen after the factor
     if (i == 0) {
         if (T.host_info) {  // the status word straight to the pinned host copy
             const int32_t st = fail < n ? fail + 1 : 0x7f7f7f7f;
@@ -1010,7 +990,7 @@ __global__ __launch_bounds__(64) void tiny_dense_kernel(DevPlan P, TinyPlan T, i
 
 hipError_t launch_tiny_dense(const DevPlan& P, const TinyPlan& T, int n, const double* Ax, hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    if (n > TINY_DENSE_N) return hipErrorInvalidValue;
+    if (n > TINY_DENSE_N || T.na != tiny_dense_np(n) * 64) return hipErrorInvalidValue;  // the lane map's shape
     if (n <= 16)
         hipLaunchKernelGGL(tiny_dense_kernel<16>, dim3(1), dim3(64), 0, st, P, T, n, Ax);
     else if (n <= 32)

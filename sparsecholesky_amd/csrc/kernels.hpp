@@ -197,10 +197,10 @@ constexpr int TINY_PR_LDS = 2048;    // extend-add pairs staged in LDS with the 
 hipError_t launch_tiny_tree(const DevPlan& P, const TinyPlan& T, int maxm, const double* Ax, hipStream_t st);
 // Tiny dense (n <= TINY_DENSE_N, one device): the whole matrix as one dense lower
 // triangle in one wave, lane i holding row i in registers, four pivots per step.  The
-// TinyPlan lists are reused: a = (Ax index, dense index r * TINY_DENSE_LD + c), pr =
-// (dense index, panel-pool offset) per stored panel entry; nf, ph unused.
+// TinyPlan list a is reused as the lane map: a[c * 64 + r] = (Ax index of entry (r, c)
+// or -1, its panel-pool offset or -1) for the kernel's padded order NP; na = NP * 64.
 constexpr int TINY_DENSE_N = 64;
-constexpr int TINY_DENSE_LD = 65;  // padded row stride of the dense image in LDS
+inline int tiny_dense_np(int n) { return n <= 16 ? 16 : n <= 32 ? 32 : n <= 48 ? 48 : 64; }
 hipError_t launch_tiny_dense(const DevPlan& P, const TinyPlan& T, int n, const double* Ax, hipStream_t st);
 
 hipError_t launch_front_chain(const DevPlan& P, const ChainPlan& C, int first, int count, int maxm,

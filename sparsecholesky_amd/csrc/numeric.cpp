@@ -7,6 +7,8 @@
 //   work arena  liveness-planned contribution blocks (memplan.cpp), ld = mb_s
 #include "numeric_impl.hpp"
 
+#include <chrono>
+
 namespace sc {
 
 int64_t dalloc(Numeric& N, size_t bytes, void*& p) {
@@ -387,6 +389,9 @@ int64_t numeric_factor(Numeric& N, const double* d_Ax, bool sync) {
         N.ev.assign(2 * N.sched.size(), nullptr);
         for (auto& e : N.ev) HIP_TRY(hipEventCreate(&e));
     }
+    // tiny path (the kernel stores the status word to pinned host memory itself): mark
+    // it pending, so that numeric_status can wait on the word instead of the stream
+    if (N.TP.host_info) *(volatile int32_t*)N.h_info = Numeric::STATUS_PENDING;
     if (N.use_graph && N.profile != 1) {
         // the whole level schedule (both streams, and the timing events when
         // profiling) as one hipGraph, re-captured only when its inputs change
@@ -424,9 +429,24 @@ int64_t numeric_status(Numeric& N) {
     if (!N.factored) return SC_ERR_STATE;
     if (N.status_valid) return N.status;
     HIP_TRY(hipSetDevice(N.device));
+    // tiny path, unprofiled: the kernel's last act is the system-scope release store of
+    // the status word (every panel store of its one wave is visible before it), so the
+    // host polls the pinned word -- a few microseconds sooner than the stream's
+    // completion signal; after ~2 ms of polling it falls back to the stream sync
+    bool seen = false;
+    if (N.TP.host_info && N.profile == 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t it = 1;; ++it) {
+            if (*(volatile int32_t*)N.h_info != Numeric::STATUS_PENDING) {
+                seen = true;
+                break;
+            }
+            if ((it & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+        }
+    }
     // every stream's work is joined into the main stream before the status copy
-    HIP_TRY(hipStreamSynchronize(N.stream));
-    int32_t info = *N.h_info;
+    if (!seen) HIP_TRY(hipStreamSynchronize(N.stream));
+    int32_t info = *(volatile int32_t*)N.h_info;
     if (!N.owner.empty() && !N.emulated && !N.dry_comm) {  // one rank per process: the global minimum
         const int64_t rc = dist_min_info(N, info);
         if (rc != SC_OK) return rc;

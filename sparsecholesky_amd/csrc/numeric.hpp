@@ -211,6 +211,7 @@ struct Numeric {
     DevPlan* d_plans = nullptr;  // the hosted ranks' DevPlans (CB SYRK extend-add gather)
     int32_t* d_info = nullptr;       // shared by the hosted ranks' DevPlans
     int32_t* h_info = nullptr;       // pinned host copy, written at the end of each factorization
+    static constexpr int32_t STATUS_PENDING = -2;  // h_info before the tiny kernel's status store
     double* d_Ax_owned = nullptr;
     const double* last_Ax = nullptr;
     bool factored = false;

@@ -1211,21 +1211,22 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
     // launch, postorder (the internal numbering), everything in LDS
     // single device, n <= TINY_DENSE_N (and the tiny_dense option): the whole matrix as
     // one dense lower triangle in one wave (kernels.hip tiny_dense_kernel); the plan is
-    // the A entries' dense positions and, per supernode panel entry, the dense position
-    // it is gathered from (internal numbering: the factor of the postordered matrix is
-    // the postordered factor, so the dense image is the multifrontal result)
+    // one (Ax index, panel position) pair per dense entry (column c, row r) at c * 64 + r,
+    // -1 where the entry has no A value / is not stored (internal numbering: the factor
+    // of the postordered matrix is the postordered factor, so the dense image is the
+    // multifrontal result)
     const bool dense = !multi && S.opt.tiny_dense && S.n > 0 && S.n <= TINY_DENSE_N && S.nnzA_in <= INT32_MAX;
     if (dense) {
         for (int32_t s = 0; s < S.ns; ++s) {
             const int m = S.sn_m[s], w = S.w(s), c0 = S.sn_start[s];
             const int32_t* rows = S.rows.data() + S.rows_ptr[s];
+            if (B.ta.empty()) B.ta.assign((size_t)tiny_dense_np((int)S.n) * 64, make_int2(-1, -1));
             for (int lc = 0; lc < w; ++lc)
                 for (int64_t q = S.a_ptr[c0 + lc]; q < S.a_ptr[c0 + lc + 1]; ++q)
-                    B.ta.push_back(make_int2((int32_t)S.a_src[q], rows[S.a_pos[q]] * TINY_DENSE_LD + c0 + lc));
+                    B.ta[(size_t)(c0 + lc) * 64 + rows[S.a_pos[q]]].x = (int32_t)S.a_src[q];
             const int64_t off = N.R[0].panel_off[s];
             for (int j = 0; j < w; ++j)
-                for (int i = j; i < m; ++i)
-                    B.tpr.push_back(make_int2(rows[i] * TINY_DENSE_LD + c0 + j, (int32_t)(off + (int64_t)j * m + i)));
+                for (int i = j; i < m; ++i) B.ta[(size_t)(c0 + j) * 64 + rows[i]].y = (int32_t)(off + (int64_t)j * m + i);
         }
         Launch L {};
         L.kind = L_SMALL;
