@@ -28,7 +28,7 @@ int64_t debug_syrk(double* dC, int ldc, const double* dA, int lda, int M, int Nn
     if (e == hipSuccess && !tiles.empty())
         e = hipMemcpy(dt, tiles.data(), tiles.size() * sizeof(int2), hipMemcpyHostToDevice);
     // K <= 128: the lean instance (as the schedule's default syrk_lean_kmax picks it)
-    if (e == hipSuccess) e = launch_syrk(d, dt, (int)tiles.size(), bt, 0, nullptr, 0, nullptr, K <= 128);
+    if (e == hipSuccess) e = launch_syrk(d, dt, (int)tiles.size(), bt, 0, nullptr, 0, GatherTab {}, K <= 128);
     hipError_t e2 = hipDeviceSynchronize();
     (void)hipFree(d);
     (void)hipFree(dt);
@@ -160,7 +160,7 @@ int64_t debug_contention(int M, int K, int chain_rows, int nchain, int mode, int
     const int resident = (mode & 8) ? mask_stride : 0;  // bit 3: the hog as a resident grid of this size
     auto hog_direct = [&]() {
         if (resident > 0)
-            return launch_syrk_resident((GemmTask*)bt, (int2*)bl, ntiles, SYRK_BT_LARGE, 0, s_hog, 0, nullptr, resident);
+            return launch_syrk_resident((GemmTask*)bt, (int2*)bl, ntiles, SYRK_BT_LARGE, 0, s_hog, 0, GatherTab {}, resident);
         return launch_syrk((GemmTask*)bt, (int2*)bl, ntiles, SYRK_BT_LARGE, 0, s_hog);
     };
     auto hog = [&]() {

@@ -1384,107 +1384,97 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
 // columns x 4 rows per load hit distinct banks); wave w owns the chunk's columns
 // c = w (mod waves), so children add in their fixed order with no atomics and no
 // barrier per child (deterministic).  A child's CB rows that land in a 64-row block
-// of the parent's CB are one contiguous run (relind is increasing): tile_bnd.
-// wave-uniform values kept in SGPRs (the child loop is uniform; without this the
-// compiler keeps its counters in VGPRs and branches per lane)
-__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
-template <class T>
-__device__ __forceinline__ T* uni_ptr(T* p) {
-    const uint64_t v = reinterpret_cast<uint64_t>(p);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
-}
-
+// of the parent's CB are one contiguous run (relind is increasing), and so are its
+// columns in a 64-column block: the host's segment table (GSeg) lists, per 64 x 64
+// block of the CB, each child's runs and base pointers -- one uniform (scalar) load
+// per child instead of the child-list / plan / bounds lookup chain.
 template <int BT, int WM, int WN, int BK = 16, int GR = 64>
-__device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const DevPlan& P, int row0, int col0,
+__device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const int64_t* __restrict__ gblk,
+                                                     const GSeg* __restrict__ gseg, int row0, int col0,
                                                      double4_t (&acc)[BT / WM / 16][BT / WN / 16], double* smem) {
     constexpr int NW = WM * WN, NT = 64 * NW;
     constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
-    // GR: rows per chunk (64, or 32 for the lean instance), GLD: LDS column stride
-    // (doubles); TB: row granularity of tile_bnd (the parent's 64-row CB blocks)
-    constexpr int GLD = GR + 1, TB = 64;
+    // GR: rows per chunk (64, or 32 for the lean instance), GLD: LDS column stride (doubles)
+    constexpr int GLD = GR + 1;
     // child columns per batch of loads: all of a wave's <= 64 / NW columns per child for
     // 64-tiles; 4 for 128-tiles (VGPR budget: 4 waves / SIMD)
     constexpr int GQ = BT == 64 ? (GR == 32 ? 8 : 64 / NW) : SC_GATHER_Q;
-    constexpr int GC = 64;  // children staged per pass (one lane each)
+    // segments whose relative indices are loaded together (VGPR budget: 128-tiles keep
+    // four workgroups per CU with one)
+    constexpr int SB = BT == 64 ? 4 : 1;
     constexpr int OPS = 2 * 2 * BK * (BT + 16);  // the operand stages' doubles (smem)
-    static_assert(BT * GLD + GC * 6 <= OPS, "gather chunk and child table fit the operand LDS");
+    static_assert(BT * GLD <= OPS, "gather chunk fits the operand LDS");
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wr = wid / WN, wc = wid % WN;
-    const int s = T.gs;
     const int w = T.K;
     const int mb = T.M;
-    const int cp0 = uni(P.child_ptr[s]), cp1 = uni(P.child_ptr[s + 1]);
+    const int nb = (mb + 63) >> 6;
+    const int64_t* __restrict__ blk = gblk + T.gb;
+    const GSeg* __restrict__ seg = gseg;
     double* G = smem;
-    // child table (one entry per staged child): CB base, relind base, then mbc and the
-    // bounds of its CB rows in this chunk's rows and in the tile's columns
-    const double** s_cb = reinterpret_cast<const double**>(smem + BT * GLD);
-    const int32_t** s_rel = reinterpret_cast<const int32_t**>(smem + BT * GLD + GC);
-    int32_t* s_int = reinterpret_cast<int32_t*>(smem + BT * GLD + 2 * GC);  // [5][GC]
     double* __restrict__ C = T.C;
     const int64_t ldc = T.ldc;
     const __amdgpu_buffer_rsrc_t rc = buf_rsrc(C + (int64_t)col0 * ldc, (uint32_t)(min(BT, T.N - col0) * ldc * 8));
 #pragma unroll 1
     for (int h = 0; h < BT / GR; ++h) {
         const int r0 = row0 + h * GR;  // CB rows of this chunk: [r0, r0 + GR)
+        const int rb = r0 >> 6;        // its 64-row block of the CB
         if (h) __syncthreads();        // previous chunk's G fully read
         for (int e = tid; e < BT * GLD; e += NT) G[e] = 0.0;
-        for (int cbase = cp0;; cbase += GC) {
-            const int nc = min(GC, cp1 - cbase);
-            // one lane per child: every child's metadata loads in flight together
-            if (wid == 0 && lane < nc) {
-                const int c = P.child_list[cbase + lane];
-                const int mbc = P.sn_m[c] - (P.sn_start[c + 1] - P.sn_start[c]);
-                const int32_t* tb = P.tile_bnd + P.tb_ptr[c];
-                s_cb[lane] = P.cb_pool + P.cb_off[c];
-                s_rel[lane] = P.relind + P.rel_ptr[c];
-                s_int[0 * GC + lane] = mbc;
-                s_int[1 * GC + lane] = bnd_at(tb, r0 / TB, mbc);
-                s_int[2 * GC + lane] = bnd_at(tb, r0 / TB + 1, mbc);
-                s_int[3 * GC + lane] = bnd_at(tb, col0 / TB, mbc);
-                s_int[4 * GC + lane] = bnd_at(tb, (col0 + BT) / TB, mbc);
-            }
-            __syncthreads();
-            for (int i = 0; r0 < mb && i < nc; ++i) {
-                const int ilo = uni(s_int[1 * GC + i]), ihi = uni(s_int[2 * GC + i]);
-                const int jlo = uni(s_int[3 * GC + i]), jhi = uni(s_int[4 * GC + i]);
-                if (ilo >= ihi || jlo >= jhi) continue;
-                const int mbc = uni(s_int[i]);
-                const int32_t* __restrict__ rel = uni_ptr(s_rel[i]);
-                const double* __restrict__ cb = uni_ptr(s_cb[i]);
-                // this lane's row of the chunk (<= 64 child rows map into 64 parent rows)
-                const int ic = ilo + lane;
-                int prow = ic < ihi ? rel[ic] - w - r0 : -1;
-                if (prow >= GR) prow = -1;  // 32-row chunks: the other half of the 64-row block
-                for (int jb = jlo; jb < jhi; jb += 64) {
-                    const int jl = jb + lane;
-                    const int pcl = jl < jhi ? rel[jl] - w - col0 : -1;
-                    uint64_t mask = __ballot(pcl >= 0 && pcl % NW == wid);
+        __syncthreads();
+        // the segments of the chunk's blocks (rb, cb), cb over the tile's 64-column
+        // blocks on or below the diagonal, in the host table's (child) order: each G
+        // entry gets its children's adds in child order (deterministic, no atomics)
+        const int cb1 = min(min(nb, rb + 1), (col0 + BT) >> 6);
+        for (int cbk = col0 >> 6; r0 < mb && cbk < cb1; ++cbk) {
+            const int64_t bi = (int64_t)rb * (rb + 1) / 2 + cbk;
+            const int64_t p0 = blk[bi], p1 = blk[bi + 1];
+            for (int64_t pb = p0; pb < p1; pb += SB) {
+                // this lane's chunk row and tile column of SB segments, loads in flight together
+                int prw[SB], pcl[SB];
+#pragma unroll
+                for (int q = 0; q < SB; ++q) {
+                    prw[q] = -1;
+                    pcl[q] = -1;
+                    if (pb + q < p1) {
+                        const GSeg& g = seg[pb + q];
+                        const int ic = g.ilo + lane, jl = g.jlo + lane;
+                        if (ic < g.ihi) prw[q] = g.rel[ic] - w - r0;
+                        if (jl < g.jhi) pcl[q] = g.rel[jl] - w - col0;
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < SB; ++q) {
+                    if (pb + q >= p1) break;
+                    const GSeg& g = seg[pb + q];
+                    const int ic = g.ilo + lane;
+                    const int prow = prw[q] < GR ? prw[q] : -1;  // 32-row chunks: the other half of the block
+                    const int mbc = g.mbc;
+                    const double* __restrict__ cb = g.cb;
+                    uint64_t mask = __ballot(pcl[q] >= 0 && pcl[q] % NW == wid);
                     while (mask) {  // up to GQ owned child columns (uniform), all loads in flight first
                         int jc[GQ], pc[GQ];
 #pragma unroll
-                        for (int q = 0; q < GQ; ++q) {
+                        for (int u = 0; u < GQ; ++u) {
                             const int b = mask ? __builtin_ctzll(mask) : -1;
-                            jc[q] = b < 0 ? -1 : jb + b;
-                            pc[q] = b < 0 ? 0 : __builtin_amdgcn_readlane(pcl, b);
+                            jc[u] = b < 0 ? -1 : g.jlo + b;
+                            pc[u] = b < 0 ? 0 : __builtin_amdgcn_readlane(pcl[q], b);
                             mask &= mask - 1;
                         }
                         double v[GQ];
                         bool ok[GQ];
 #pragma unroll
-                        for (int q = 0; q < GQ; ++q) {  // column jc of the child's CB, rows >= jc
-                            ok[q] = jc[q] >= 0 && prow >= 0 && ic >= jc[q];
-                            const __amdgpu_buffer_rsrc_t rs = buf_rsrc(cb + (int64_t)max(jc[q], 0) * mbc, (uint32_t)mbc * 8u);
-                            v[q] = buf_ld(rs, ok[q] ? ic * 8 : BUF_DEAD, 0);
+                        for (int u = 0; u < GQ; ++u) {  // column jc of the child's CB, rows >= jc
+                            ok[u] = jc[u] >= 0 && prow >= 0 && ic >= jc[u];
+                            const __amdgpu_buffer_rsrc_t rs = buf_rsrc(cb + (int64_t)max(jc[u], 0) * mbc, (uint32_t)mbc * 8u);
+                            v[u] = buf_ld(rs, ok[u] ? ic * 8 : BUF_DEAD, 0);
                         }
 #pragma unroll
-                        for (int q = 0; q < GQ; ++q)
-                            if (ok[q]) G[pc[q] * GLD + prow] += v[q];
+                        for (int u = 0; u < GQ; ++u)
+                            if (ok[u]) G[pc[u] * GLD + prow] += v[u];
                     }
                 }
             }
-            if (cbase + GC >= cp1) break;
-            __syncthreads();  // the child table is restaged
         }
         __syncthreads();
         // the waves whose MFMA rows lie in this chunk (a wave's BT / WM <= 64 rows sit in
@@ -1609,7 +1599,8 @@ __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t
 // bound (a few K stages, then the C traffic), not MFMA-bound
 template <int BT, int WM, int WN, int TAG, int EPI, int LEAN = 0>
 __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ tasks, const int2* __restrict__ tiles,
-                                               int bidx, const DevPlan* __restrict__ plans) {
+                                               int bidx, const int64_t* __restrict__ gblk,
+                                               const GSeg* __restrict__ gseg) {
     constexpr int BK = LEAN ? 8 : 16;
     constexpr int LDT = BT + 16;
     constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
@@ -1638,7 +1629,7 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
 
     if constexpr (TAG == 1) {
         if (T.gs >= 0) {  // the front's CB is not assembled: gather the children's entries
-            syrk_gather_epilogue<BT, WM, WN, BK, LEAN ? 32 : 64>(T, plans[T.gv], row0, col0, acc, smem);
+            syrk_gather_epilogue<BT, WM, WN, BK, LEAN ? 32 : 64>(T, gblk, gseg, row0, col0, acc, smem);
             return;
         }
     }
@@ -1690,8 +1681,9 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
 template <int BT, int WM, int WN, int TAG, int EPI, int LEAN = 0>
 __global__ __launch_bounds__(64 * WM * WN, LEAN ? (TAG ? 5 : 6) : 1) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
                                                                   const int2* __restrict__ tiles,
-                                                                  const DevPlan* __restrict__ plans) {
-    syrk_tile_body<BT, WM, WN, TAG, EPI, LEAN>(tasks, tiles, blockIdx.x, plans);
+                                                                  const int64_t* __restrict__ gblk,
+                                                                  const GSeg* __restrict__ gseg) {
+    syrk_tile_body<BT, WM, WN, TAG, EPI, LEAN>(tasks, tiles, blockIdx.x, gblk, gseg);
 }
 
 // Resident-grid instance: a grid smaller than the GPU's workgroup slots walks the tile
@@ -1702,10 +1694,11 @@ __global__ __launch_bounds__(64 * WM * WN, LEAN ? (TAG ? 5 : 6) : 1) void syrk_m
 template <int BT, int WM, int WN, int TAG, int EPI>
 __global__ __launch_bounds__(64 * WM * WN, 4) void syrk_mfma_resident_kernel(const GemmTask* __restrict__ tasks,
                                                                            const int2* __restrict__ tiles, int ntiles,
-                                                                           const DevPlan* __restrict__ plans) {
+                                                                           const int64_t* __restrict__ gblk,
+                                                                           const GSeg* __restrict__ gseg) {
     for (int b = blockIdx.x; b < ntiles; b += gridDim.x) {
         if (b != (int)blockIdx.x) __syncthreads();  // the previous tile's LDS reads are done
-        syrk_tile_body<BT, WM, WN, TAG, EPI, 0>(tasks, tiles, b, plans);
+        syrk_tile_body<BT, WM, WN, TAG, EPI, 0>(tasks, tiles, b, gblk, gseg);
     }
 }
 
@@ -2042,18 +2035,21 @@ hipError_t launch_trsm_panel(const DevPlan& P, const TrsmTask* tasks, int count,
 // bt = 64: 64x64 tiles on 4 waves (2x2); bt = 128: 128x128 tiles on 8 waves (2x4).
 // epi: epilogue with its C loads in flight together (see the kernel).
 template <int TAG, int EPI>
-static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int bt, hipStream_t st,
-                          const DevPlan* plans, bool lean) {
+static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int bt, hipStream_t st, GatherTab gt,
+                          bool lean) {
     if (bt == 64 && lean)
-        hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG, EPI, 1>), dim3(n), dim3(256), 0, st, tasks, tiles, plans);
+        hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG, EPI, 1>), dim3(n), dim3(256), 0, st, tasks, tiles, gt.blk,
+                           gt.seg);
     else if (bt == 128)
-        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, EPI>), dim3(n), dim3(512), 0, st, tasks, tiles, plans);
+        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, EPI>), dim3(n), dim3(512), 0, st, tasks, tiles, gt.blk,
+                           gt.seg);
     else
-        hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG, EPI>), dim3(n), dim3(256), 0, st, tasks, tiles, plans);
+        hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG, EPI>), dim3(n), dim3(256), 0, st, tasks, tiles, gt.blk,
+                           gt.seg);
 }
 
 hipError_t launch_syrk_resident(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag,
-                                hipStream_t st, int epi, const DevPlan* plans, int grid) {
+                                hipStream_t st, int epi, GatherTab gt, int grid) {
     if (total_tiles <= 0) return hipSuccess;
     grid = std::max(8, std::min(grid, (total_tiles + 7) / 8 * 8));
     const dim3 g(grid);
@@ -2066,7 +2062,7 @@ hipError_t launch_syrk_resident(const GemmTask* tasks, const int2* tiles, int to
     }
 #define SC_RES(BT_, WM_, WN_, TAG_, EPI_)                                                                          \
     hipLaunchKernelGGL((syrk_mfma_resident_kernel<BT_, WM_, WN_, TAG_, EPI_>), g, dim3(64 * WM_ * WN_), 0, st, tasks, \
-                       tiles, total_tiles, plans)
+                       tiles, total_tiles, gt.blk, gt.seg)
     if (bt == 128) {
         if (tag) {
             if (epi) SC_RES(128, 2, 4, 1, 1); else SC_RES(128, 2, 4, 1, 0);
@@ -2085,7 +2081,7 @@ hipError_t launch_syrk_resident(const GemmTask* tasks, const int2* tiles, int to
 }
 
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
-                       int epi, const DevPlan* plans, bool lean) {
+                       int epi, GatherTab gt, bool lean) {
     if (total_tiles <= 0) return hipSuccess;
     if (tag == 2) {
         if (bt == 128)
@@ -2095,11 +2091,11 @@ hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles
         return hipGetLastError();
     }
     if (tag)
-        epi ? launch_syrk_t<1, 1>(tasks, tiles, total_tiles, bt, st, plans, lean)
-            : launch_syrk_t<1, 0>(tasks, tiles, total_tiles, bt, st, plans, lean);
+        epi ? launch_syrk_t<1, 1>(tasks, tiles, total_tiles, bt, st, gt, lean)
+            : launch_syrk_t<1, 0>(tasks, tiles, total_tiles, bt, st, gt, lean);
     else
-        epi ? launch_syrk_t<0, 1>(tasks, tiles, total_tiles, bt, st, plans, lean)
-            : launch_syrk_t<0, 0>(tasks, tiles, total_tiles, bt, st, plans, lean);
+        epi ? launch_syrk_t<0, 1>(tasks, tiles, total_tiles, bt, st, gt, lean)
+            : launch_syrk_t<0, 0>(tasks, tiles, total_tiles, bt, st, gt, lean);
     return hipGetLastError();
 }
 

@@ -60,11 +60,31 @@ struct DevPlan {
     int32_t tall_skip;  // rows right below the first slab that stay in the panel (panel_tall = 3)
 };
 
+// One child's share of one 64 x 64 block (rb, cb) of a parent's contribution block
+// (the CB SYRK's extend-add gather): its CB rows [ilo, ihi) map into the parent's CB
+// rows [64 rb, 64 rb + 64) and its CB columns [jlo, jhi) into the parent's CB columns
+// [64 cb, 64 cb + 64); cb / rel: the child's CB (ld mbc) and relative indices (parent
+// front positions).  Host-built per gathering task (schedule.cpp gather_segments).
+struct GSeg {
+    const double* cb;
+    const int32_t* rel;
+    int32_t mbc, ilo, ihi, jlo, jhi, pad;
+};
+
+// The schedule's gather tables (device), kernel arguments of the CB SYRK launches.
+struct GatherTab {
+    const int64_t* blk = nullptr;
+    const GSeg* seg = nullptr;
+};
+
 // One lower-trapezoid SYRK update: C[i,j] -= sum_k A[i,k] A[j,k], j < N, j <= i < M.
 // gs >= 0 (CB updates only): C is front gs's whole contribution block and is not read;
 // the children's CB entries that fall into it are gathered instead (the extend-add of
 // the reference's apply_update, chol.hpp:1196) and C = sum(children) - A A^T is written.
-// gv: the hosted rank whose DevPlan (plans[gv]) holds the children.
+// gv: the hosted rank that holds the children.  gb: the task's offset in the gather
+// table's block list (GatherTab.blk: per 64 x 64 block (rb, cb <= rb) of the CB, at
+// gb + rb (rb + 1) / 2 + cb, the block's first segment in GatherTab.seg; the next entry
+// ends it).
 struct GemmTask {
     double* C;
     const double* A;
@@ -72,6 +92,7 @@ struct GemmTask {
     int64_t lda;
     int32_t M, N, K;
     int32_t gs = -1, gv = 0;
+    int64_t gb = -1;
     // General products (the TAG 2 launches of the tall-TRSM-by-inverse panel mode,
     // gemm_tile_body): acc(i, j) = sum_{k < K} A(i, k) B(j, k), A and B column-major
     // (element (r, k) at base[r + k ld]); out(i, j) = Cin(i, j) + sign acc(i, j) (no Cin:
@@ -235,16 +256,16 @@ hipError_t launch_panel_inv(const DevPlan& P, const int2* tasks, int count, hipS
 hipError_t launch_panel_tall(const DevPlan& P, const int4* tasks, int count, hipStream_t st);
 constexpr int TALL_ROWS = 64;  // rows per tall-TRSM workgroup
 
-// plans: the hosted ranks' DevPlans (CB tasks with gs >= 0 gather their children's entries)
+// gt: the gather tables (CB tasks with gs >= 0 gather their children's entries)
 // lean: 64 x 64 tiles with half the LDS (BK = 8; short-K launches, syrk_lean_kmax)
 // tag 2: general products (GemmTask B / Cin / Ct / sign / lower / ktri)
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
-                       int epi = 0, const DevPlan* plans = nullptr, bool lean = false);
+                       int epi = 0, GatherTab gt = {}, bool lean = false);
 // the same SYRK as a resident grid of `grid` workgroups (a multiple of 8) walking the
 // tile list: dispatched at once, so a critical-path launch on another stream finds the
 // slots the grid leaves free instead of queueing behind it
 hipError_t launch_syrk_resident(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag,
-                                hipStream_t st, int epi, const DevPlan* plans, int grid);
+                                hipStream_t st, int epi, GatherTab gt, int grid);
 // full rectangle tiles (general products that are not lower trapezoids)
 void append_tiles_full(std::vector<int2>& out, int task, int M, int N, int bt, int G = 8);
 hipError_t launch_stamp(uint64_t* slot, hipStream_t st);

@@ -208,11 +208,6 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
             }
         }
     }
-    {
-        std::vector<DevPlan> plans;
-        for (const RankMem& R : N.R) plans.push_back(R.P);
-        if ((rc = upload(N, plans, N.d_plans))) return fail(rc);
-    }
 
     SchedBuild B;
     if ((rc = build_schedule(N, B))) return fail(rc);
@@ -275,6 +270,13 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
         }
     }
     B.asml.resize(B.asmv.size(), make_int2(0, INT32_MAX));
+    {  // the CB gather's segment tables
+        int64_t* dgb = nullptr;
+        GSeg* dgs = nullptr;
+        if ((rc = upload(N, B.gblk, dgb)) || (rc = upload(N, B.gseg, dgs))) return fail(rc);
+        N.gtab.blk = dgb;
+        N.gtab.seg = dgs;
+    }
     if ((rc = upload(N, B.small, N.d_small)) || (rc = upload(N, B.asmv, N.d_asm)) || (rc = upload(N, B.asml, N.d_asml)) ||
         (rc = upload(N, B.potrf, N.d_potrf)) || (rc = upload(N, B.trsm, N.d_trsm)) ||
         (rc = upload(N, B.inv, N.d_inv)) || (rc = upload(N, B.tall, N.d_tall)) || (rc = upload(N, B.xinv, N.d_xinv)) ||
@@ -315,9 +317,9 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
         case L_CB:
             if (L.res > 0)
                 return launch_syrk_resident(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0,
-                                            st, L.epi, N.d_plans, L.res);
+                                            st, L.epi, N.gtab, L.res);
             return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st, L.epi,
-                               N.d_plans, L.lean != 0);
+                               N.gtab, L.lean != 0);
         case L_COMM:
             return comm_launch(N, L);
         case L_INV:
@@ -328,7 +330,7 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
             return launch_xinv64(N.R[L.vr].P, N.d_xinv + L.off, L.count, st);
         case L_GEMM:
             if (L.res > 0) return launch_syrk_resident(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, 2, st, 0,
-                                                       nullptr, L.res);
+                                                       GatherTab {}, L.res);
             return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, 2, st);
     }
     return hipErrorInvalidValue;

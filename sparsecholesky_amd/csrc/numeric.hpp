@@ -208,7 +208,7 @@ struct Numeric {
     int32_t* d_arrive = nullptr;  // fused POTRF + TRSM: per-block arrival counters
     GemmTask* d_gemm = nullptr;
     int2* d_tiles = nullptr;
-    DevPlan* d_plans = nullptr;  // the hosted ranks' DevPlans (CB SYRK extend-add gather)
+    GatherTab gtab;              // the CB SYRK extend-add gather's segment tables (schedule.cpp)
     int32_t* d_info = nullptr;       // shared by the hosted ranks' DevPlans
     int32_t* h_info = nullptr;       // pinned host copy, written at the end of each factorization
     static constexpr int32_t STATUS_PENDING = -2;  // h_info before the tiny kernel's status store

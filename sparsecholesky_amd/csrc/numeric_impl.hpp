@@ -89,6 +89,8 @@ struct SchedBuild {
     std::vector<XinvTask> xinv;
     std::vector<GemmTask> gemm;
     std::vector<int2> tiles;
+    std::vector<int64_t> gblk;  // CB gather: per task, per 64 x 64 CB block, its first segment
+    std::vector<GSeg> gseg;
     CommBuild cb;
 };
 

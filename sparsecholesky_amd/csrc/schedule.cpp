@@ -425,6 +425,36 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         if (!multi || k >= (int)slab_step[s].size()) return;
         for (int32_t id : slab_step[s][k]) emit_step(id);
     };
+    // the extend-add gather's segment table of front s on hosted rank v (GSeg): per 64 x 64
+    // block of its CB, every child with CB rows and columns in the block, in child order
+    // (the order the entries are added in); returns the task's offset in B.gblk
+    auto gather_segments = [&](int32_t s, int v) -> int64_t {
+        const int w = S.w(s), mb = S.mb(s), nb = (mb + 63) / 64;
+        const int64_t gb = (int64_t)B.gblk.size();
+        const RankMem& R = N.R[v];
+        for (int rb = 0; rb < nb; ++rb)
+            for (int cbk = 0; cbk <= rb; ++cbk) {
+                B.gblk.push_back((int64_t)B.gseg.size());
+                for (int32_t q = S.child_ptr[s]; q < S.child_ptr[s + 1]; ++q) {
+                    const int32_t c = S.child_list[q];
+                    const int32_t* rel = S.relind.data() + S.rel_ptr[c];
+                    const int mbc = (int)(S.rel_ptr[c + 1] - S.rel_ptr[c]);
+                    auto at = [&](int x) { return (int)(std::lower_bound(rel, rel + mbc, w + x) - rel); };
+                    GSeg g {};
+                    g.ilo = at(64 * rb);
+                    g.ihi = at(std::min(mb, 64 * rb + 64));
+                    g.jlo = at(64 * cbk);
+                    g.jhi = at(std::min(mb, 64 * cbk + 64));
+                    if (g.ilo >= g.ihi || g.jlo >= g.jhi) continue;
+                    g.cb = R.P.cb_pool + R.cb_off[c];
+                    g.rel = R.P.relind + S.rel_ptr[c];
+                    g.mbc = mbc;
+                    B.gseg.push_back(g);
+                }
+            }
+        B.gblk.push_back((int64_t)B.gseg.size());
+        return gb;
+    };
     auto is_early_sender = [&](int32_t s, int v) {
         return multi && D.early[s] && D.owner[s] == N.R[v].rank;
     };
@@ -1019,6 +1049,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 if (gather(s)) {
                     t.gs = s;
                     t.gv = v;
+                    t.gb = gather_segments(s, v);
                 }
                 cbt.push_back(t);
                 fl += (double)mb * (mb + 1.0) * t.K;
