@@ -90,9 +90,14 @@ typedef struct sc_options {
                                 written once); 0: assembly writes the whole front, the SYRK updates it */
     int32_t panel_tall;      /* 1: in a large front wider than 64 columns the 64-column POTRF/TRSM chain runs on
                                 each slab's diagonal-block rows only and the rows below the slab are solved by
-                                one tall-TRSM launch per slab (row blocks, MFMA, block inverses); 0 (default,
-                                measured faster at 128^3: 512 vs 541 ms): every chain step solves and updates
-                                all rows of the front */
+                                one tall-TRSM launch per slab (row blocks, MFMA, block inverses); 2: the rows
+                                below each slab are solved as one MFMA product with X = inv(L11) (64-block
+                                inverses, doubling products); 3: as 2 with two-level lookahead (the near rows
+                                and the next diagonal block on the main stream, the far rows and trailing updates
+                                on the lookahead stream); 4: as 3 with a left-looking trailing update (the slab
+                                after next from every slab so far, one deep-K product); 0 (default, measured
+                                faster at 128^3: 512 vs 541 ms for 1): every chain step solves and updates all
+                                rows of the front */
     int32_t trsm_fold;       /* 1: with the recursive inner order, the span-64 inner update after an even block
                                 of a slab is folded into the next block's fused POTRF/TRSM launch (each
                                 workgroup applies it to its rows and to the diagonal block) instead of being a
@@ -123,6 +128,10 @@ typedef struct sc_options {
     int32_t dist_pieces;     /* multi-GPU distributed panels: each final slab is handed over in this many column
                                 pieces (default 4: 256 of a 1024-column slab), each sent as soon as the chain has
                                 finished it, so the next slab's owner starts updating before the slab is done */
+    int32_t cb_slab;         /* 1: a large front's contribution block is updated slab by slab on the lookahead
+                                stream (CB -= L21_k L21_k^T, K = the slab width, the first pass gathering the
+                                children's entries) while the next slabs are factored, instead of by one K = w
+                                SYRK after the panel; 0 (default): one SYRK after the panel */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

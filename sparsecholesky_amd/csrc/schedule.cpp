@@ -229,7 +229,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // lookahead-stream updates as a resident grid (la_grid): all its workgroups are
         // dispatched at once, so the chain's launches on the main stream are not queued
         // behind the rest of the grid
-        L.res = ((kind == L_PANEL || kind == L_GEMM) && strm == 1 && S.opt.la_grid > 0) ? S.opt.la_grid : 0;
+        L.res = ((kind == L_PANEL || kind == L_GEMM || kind == L_CB) && strm == 1 && S.opt.la_grid > 0) ? S.opt.la_grid : 0;
         if (L.res) L.lean = 0;
         if (kind == L_GEMM) {  // general products: tile by the smaller output edge
             int minMN = INT32_MAX;
@@ -770,6 +770,11 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         auto fold = [&](int32_t s) { return S.opt.trsm_fold && S.opt.inner_order == 1 && !tall(s); };
         const bool tall3 = S.opt.panel_tall >= 3;
         int a3_ev = -1, b3_ev = -1;  // lookahead-stream events of the last slab end (panel_tall = 3)
+        // cb_slab: fronts whose CB is updated slab by slab on the lookahead stream (the
+        // first pass gathers the children's entries, later passes read C)
+        auto cb_slab = [&](int32_t s) {
+            return S.opt.cb_slab && S.mb(s) > 0 && !is_split(s) && !is_early_sender(s, v) && !tall(s);
+        };
         for (int k0 = 0; k0 < maxw; k0 += PNB) {
             Launch Lp {};
             Lp.kind = L_POTRF;
@@ -802,7 +807,8 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             std::vector<int2> tx;              // tall-by-inverse fronts at a slab end: (s, slab0)
             std::vector<GemmTask> outer_a2;    // ... their next-slab updates (general products)
             std::vector<GemmTask> d3, a3, b3;  // panel_tall = 3: next diagonal block, next slab, the rest
-            double uflops = 0.0, afl = 0.0, bfl = 0.0, d3fl = 0.0, a3fl = 0.0, b3fl = 0.0;
+            std::vector<GemmTask> cbs;         // cb_slab: this slab's CB passes
+            double uflops = 0.0, afl = 0.0, bfl = 0.0, d3fl = 0.0, a3fl = 0.0, b3fl = 0.0, cbfl = 0.0;
             for (int32_t s : large) {
                 const int w = S.w(s), m = S.sn_m[s];
                 if (w <= k0) continue;
@@ -877,6 +883,24 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     continue;
                 }
                 if (k1 == slab1 && tallx(s)) tx.push_back(make_int2(s, slab0));
+                if (k1 == slab1 && cb_slab(s)) {  // CB -= L21_k L21_k^T (K = the slab)
+                    const int mb = m - w;
+                    GemmTask t {};
+                    t.C = cb_pool + coff[s];
+                    t.A = pan + (int64_t)slab0 * m + w;
+                    t.ldc = mb;
+                    t.lda = m;
+                    t.M = mb;
+                    t.N = mb;
+                    t.K = slab1 - slab0;
+                    if (slab0 == 0 && gather(s)) {
+                        t.gs = s;
+                        t.gv = v;
+                        t.gb = gather_segments(s, v);
+                    }
+                    cbs.push_back(t);
+                    cbfl += (double)mb * (mb + 1.0) * t.K;
+                }
                 if (k1 == slab1 && slab1 < w) {
                     // outer_a is the last update of block slab1: a pending stream-1 outer
                     // update of those columns is waited for before outer_a runs
@@ -1009,6 +1033,11 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 push_gemm_launch(L_PANEL, lev, outer_b, 0, bfl, 1);
                 b_pending = push_record(1);
             }
+            if (!cbs.empty()) {  // after this slab's outer update, on the lookahead stream
+                if (outer_b.empty()) push_wait(1, push_record(0));
+                push_gemm_launch(L_CB, lev, cbs, 1, cbfl, 1);
+                b_pending = push_record(1);
+            }
         }
         if (b_pending >= 0) push_wait(0, b_pending);
         if (b3_ev >= 0) push_wait(0, b3_ev);  // panel_tall = 3: the lookahead stream's last far rows
@@ -1037,7 +1066,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             double fl = 0.0;
             for (int32_t s : large) {
                 const int w = S.w(s), m = S.sn_m[s], mb = m - w;
-                if (mb <= 0 || (w >= 256) != (big == 1) || is_split(s) || is_early_sender(s, v)) continue;
+                if (mb <= 0 || (w >= 256) != (big == 1) || is_split(s) || is_early_sender(s, v) || cb_slab(s)) continue;
                 GemmTask t {};
                 t.C = cb_pool + coff[s];
                 t.A = panel_pool + poff[s] + w;
