@@ -64,6 +64,37 @@ def comm_model(symb, n, link_gbs, msg_us):
     return out
 
 
+KINDS = {0: "INIT", 1: "SLAB", 2: "DELIVER"}
+
+
+def comm_by_kind(symb, n, link_gbs, msg_us):
+    """GB sent per comm-step kind, and per kind the largest per-rank serialised link time
+    (the comm_model sum restricted to that kind's steps)."""
+    import numpy as np
+
+    st = symb.dist_steps(n)
+    gb = {k: 0.0 for k in KINDS.values()}
+    ms = {k: [] for k in KINDS.values()}
+    for r in range(n):
+        step, peer, nb, snd = symb.dist_schedule(n, r)
+        t = {k: 0.0 for k in KINDS.values()}
+        for a in np.unique(step):
+            sel = step == a
+            kind = KINDS.get(int(st["kind"][a]), str(int(st["kind"][a])))
+            link = {}
+            for p, b, s in zip(peer[sel], nb[sel], snd[sel]):
+                x = link.setdefault(int(p), [0, 0])
+                x[0 if s else 1] += int(b)
+                if s:
+                    gb[kind] = gb.get(kind, 0.0) + int(b) / 1e9
+            t[kind] = t.get(kind, 0.0) + max(max(x) for x in link.values()) / (link_gbs * 1e9) * 1e3 + \
+                sel.sum() * msg_us * 1e-3
+        for k, v in t.items():
+            ms.setdefault(k, []).append(v)
+    return ({k: round(v, 2) for k, v in gb.items()},
+            {k: round(max(v), 1) if v else 0.0 for k, v in ms.items()})
+
+
 def rank_timeline(num):
     """From one eager profiled factorization of a dry handle: (total ms, post[step],
     need[step]) -- the step's comm-stream start, and the start of the first main-stream
@@ -142,7 +173,9 @@ def main():
         symb = sc.Symbolic(sc.laplacian3d(args.k), **kw)
         for n in [int(x) for x in args.n.split(",")]:
             cm = comm_model(symb, n, args.link_gbs, args.msg_us)
-            print(json.dumps({"k": args.k, "n": n, "opts": kw, "link_GBs": args.link_gbs, **cm}), flush=True)
+            gbk, msk = comm_by_kind(symb, n, args.link_gbs, args.msg_us)
+            print(json.dumps({"k": args.k, "n": n, "opts": kw, "link_GBs": args.link_gbs, **cm,
+                              "sent_GB_by_kind": gbk, "serial_link_ms_max_rank_by_kind": msk}), flush=True)
         return
     import torch
 
