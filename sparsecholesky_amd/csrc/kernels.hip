@@ -1522,7 +1522,7 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const in
     static_assert(BT * GLD <= OPS, "gather chunk fits the operand LDS");
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wr = wid / WN, wc = wid % WN;
-    const int w = T.K;
+    const int w = T.gw;
     const int mb = T.M;
     const int nb = (mb + 63) >> 6;
     const int64_t* __restrict__ blk = gblk + T.gb;

@@ -93,6 +93,7 @@ struct GemmTask {
     int32_t M, N, K;
     int32_t gs = -1, gv = 0;
     int64_t gb = -1;
+    int32_t gw = 0;  // gathering tasks: the front's width (the CB starts at front row gw; K may be one slab)
     // General products (the TAG 2 launches of the tall-TRSM-by-inverse panel mode,
     // gemm_tile_body): acc(i, j) = sum_{k < K} A(i, k) B(j, k), A and B column-major
     // (element (r, k) at base[r + k ld]); out(i, j) = Cin(i, j) + sign acc(i, j) (no Cin:

@@ -770,6 +770,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         auto fold = [&](int32_t s) { return S.opt.trsm_fold && S.opt.inner_order == 1 && !tall(s); };
         const bool tall3 = S.opt.panel_tall >= 3;
         int a3_ev = -1, b3_ev = -1;  // lookahead-stream events of the last slab end (panel_tall = 3)
+        int cb_pending = -1;         // cb_slab: the lookahead stream's last CB pass
         // cb_slab: fronts whose CB is updated slab by slab on the lookahead stream (the
         // first pass gathers the children's entries, later passes read C)
         auto cb_slab = [&](int32_t s) {
@@ -897,6 +898,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                         t.gs = s;
                         t.gv = v;
                         t.gb = gather_segments(s, v);
+                        t.gw = w;
                     }
                     cbs.push_back(t);
                     cbfl += (double)mb * (mb + 1.0) * t.K;
@@ -1036,11 +1038,12 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             if (!cbs.empty()) {  // after this slab's outer update, on the lookahead stream
                 if (outer_b.empty()) push_wait(1, push_record(0));
                 push_gemm_launch(L_CB, lev, cbs, 1, cbfl, 1);
-                b_pending = push_record(1);
+                cb_pending = push_record(1);  // joined at the level end (the chain never waits for it)
             }
         }
         if (b_pending >= 0) push_wait(0, b_pending);
         if (b3_ev >= 0) push_wait(0, b3_ev);  // panel_tall = 3: the lookahead stream's last far rows
+        if (cb_pending >= 0) push_wait(0, cb_pending);
         // early-delivery children: the CB SYRK in column groups, an event after each
         // (the group's comm sub-step waits for exactly that event)
         for (int32_t s : large) {
@@ -1079,6 +1082,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     t.gs = s;
                     t.gv = v;
                     t.gb = gather_segments(s, v);
+                    t.gw = w;
                 }
                 cbt.push_back(t);
                 fl += (double)mb * (mb + 1.0) * t.K;
