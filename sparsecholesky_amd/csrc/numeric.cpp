@@ -293,25 +293,25 @@ static hipStream_t stream_of(const Numeric& N, int strm) {
 }
 
 static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
-    hipStream_t st = stream_of(N, L.strm);
+    hipStream_t st = stream_of(N, L.strm);  // every kind on the stream its schedule entry names
     switch (L.kind) {
         case L_RECORD:
             return hipEventRecord(N.sync_ev[L.count], st);
         case L_WAIT:
             return hipStreamWaitEvent(st, N.sync_ev[L.count], 0);
         case L_SMALL:
-            if (L.big == 1) return launch_front_chain(N.R[L.vr].P, N.CP, (int)L.off, L.count, L.maxm, d_Ax, N.stream);
-            if (L.big == 2) return launch_tiny_tree(N.R[L.vr].P, N.TP, L.maxm, d_Ax, N.stream);
-            if (L.big == 3) return launch_tiny_dense(N.R[L.vr].P, N.TP, L.maxm, d_Ax, N.stream);
-            return launch_front_small(N.R[L.vr].P, N.d_small + L.off, L.count, L.maxm, false, d_Ax, N.stream);
+            if (L.big == 1) return launch_front_chain(N.R[L.vr].P, N.CP, (int)L.off, L.count, L.maxm, d_Ax, st);
+            if (L.big == 2) return launch_tiny_tree(N.R[L.vr].P, N.TP, L.maxm, d_Ax, st);
+            if (L.big == 3) return launch_tiny_dense(N.R[L.vr].P, N.TP, L.maxm, d_Ax, st);
+            return launch_front_small(N.R[L.vr].P, N.d_small + L.off, L.count, L.maxm, false, d_Ax, st);
         case L_ASM:
             // epi = 1: distributed-assembly launch, column limits parallel to the tasks
-            return launch_assemble_large(N.R[L.vr].P, N.d_asm + L.off, L.count, d_Ax, N.stream, L.big != 0,
+            return launch_assemble_large(N.R[L.vr].P, N.d_asm + L.off, L.count, d_Ax, st, L.big != 0,
                                          L.epi ? N.d_asml + L.off : nullptr);
         case L_POTRF:
-            return launch_potrf_diag(N.R[L.vr].P, N.d_potrf + L.off, L.count, N.stream);
+            return launch_potrf_diag(N.R[L.vr].P, N.d_potrf + L.off, L.count, st);
         case L_TRSM:
-            return launch_trsm_panel(N.R[L.vr].P, N.d_trsm + L.off, L.count, N.stream, L.big != 0, N.d_arrive,
+            return launch_trsm_panel(N.R[L.vr].P, N.d_trsm + L.off, L.count, st, L.big != 0, N.d_arrive,
                                      L.epi);
         case L_PANEL:
         case L_CB:
@@ -323,9 +323,9 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
         case L_COMM:
             return comm_launch(N, L);
         case L_INV:
-            return launch_panel_inv(N.R[L.vr].P, N.d_inv + L.off, L.count, N.stream);
+            return launch_panel_inv(N.R[L.vr].P, N.d_inv + L.off, L.count, st);
         case L_TALL:
-            return launch_panel_tall(N.R[L.vr].P, N.d_tall + L.off, L.count, N.stream);
+            return launch_panel_tall(N.R[L.vr].P, N.d_tall + L.off, L.count, st);
         case L_XINV:
             return launch_xinv64(N.R[L.vr].P, N.d_xinv + L.off, L.count, st);
         case L_GEMM:
