@@ -924,6 +924,11 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                             gen_update(outer_a2, afl, pan + (int64_t)n1 * m + n1, m, pan + (int64_t)n1 * m + n1, m,
                                        pan + (int64_t)slab0 * m + n1, m, pan + (int64_t)slab0 * m + n1, m, m - n1,
                                        nxt - n1, K, true);
+                    } else if (S.opt.lookahead == 2) {
+                        // left-looking: only the next slab, by every slab so far (one deep-K
+                        // product on the main stream; the chain then has the GPU to itself)
+                        add_update(outer_a, afl, pan, m, m, slab1, std::min(w, slab1 + NBO), 0, slab1);
+                        continue;
                     } else {
                         add_update(outer_a, afl, pan, m, m, slab1, nxt, slab0, slab1);
                     }
