@@ -133,6 +133,9 @@ typedef struct sc_options {
                                 stream (CB -= L21_k L21_k^T, K = the slab width, the first pass gathering the
                                 children's entries) while the next slabs are factored, instead of by one K = w
                                 SYRK after the panel; 0 (default): one SYRK after the panel */
+    int32_t cb_gather_min_w; /* with cb_gather: only fronts at least this wide gather their children's entries in the
+                                CB SYRK; narrower fronts (short-K CB launches) are assembled whole and their SYRK
+                                updates C in place (default 0: every large front gathers) */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

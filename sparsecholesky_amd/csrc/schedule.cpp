@@ -697,7 +697,10 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         if (large.empty()) return;
         // fronts whose CB SYRK gathers the children's CB entries itself (one CB launch
         // task covering the whole CB): their assembly stops at the panel columns
-        auto gather = [&](int32_t s) { return S.opt.cb_gather && S.mb(s) > 0 && !is_split(s) && !is_early_sender(s, v); };
+        auto gather = [&](int32_t s) {
+            return S.opt.cb_gather && S.mb(s) > 0 && S.w(s) >= S.opt.cb_gather_min_w && !is_split(s) &&
+                   !is_early_sender(s, v);
+        };
         // assembly: fronts with m >= ASM_TILE_MIN_M one workgroup per (front, 16
         // columns, 256-row tile), write-once (big = 1); smaller fronts one workgroup per
         // (front, 16 columns) streaming child columns (measured faster below ~8k rows)

@@ -763,7 +763,8 @@ PANEL_OPTS = [dict(inner_order=0), dict(inner_order=0, lookahead=0), dict(lookah
               dict(cb_slab=1), dict(cb_slab=1, panel_nb_outer=128), dict(cb_slab=1, cb_gather=0, panel_nb_outer=128),
               dict(cb_slab=1, la_grid=64, panel_nb_outer=192), dict(cb_slab=1, lookahead=0, panel_nb_outer=128),
               dict(lookahead=2), dict(lookahead=2, panel_nb_outer=128), dict(lookahead=2, panel_nb_outer=192, inner_order=0),
-              dict(lookahead=2, panel_tall=1, panel_nb_outer=128)]
+              dict(lookahead=2, panel_tall=1, panel_nb_outer=128), dict(cb_gather_min_w=64),
+              dict(cb_gather_min_w=100000)]
 
 
 @pytest.mark.parametrize("opts", PANEL_OPTS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
