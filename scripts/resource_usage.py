@@ -2,7 +2,7 @@
 """Per-kernel VGPR / AGPR / scratch / occupancy of a HIP source compiled for gfx950
 (hipcc -Rpass-analysis=kernel-resource-usage), one line per kernel.
 
-  python scripts/resource_usage.py [kernels.hip] [name-filter]
+  [SC_FLAGS="-DX=1"] python scripts/resource_usage.py [kernels.hip] [name-filter]
 """
 import os
 import re
@@ -14,7 +14,7 @@ src = os.path.abspath(sys.argv[1]) if len(sys.argv) > 1 else os.path.join(ROOT, 
 filt = sys.argv[2] if len(sys.argv) > 2 else ""
 cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-munsafe-fp-atomics",
        "-I" + os.path.join(ROOT, "include"), "-x", "hip", "-c", src, "-o", "/tmp/resource_usage.o",
-       "--offload-device-only", "-Rpass-analysis=kernel-resource-usage"]
+       "--offload-device-only", "-Rpass-analysis=kernel-resource-usage"] + os.environ.get("SC_FLAGS", "").split()
 out = subprocess.run(cmd, capture_output=True, text=True, cwd=os.path.dirname(os.path.abspath(src))).stderr
 cur = None
 rows = {}
