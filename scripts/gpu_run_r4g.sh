@@ -1,6 +1,6 @@
 export TMPDIR=/tmp; mkdir -p gpurun_out
 # CB / panel SYRK K loop with LDS-DMA operand stages (SC_GLDS) against the same build without
-timeout -k 10 500 bash scripts/gpu.sh ab def glds || exit 1
+timeout -k 10 700 bash scripts/gpu.sh ab def glds glds2 || exit 1
 # tiny dense: factor-twice probe and the LDS-resident variant
 timeout -k 10 400 bash scripts/gpu.sh tiny td_p2 td_lds || exit 1
 # distributed plan parity (slab pieces included)

@@ -1722,15 +1722,17 @@ __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t
 #define SC_GLDS 0
 #endif
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
-template <int BT, int WM, int WN, int BK = 16>
+template <int BT, int WM, int WN, int BK = 16, int NS = 2>
 __device__ __forceinline__ void mfma_kloop_glds(const double* __restrict__ A, int64_t lda, int K, int M, int N, int row0,
                                                 int col0, double4_t (&acc)[BT / WM / 16][BT / WN / 16], double* smem) {
     static_assert(BT == 128, "one 1-KB wave-instruction per k-row");
+    static_assert(NS >= 2, "at least double-buffered");
     constexpr int NW = WM * WN;
     constexpr int LDT = BT + 16;
     constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
-    double(*As)[BK * LDT] = reinterpret_cast<double(*)[BK * LDT]>(smem);
-    double(*Bs)[BK * LDT] = reinterpret_cast<double(*)[BK * LDT]>(smem + 2 * BK * LDT);
+    constexpr int DPS = 2 * (BK / NW);  // DMA instructions per wave per stage
+    double* As = smem;                  // stage s: As + s * BK * LDT
+    double* Bs = smem + NS * BK * LDT;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = tid >> 6;
@@ -1745,26 +1747,37 @@ __device__ __forceinline__ void mfma_kloop_glds(const double* __restrict__ A, in
             const int kk = wid + i * NW;
             const int va = (kk < nrow && ra < M) ? (int)((ra + kk * lda) * 8) : BUF_DEAD;
             const int vb = (kk < nrow && rb < N) ? (int)((rb + kk * lda) * 8) : BUF_DEAD;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(As[buf] + kk * LDT), 16, va, 0, 0, 0);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(Bs[buf] + kk * LDT), 16, vb, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(As + (buf * BK + kk) * LDT), 16, va, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(Bs + (buf * BK + kk) * LDT), 16, vb, 0, 0, 0);
         }
     };
     const int nk = (K + BK - 1) / BK;
-    dma(0, 0);
+#pragma unroll
+    for (int st = 0; st < NS - 1; ++st)
+        if (st < nk) dma(st * BK, st);
     for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of stage kt landed
-        __syncthreads();  // every wave's DMA landed; every wave is done with buffer cur ^ 1
-        if (kt + 1 < nk) dma((kt + 1) * BK, cur ^ 1);
+        const int cur = kt % NS;
+        // stage kt landed (this wave's DMA): later stages (up to NS - 2) may stay in flight
+        if (NS == 2 || kt + NS - 2 >= nk) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if constexpr (NS > 2) {
+            static_assert(DPS * (NS - 2) <= 63, "vmcnt range");
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS * (NS - 2)) : "memory");
+        }
+        // every wave's DMA of stage kt landed; every wave is done with the buffer refilled
+        // next (raw barrier: a __syncthreads() would drain the DMAs still in flight)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (kt + NS - 1 < nk) dma((kt + NS - 1) * BK, (kt + NS - 1) % NS);
+        const double* Ac = As + cur * BK * LDT;
+        const double* Bc = Bs + cur * BK * LDT;
         double av[2][RTM], bv[2][RTN];
         auto lread = [&](int kk, int slot) {
             const int krow = kk + (lane >> 4);
 #pragma unroll
-            for (int a = 0; a < RTM; ++a)
-                av[slot][a] = As[cur][krow * LDT + wr * (BT / WM) + a * 16 + (lane & 15)];
+            for (int a = 0; a < RTM; ++a) av[slot][a] = Ac[krow * LDT + wr * (BT / WM) + a * 16 + (lane & 15)];
 #pragma unroll
-            for (int b = 0; b < RTN; ++b)
-                bv[slot][b] = Bs[cur][krow * LDT + wc * (BT / WN) + b * 16 + (lane & 15)];
+            for (int b = 0; b < RTN; ++b) bv[slot][b] = Bc[krow * LDT + wc * (BT / WN) + b * 16 + (lane & 15)];
         };
         lread(0, 0);
 #pragma unroll
@@ -1778,7 +1791,7 @@ __device__ __forceinline__ void mfma_kloop_glds(const double* __restrict__ A, in
                     acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[slot][a], bv[slot][b], acc[a][b], 0, 0, 0);
         }
     }
-    __syncthreads();  // the epilogue reuses the stages' LDS
+    __syncthreads();  // the epilogue reuses the stages' LDS (no DMA is in flight here)
 }
 
 // LEAN (short-K launches on 64 x 64 tiles): BK = 8 and 32-row gather chunks halve the
@@ -1812,8 +1825,10 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
     for (int a = 0; a < RTM; ++a)
 #pragma unroll
         for (int b = 0; b < RTN; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
-    if constexpr (SC_GLDS && BT == 128)
-        mfma_kloop_glds<BT, WM, WN, BK>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
+    if constexpr (SC_GLDS == 1 && BT == 128)
+        mfma_kloop_glds<BT, WM, WN, BK, 2>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
+    else if constexpr (SC_GLDS == 2 && BT == 128)  // four stages of 8 k (the same LDS)
+        mfma_kloop_glds<BT, WM, WN, BK / 2, 4>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
     else
         mfma_kloop<BT, WM, WN, 0, BK>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
 
