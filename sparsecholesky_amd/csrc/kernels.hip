@@ -787,7 +787,7 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 #ifndef SC_TD_PROBE
-#define SC_TD_PROBE 0  // timing probes (scripts/tiny_probe.py): 1 no factorization, 2 factor twice
+#define SC_TD_PROBE 0  // timing probe (scripts/tiny_probe.py): 1 = loads and stores only, no factorization
 #endif
 // raw[4 * r .. 4 * r + 3] = step columns of row r (published) -> D and its factor
 __device__ __forceinline__ void td_factor_d(const double* raw, int J, double (&Ld)[4][4], double (&rc)[4], int& bad) {
@@ -951,23 +951,17 @@ __global__ __launch_bounds__(64) void tiny_dense_kernel(DevPlan P, TinyPlan T, i
     int fail = n;
     double Ld[4][4], rc[4];
     int bad;
-    // probe 2: the same factorization twice through the same code (the second pass with
-    // the instruction cache warm)
-#pragma nounroll
-    for (int pass = 0; pass < (SC_TD_PROBE == 2 ? 2 : 1); ++pass) {
 #pragma unroll
-        for (int j = 0; j < NP; ++j) a[j] = q[j].x >= 0 ? Ax[q[j].x] : 0.0;
+    for (int j = 0; j < NP; ++j) a[j] = q[j].x >= 0 ? Ax[q[j].x] : 0.0;
 #pragma unroll
-        for (int j = 0; j < NP; ++j) a[j] = (i == j && i >= n) ? 1.0 : a[j];  // identity padding
-        fail = n;
-        if (SC_TD_PROBE != 1) {
-            wave_lds_sync();
-            *reinterpret_cast<double2*>(raw + 4 * i) = make_double2(a[0], a[1]);
-            *reinterpret_cast<double2*>(raw + 4 * i + 2) = make_double2(a[2], a[3]);
-            wave_lds_sync();
-            td_factor_d(raw, 0, Ld, rc, bad);
-            td_steps<NP, 0>(a, Ld, rc, bad, fail, raw, lv, i);
-        }
+    for (int j = 0; j < NP; ++j) a[j] = (i == j && i >= n) ? 1.0 : a[j];  // identity padding
+    if (SC_TD_PROBE != 1) {
+        wave_lds_sync();
+        *reinterpret_cast<double2*>(raw + 4 * i) = make_double2(a[0], a[1]);
+        *reinterpret_cast<double2*>(raw + 4 * i + 2) = make_double2(a[2], a[3]);
+        wave_lds_sync();
+        td_factor_d(raw, 0, Ld, rc, bad);
+        td_steps<NP, 0>(a, Ld, rc, bad, fail, raw, lv, i);
     }
     if (fail > n) fail = n;  // padding pivots never fail; a failure at or past n is none
 #pragma unroll
@@ -988,125 +982,9 @@ __global__ __launch_bounds__(64) void tiny_dense_kernel(DevPlan P, TinyPlan T, i
     }
 }
 
-// Tiny dense, LDS-resident variant (SC_TD_LDS = 1): the matrix in LDS column by column
-// (Dm[j * 64 + i], lane i = row i: conflict-free), the four-pivot steps a rolled loop
-// (a few hundred bytes of code, warm in the instruction cache after the first step,
-// where the register variant streams ~40 KB of straight-line code per launch).  Per
-// step every lane factors the 4 x 4 diagonal block (broadcast LDS reads), solves and
-// publishes its row of the step panel, then updates its row of every later column.
-#ifndef SC_TD_LDS
-#define SC_TD_LDS 0
-#endif
-template <int NP>
-__global__ __launch_bounds__(64) void tiny_dense_lds_kernel(DevPlan P, TinyPlan T, int n, const double* __restrict__ Ax) {
-    __shared__ __attribute__((aligned(16))) double Dm[NP * 64];
-    __shared__ __attribute__((aligned(16))) double lv[NP * 4];
-    __shared__ int po[NP * 64];
-    const int i = threadIdx.x;
-    {
-        int2 q[NP];
-#pragma unroll
-        for (int j = 0; j < NP; ++j) q[j] = T.a[j * 64 + i];
-        double a[NP];
-#pragma unroll
-        for (int j = 0; j < NP; ++j) a[j] = q[j].x >= 0 ? Ax[q[j].x] : 0.0;
-#pragma unroll
-        for (int j = 0; j < NP; ++j) {
-            Dm[j * 64 + i] = (i == j && i >= n) ? 1.0 : a[j];  // identity padding
-            po[j * 64 + i] = q[j].y;
-        }
-    }
-    wave_lds_sync();
-    int fail = n;
-#pragma unroll 1
-    for (int J = 0; J < NP; J += 4) {
-        // the 4 x 4 diagonal block (rows J.., columns J..; broadcast reads) and its factor
-        double Ld[4][4], rc[4];
-        int bad = 4;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            double dd = Dm[(J + c) * 64 + J + c];
-#pragma unroll
-            for (int t = 0; t < c; ++t) dd = fma(-Ld[c][t], Ld[c][t], dd);
-            if (!(dd > 0.0)) bad = min(bad, c);
-            rc[c] = rsqrt_f64(dd);
-            Ld[c][c] = dd * rc[c];
-#pragma unroll
-            for (int r = c + 1; r < 4; ++r) {
-                double x = Dm[(J + c) * 64 + J + r];
-#pragma unroll
-                for (int t = 0; t < c; ++t) x = fma(-Ld[r][t], Ld[c][t], x);
-                Ld[r][c] = x * rc[c];
-            }
-        }
-        if (bad < 4) fail = min(fail, J + bad);
-        // this lane's row of the step panel: l = a[J..J+3] L_D^-T (rows below the block)
-        const bool below = i >= J + 4;
-        double l[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            double x = below ? Dm[(J + k) * 64 + i] : 0.0;
-#pragma unroll
-            for (int t = 0; t < k; ++t) x = fma(-l[t], Ld[k][t], x);
-            l[k] = x * rc[k];
-        }
-        *reinterpret_cast<double2*>(lv + 4 * i) = make_double2(l[0], l[1]);
-        *reinterpret_cast<double2*>(lv + 4 * i + 2) = make_double2(l[2], l[3]);
-        // the step's columns become final: L_D (the block's rows) or l (below)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            double v = below ? l[c] : Dm[(J + c) * 64 + i];
-#pragma unroll
-            for (int r = c; r < 4; ++r) v = i == J + r ? Ld[r][c] : v;
-            Dm[(J + c) * 64 + i] = v;
-        }
-        wave_lds_sync();  // every lane's l published
-        // rank-4 update of this lane's row in every later column (entries above the
-        // diagonal are updated too and never read)
-#pragma unroll 2
-        for (int jj = J + 4; jj < NP; ++jj) {
-            const double2 x01 = *reinterpret_cast<const double2*>(lv + 4 * jj);
-            const double2 x23 = *reinterpret_cast<const double2*>(lv + 4 * jj + 2);
-            double y = Dm[jj * 64 + i];
-            y = fma(-l[0], x01.x, y);
-            y = fma(-l[1], x01.y, y);
-            y = fma(-l[2], x23.x, y);
-            y = fma(-l[3], x23.y, y);
-            Dm[jj * 64 + i] = y;
-        }
-        wave_lds_sync();  // the next step's reads see the update; lv free again
-    }
-    if (fail > n) fail = n;  // padding pivots never fail; a failure at or past n is none
-#pragma unroll 4
-    for (int j = 0; j < NP; ++j) {
-        const int o = po[j * 64 + i];
-        if (o >= 0) P.panel_pool[o] = Dm[j * 64 + i];
-    }
-    if (i == 0) {
-        if (T.host_info) {
-            const int32_t st = fail < n ? fail + 1 : 0x7f7f7f7f;
-            P.info[0] = st;
-            __hip_atomic_store(T.host_info, st, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        } else if (fail < n) {
-            report_fail(P.info, fail);
-        }
-    }
-}
-
 hipError_t launch_tiny_dense(const DevPlan& P, const TinyPlan& T, int n, const double* Ax, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     if (n > TINY_DENSE_N || T.na != tiny_dense_np(n) * 64) return hipErrorInvalidValue;  // the lane map's shape
-    if (SC_TD_LDS) {
-        if (n <= 16)
-            hipLaunchKernelGGL(tiny_dense_lds_kernel<16>, dim3(1), dim3(64), 0, st, P, T, n, Ax);
-        else if (n <= 32)
-            hipLaunchKernelGGL(tiny_dense_lds_kernel<32>, dim3(1), dim3(64), 0, st, P, T, n, Ax);
-        else if (n <= 48)
-            hipLaunchKernelGGL(tiny_dense_lds_kernel<48>, dim3(1), dim3(64), 0, st, P, T, n, Ax);
-        else
-            hipLaunchKernelGGL(tiny_dense_lds_kernel<64>, dim3(1), dim3(64), 0, st, P, T, n, Ax);
-        return hipGetLastError();
-    }
     if (n <= 16)
         hipLaunchKernelGGL(tiny_dense_kernel<16>, dim3(1), dim3(64), 0, st, P, T, n, Ax);
     else if (n <= 32)
