@@ -149,7 +149,10 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
     auto is_dpanel = [&](int32_t s) { return multi && D.pd[s] >= 0; };
     std::vector<int32_t> hosted_of((size_t)std::max(N.nranks, 1), -1);  // rank -> index into N.R
     for (size_t v = 0; v < N.R.size(); ++v) hosted_of[N.R[v].rank] = (int32_t)v;
-    std::vector<int32_t> init_step, early_step0, deliver_step((size_t)S.nlevels, -1);
+    std::vector<int32_t> init_step, deliver_step((size_t)S.nlevels, -1);
+    // early children: early_step[c][g] = the DELIVER step of column group g (-1: none; a
+    // group whose columns all stay on the producer has no messages and no step)
+    std::vector<std::vector<int32_t>> early_step;
     // split fronts / distributed panels: slab_step[s][k] = the steps of slab k's pieces (dist_pieces)
     std::vector<std::vector<std::vector<int32_t>>> slab_step;
     std::vector<std::vector<int>> early_ev((size_t)S.ns);  // sender: event after each CB column group
@@ -158,7 +161,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
     if (multi) {
         init_step.assign((size_t)S.ns, -1);
         slab_step.assign((size_t)S.ns, {});
-        early_step0.assign((size_t)S.ns, -1);
+        early_step.assign((size_t)S.ns, {});
         for (int32_t id = 0; id < (int32_t)D.steps.size(); ++id) {
             const DistStep& t = D.steps[id];
             if (t.kind == STEP_INIT) init_step[t.s] = id;
@@ -169,7 +172,11 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 ks[t.k][t.p] = id;
             }
             if (t.kind == STEP_DELIVER && t.s < 0) deliver_step[t.level] = id;
-            if (t.kind == STEP_DELIVER && t.s >= 0 && t.k == 0) early_step0[t.s] = id;
+            if (t.kind == STEP_DELIVER && t.s >= 0) {
+                auto& es = early_step[t.s];
+                if ((int)es.size() <= t.k) es.resize((size_t)t.k + 1, -1);
+                es[t.k] = id;
+            }
         }
         step_beg.assign(D.steps.size() + 1, 0);
         for (const DistMsg& g : D.msgs) step_beg[g.step + 1]++;
@@ -1437,11 +1444,12 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // contribution blocks that leave / enter the hosted ranks after this level:
         // early children's column groups first, then the rest
         for (int32_t c : by_level[lev]) {
-            if (!D.early[c] || early_step0[c] < 0) continue;
+            if (!D.early[c] || early_step[c].empty()) continue;
             const int ng = (S.mb(c) + D.early_gw - 1) / D.early_gw;
             const int vs = hosted_of[D.owner[c]];
             for (int g = 0; g < ng; ++g)
-                emit_step(early_step0[c] + g, vs >= 0 && !early_ev[c].empty() ? early_ev[c][g] : -1);
+                if (g < (int)early_step[c].size())
+                    emit_step(early_step[c][g], vs >= 0 && !early_ev[c].empty() ? early_ev[c][g] : -1);
         }
         emit_step(deliver_step[lev]);
         comm_done[lev] = push_record(2);
