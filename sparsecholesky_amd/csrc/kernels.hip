@@ -1588,90 +1588,6 @@ __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t
     }
 }
 
-// The same K loop with the operand stages written by LDS-DMA (SC_GLDS = 1, 128-tiles of
-// the single-operand SYRK): every k-row of a stage is 128 consecutive doubles of A's
-// column (1 KB), one buffer_load_dwordx4 ... lds per wave-instruction into its padded LDS
-// row (lane-linear, no row crossing).  No staging registers and no ds_write pass; the
-// next stage's DMA is issued right after the barrier that frees its buffer and lands
-// under this stage's MFMAs.  Rows past M read whatever follows in the column (finite
-// panel entries) or 0 past the stage's range: they only feed accumulator rows / columns
-// that are never stored.
-#ifndef SC_GLDS
-#define SC_GLDS 0
-#endif
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-template <int BT, int WM, int WN, int BK = 16, int NS = 2>
-__device__ __forceinline__ void mfma_kloop_glds(const double* __restrict__ A, int64_t lda, int K, int M, int N, int row0,
-                                                int col0, double4_t (&acc)[BT / WM / 16][BT / WN / 16], double* smem) {
-    static_assert(BT == 128, "one 1-KB wave-instruction per k-row");
-    static_assert(NS >= 2, "at least double-buffered");
-    constexpr int NW = WM * WN;
-    constexpr int LDT = BT + 16;
-    constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
-    constexpr int DPS = 2 * (BK / NW);  // DMA instructions per wave per stage
-    double* As = smem;                  // stage s: As + s * BK * LDT
-    double* Bs = smem + NS * BK * LDT;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wid = tid >> 6;
-    const int wr = wid / WN, wc = wid % WN;
-    auto dma = [&](int k0, int buf) {
-        const int nrow = min(BK, K - k0);
-        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(A + (int64_t)k0 * lda, (uint32_t)(nrow * lda * 8 + 16));
-        const int ra = row0 + 2 * lane, rb = col0 + 2 * lane;
-        static_assert(BK % NW == 0, "every wave moves the same number of k-rows");
-#pragma unroll
-        for (int i = 0; i < BK / NW; ++i) {
-            const int kk = wid + i * NW;
-            const int va = (kk < nrow && ra < M) ? (int)((ra + kk * lda) * 8) : BUF_DEAD;
-            const int vb = (kk < nrow && rb < N) ? (int)((rb + kk * lda) * 8) : BUF_DEAD;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(As + (buf * BK + kk) * LDT), 16, va, 0, 0, 0);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(Bs + (buf * BK + kk) * LDT), 16, vb, 0, 0, 0);
-        }
-    };
-    const int nk = (K + BK - 1) / BK;
-#pragma unroll
-    for (int st = 0; st < NS - 1; ++st)
-        if (st < nk) dma(st * BK, st);
-    for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt % NS;
-        // stage kt landed (this wave's DMA): later stages (up to NS - 2) may stay in flight
-        if (NS == 2 || kt + NS - 2 >= nk) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else if constexpr (NS > 2) {
-            static_assert(DPS * (NS - 2) <= 63, "vmcnt range");
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS * (NS - 2)) : "memory");
-        }
-        // every wave's DMA of stage kt landed; every wave is done with the buffer refilled
-        // next (raw barrier: a __syncthreads() would drain the DMAs still in flight)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (kt + NS - 1 < nk) dma((kt + NS - 1) * BK, (kt + NS - 1) % NS);
-        const double* Ac = As + cur * BK * LDT;
-        const double* Bc = Bs + cur * BK * LDT;
-        double av[2][RTM], bv[2][RTN];
-        auto lread = [&](int kk, int slot) {
-            const int krow = kk + (lane >> 4);
-#pragma unroll
-            for (int a = 0; a < RTM; ++a) av[slot][a] = Ac[krow * LDT + wr * (BT / WM) + a * 16 + (lane & 15)];
-#pragma unroll
-            for (int b = 0; b < RTN; ++b) bv[slot][b] = Bc[krow * LDT + wc * (BT / WN) + b * 16 + (lane & 15)];
-        };
-        lread(0, 0);
-#pragma unroll
-        for (int kk = 0; kk < BK; kk += 4) {
-            const int slot = (kk / 4) & 1;
-            if (kk + 4 < BK) lread(kk + 4, slot ^ 1);
-#pragma unroll
-            for (int a = 0; a < RTM; ++a)
-#pragma unroll
-                for (int b = 0; b < RTN; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[slot][a], bv[slot][b], acc[a][b], 0, 0, 0);
-        }
-    }
-    __syncthreads();  // the epilogue reuses the stages' LDS (no DMA is in flight here)
-}
-
 // LEAN (short-K launches on 64 x 64 tiles): BK = 8 and 32-row gather chunks halve the
 // LDS (20 KB), so six workgroups fit a CU instead of four -- these launches are latency-
 // bound (a few K stages, then the C traffic), not MFMA-bound
@@ -1703,12 +1619,9 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
     for (int a = 0; a < RTM; ++a)
 #pragma unroll
         for (int b = 0; b < RTN; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
-    if constexpr (SC_GLDS == 1 && BT == 128)
-        mfma_kloop_glds<BT, WM, WN, BK, 2>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
-    else if constexpr (SC_GLDS == 2 && BT == 128)  // four stages of 8 k (the same LDS)
-        mfma_kloop_glds<BT, WM, WN, BK / 2, 4>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
-    else
-        mfma_kloop<BT, WM, WN, 0, BK>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
+    // (operand stages by LDS-DMA, buffer_load_dwordx4 ... lds per 1-KB k-row, measured
+    // slower: 510.5 ms with two 16-deep stages, 521.5 with four 8-deep, vs 505.7-507.3)
+    mfma_kloop<BT, WM, WN, 0, BK>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
 
     if constexpr (TAG == 1) {
         if (T.gs >= 0) {  // the front's CB is not assembled: gather the children's entries
