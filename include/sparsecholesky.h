@@ -70,7 +70,9 @@ typedef struct sc_options {
     int32_t syrk_tile;       /* 0 = auto (128x128/8 waves for wide, deep updates, else 64x64/4 waves); 64; 128 */
     int32_t lookahead;       /* 0: none; 1 (default): trailing panel updates on a 2nd stream, overlapping the
                                 next slab's POTRF/TRSM chain; 2: left-looking -- at each slab end only the next
-                                slab is updated, by every slab so far (one deep-K product), on the main stream */
+                                slab is updated, by every slab so far (one deep-K product), on the main stream;
+                                3: the next slab by the slab just finished (main stream) and the slab after next by
+                                every slab so far (lookahead stream, one deep-K product) */
     int32_t inner_order;     /* updates inside a slab: 0 right-looking (K = 64), 1 recursive (K = 64..NBO/2) */
     int32_t asm_tile_min_m;  /* fronts with m >= this use the write-once tiled assembly (0 = default 8192) */
     int32_t dist_split;      /* multi-GPU: a shared front with a contribution block keeps its panel on one rank and

@@ -939,6 +939,14 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                         // product on the main stream; the chain then has the GPU to itself)
                         add_update(outer_a, afl, pan, m, m, slab1, std::min(w, slab1 + NBO), 0, slab1);
                         continue;
+                    } else if (S.opt.lookahead == 3) {
+                        // the next slab by this slab (main stream), and only the slab after next
+                        // by every slab so far (lookahead stream: one deep-K product whose grid
+                        // fits the GPU at once, so the chain's launches do not queue behind it)
+                        const int n1 = std::min(w, slab1 + NBO);
+                        add_update(outer_a, afl, pan, m, m, slab1, n1, slab0, slab1);
+                        add_update(outer_b, bfl, pan, m, m, n1, std::min(w, n1 + NBO), 0, slab1);
+                        continue;
                     } else {
                         add_update(outer_a, afl, pan, m, m, slab1, nxt, slab0, slab1);
                     }

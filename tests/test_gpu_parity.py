@@ -396,11 +396,12 @@ def lap48_oracle():
                                   dict(trsm_split_wg=1), dict(panel_tall=2), dict(panel_tall=2, lookahead=0),
                                   dict(la_grid=448), dict(panel_tall=3), dict(panel_tall=3, la_grid=448),
                                   dict(panel_tall=4, la_grid=448), dict(cb_slab=1), dict(cb_slab=1, la_grid=448),
-                                  dict(cb_slab=1, cb_gather=0, panel_nb_outer=256), dict(lookahead=2)],
+                                  dict(cb_slab=1, cb_gather=0, panel_nb_outer=256), dict(lookahead=2),
+                                  dict(lookahead=3)],
                          ids=["default", "tiled_asm", "assembled_cb", "tall_trsm", "split_potrf", "tall_inv",
                               "tall_inv_nolookahead", "resident_lookahead", "two_level", "two_level_resident",
                               "two_level_left_looking", "cb_by_slab", "cb_by_slab_resident", "cb_by_slab_assembled",
-                              "left_looking"])
+                              "left_looking", "left_looking_lookahead"])
 def test_lap48_full_parity(gpu, lap48_oracle, opts):
     # the whole 48^3 factor (n = 110592, F = 7.07e10: a 2304-wide root, CB SYRK with K
     # up to 1152 on 128 x 128 tiles) against the oracle, exact pattern and rel-Fro;
@@ -763,7 +764,8 @@ PANEL_OPTS = [dict(inner_order=0), dict(inner_order=0, lookahead=0), dict(lookah
               dict(cb_slab=1), dict(cb_slab=1, panel_nb_outer=128), dict(cb_slab=1, cb_gather=0, panel_nb_outer=128),
               dict(cb_slab=1, la_grid=64, panel_nb_outer=192), dict(cb_slab=1, lookahead=0, panel_nb_outer=128),
               dict(lookahead=2), dict(lookahead=2, panel_nb_outer=128), dict(lookahead=2, panel_nb_outer=192, inner_order=0),
-              dict(lookahead=2, panel_tall=1, panel_nb_outer=128), dict(cb_gather_min_w=64),
+              dict(lookahead=2, panel_tall=1, panel_nb_outer=128), dict(lookahead=3), dict(lookahead=3, panel_nb_outer=128),
+              dict(lookahead=3, panel_nb_outer=192, inner_order=0), dict(cb_gather_min_w=64),
               dict(cb_gather_min_w=100000)]
 
 
