@@ -138,6 +138,8 @@ typedef struct sc_options {
     int32_t cb_gather_min_w; /* with cb_gather: only fronts at least this wide gather their children's entries in the
                                 CB SYRK; narrower fronts (short-K CB launches) are assembled whole and their SYRK
                                 updates C in place (default 0: every large front gathers) */
+    int32_t la_split;        /* > 1: a lookahead-stream panel update runs as this many back-to-back launches over
+                                consecutive parts of its tile list (default 1: one launch) */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

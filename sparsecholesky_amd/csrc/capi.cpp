@@ -99,6 +99,7 @@ void sc_default_options(sc_options* opt) {
     opt->dist_pieces = 4;
     opt->cb_slab = 0;
     opt->cb_gather_min_w = 0;
+    opt->la_split = 1;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,

@@ -305,6 +305,24 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             N.sched.push_back(T);
             return;
         }
+        // la_split: a big lookahead-stream update as P back-to-back launches over consecutive
+        // parts of its tile list (each a multiple of 8 tiles: the XCD mapping holds), so a
+        // chain launch on the main stream waits for one part's dispatch, not the whole grid's
+        const int P = (strm == 1 && kind == L_PANEL && !L.res) ? std::max(1, S.opt.la_split) : 1;
+        if (P > 1 && L.count >= 64 * P) {
+            const int per = (L.count / P + 7) / 8 * 8;
+            const double fl_all = L.flops, by_all = L.bytes;
+            const int n_all = L.count;
+            for (int q = 0, t0 = 0; t0 < n_all; ++q, t0 += per) {
+                Launch Q = L;
+                Q.toff = L.toff + t0;
+                Q.count = std::min(per, n_all - t0);
+                Q.flops = fl_all * Q.count / n_all;
+                Q.bytes = by_all * Q.count / n_all;
+                N.sched.push_back(Q);
+            }
+            return;
+        }
         N.sched.push_back(L);
     };
     // cross-stream dependencies: record an event on a stream / make a stream wait on it
