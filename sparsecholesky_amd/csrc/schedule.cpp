@@ -313,7 +313,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             const int per = (L.count / P + 7) / 8 * 8;
             const double fl_all = L.flops, by_all = L.bytes;
             const int n_all = L.count;
-            for (int q = 0, t0 = 0; t0 < n_all; ++q, t0 += per) {
+            for (int t0 = 0; t0 < n_all; t0 += per) {
                 Launch Q = L;
                 Q.toff = L.toff + t0;
                 Q.count = std::min(per, n_all - t0);
