@@ -346,7 +346,9 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
     // wait for the main stream's work so far (their data); the main stream waits
     // for the step when it receives.  Messages keep the plan order, so every peer
     // pair posts its matching sends and receives in the same order.
-    auto emit_step = [&](int32_t id, int send_ev = -1) {
+    // recv_strm: the stream that consumes what the step receives (it waits for the step;
+    // the main stream by default)
+    auto emit_step = [&](int32_t id, int send_ev = -1, int recv_strm = 0) {
         if (!multi || id < 0 || emitted[id]) return;
         emitted[id] = 1;
         Launch L {};
@@ -439,16 +441,16 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // level (the per-level guard below)
         if (any_send) push_wait(2, send_ev >= 0 ? send_ev : push_record(0));
         N.sched.push_back(L);
-        if (any_recv) push_wait(0, push_record(2));
+        if (any_recv) push_wait(recv_strm, push_record(2));
     };
     // the step of piece p of slab k of front s (-1: none), and all pieces of slab k
     auto slab_piece = [&](int32_t s, int k, int p) -> int32_t {
         if (!multi || k >= (int)slab_step[s].size() || p >= (int)slab_step[s][k].size()) return -1;
         return slab_step[s][k][p];
     };
-    auto emit_slab = [&](int32_t s, int k) {
+    auto emit_slab = [&](int32_t s, int k, int recv_strm = 0) {
         if (!multi || k >= (int)slab_step[s].size()) return;
-        for (int32_t id : slab_step[s][k]) emit_step(id);
+        for (int32_t id : slab_step[s][k]) emit_step(id, -1, recv_strm);
     };
     // the extend-add gather's segment table of front s on hosted rank v (GSeg): per 64 x 64
     // block of its CB, every child with CB rows and columns in the block, in child order
@@ -1267,7 +1269,9 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                         push_gemm_launch(L_PANEL, lev, t0, 0, fl);
                     }
                 }
-                emit_slab(s, k);
+                // the rest of slab k feeds only the lookahead stream's updates here: that
+                // stream waits for it, the main stream (this rank's chain) does not
+                emit_slab(s, k, 1);
                 std::vector<GemmTask> t1;
                 double fl = 0.0;
                 for (int j = k + 2; j < nsl; ++j) {
