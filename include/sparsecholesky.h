@@ -129,7 +129,7 @@ typedef struct sc_options {
                                 workgroups walking their tiles (dispatched at once, so the 64-column chain on the
                                 main stream finds the slots it leaves free); 0: one workgroup per tile */
     int32_t dist_pieces;     /* multi-GPU distributed panels: each final slab is handed over in this many column
-                                pieces (default 4: 256 of a 1024-column slab), each sent as soon as the chain has
+                                pieces (default 2: 512 of a 1024-column slab), each sent as soon as the chain has
                                 finished it, so the next slab's owner starts updating before the slab is done */
     int32_t cb_slab;         /* 1: a large front's contribution block is updated slab by slab on the lookahead
                                 stream (CB -= L21_k L21_k^T, K = the slab width, the first pass gathering the

@@ -96,7 +96,7 @@ void sc_default_options(sc_options* opt) {
     opt->tiny_dense = 1;
     opt->dist_asm = 1;
     opt->la_grid = 0;
-    opt->dist_pieces = 4;
+    opt->dist_pieces = 2;
     opt->cb_slab = 0;
     opt->cb_gather_min_w = 0;
     opt->la_split = 1;
