@@ -140,6 +140,8 @@ typedef struct sc_options {
                                 updates C in place (default 0: every large front gathers) */
     int32_t la_split;        /* > 1: a lookahead-stream panel update runs as this many back-to-back launches over
                                 consecutive parts of its tile list (default 1: one launch) */
+    int32_t la_after;        /* 1: at a slab end the lookahead stream's trailing update starts after the next slab's
+                                update (main stream) has finished instead of beside it (default 0) */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

@@ -1072,6 +1072,9 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 fa2 = afl - fa;
                 push_gemm_launch(L_PANEL, lev, outer_a, 0, fa);
                 push_gemm_launch(L_GEMM, lev, outer_a2, 0, fa2);
+                // la_after: the lookahead stream's rest starts once the next slab's update is
+                // done (that update runs alone; the rest overlaps the next slab's chain only)
+                if (S.opt.la_after && !outer_b.empty()) e_trsm = push_record(0);
             }
             if (!outer_b.empty()) {
                 push_wait(1, e_trsm);
