@@ -43,6 +43,11 @@ def test_default_options():
     o = sc.default_options()
     assert o.relax == 1 and list(o.nrelax) == [4, 16, 48] and o.small_front_max == 128
     assert o.panel_nb == 64 and o.panel_nb_outer == 1024 and o.syrk_tile == 0
+    # round-4 fields: distributed assembly and two slab pieces on; the measured-slower
+    # schedule knobs off
+    assert o.dist_asm == 1 and o.dist_pieces == 2
+    assert o.la_grid == 0 and o.cb_slab == 0 and o.la_split == 1 and o.la_after == 0 and o.cb_gather_min_w == 0
+    assert o.lookahead == 1 and o.panel_tall == 0
     assert o.lookahead == 1 and o.inner_order == 1 and o.asm_tile_min_m == 0
 
 
