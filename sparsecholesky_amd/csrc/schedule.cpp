@@ -496,6 +496,10 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     g.jlo = at(64 * cbk);
                     g.jhi = at(std::min(mb, 64 * cbk + 64));
                     if (g.ilo >= g.ihi || g.jlo >= g.jhi) continue;
+                    if (R.cb_off[c] < 0) {  // the memory plan keeps every gathered child's CB here
+                        N.err = "schedule: gathered child CB not resident on its parent's rank";
+                        continue;
+                    }
                     g.cb = R.P.cb_pool + R.cb_off[c];
                     g.rel = R.P.relind + S.rel_ptr[c];
                     g.mbc = mbc;
