@@ -142,8 +142,6 @@ typedef struct sc_options {
                                 consecutive parts of its tile list (default 1: one launch) */
     int32_t la_after;        /* 1: at a slab end the lookahead stream's trailing update starts after the next slab's
                                 update (main stream) has finished instead of beside it (default 0) */
-    int32_t la_streams;      /* > 1 (at most 4): a lookahead-stream panel update runs as that many parts over
-                                consecutive tile ranges on as many streams at once (default 1) */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

@@ -102,8 +102,6 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     // under hipGraph replay (569 -> 649 ms at 128^3, any priority, any
     // GPU_MAX_HW_QUEUES) though nothing runs on it; eager runs (multi-rank) see 0.5%.
     if (ok && multi) ok = hipStreamCreateWithPriority(&N.stream3, hipStreamNonBlocking, prio_hi) == hipSuccess;
-    for (int q = 0; ok && q + 1 < std::min(S.opt.la_streams, 4); ++q)
-        ok = hipStreamCreateWithPriority(&N.stream_la[q], hipStreamNonBlocking, prio_lo) == hipSuccess;
     if (!ok) {
         N.err = "hipStreamCreate failed";
         return fail(SC_ERR_HIP);
@@ -291,7 +289,6 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
 
 
 static hipStream_t stream_of(const Numeric& N, int strm) {
-    if (strm >= 3) return N.stream_la[strm - 3];
     return strm == 2 ? N.stream3 : strm == 1 ? N.stream2 : N.stream;
 }
 
@@ -635,8 +632,6 @@ void numeric_free(Numeric* Np) {
     if (N.stream) (void)hipStreamDestroy(N.stream);
     if (N.stream2) (void)hipStreamDestroy(N.stream2);
     if (N.stream3) (void)hipStreamDestroy(N.stream3);
-    for (hipStream_t& x : N.stream_la)
-        if (x) (void)hipStreamDestroy(x);
     delete Np;
 }
 

@@ -187,7 +187,6 @@ struct Numeric {
     hipStream_t stream = nullptr;
     hipStream_t stream2 = nullptr;  // trailing panel updates overlapped with the next slab
     hipStream_t stream3 = nullptr;  // multi-rank: comm stream (pack, transfer group, unpack), strm == 2
-    hipStream_t stream_la[3] = {nullptr, nullptr, nullptr};  // la_streams > 1: strm 3.. (lookahead parts)
     std::vector<hipEvent_t> sync_ev;
     int32_t n_sync_events = 0;
     std::vector<RankMem> R;          // hosted ranks

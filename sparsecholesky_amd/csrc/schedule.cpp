@@ -208,22 +208,6 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         }
         return b;
     };
-    // cross-stream dependencies: record an event on a stream / make a stream wait on it
-    auto push_record = [&](int strm) -> int {
-        Launch L {};
-        L.kind = L_RECORD;
-        L.strm = strm;
-        L.count = N.n_sync_events++;
-        N.sched.push_back(L);
-        return L.count;
-    };
-    auto push_wait = [&](int strm, int ev) {
-        Launch L {};
-        L.kind = L_WAIT;
-        L.strm = strm;
-        L.count = ev;
-        N.sched.push_back(L);
-    };
     auto push_gemm_launch = [&](int kind, int level, const std::vector<GemmTask>& tasks, int big,
                                 double flops, int strm = 0) {
         if (tasks.empty()) return;
@@ -321,29 +305,6 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             N.sched.push_back(T);
             return;
         }
-        // la_streams: a big lookahead-stream update as parts over consecutive tile ranges on
-        // that many streams at once (each part a smaller grid, dispatched beside the others);
-        // stream 1 waits for every part, so the caller's event after it covers them all
-        const int NS = (strm == 1 && kind == L_PANEL && !L.res) ? std::min(4, std::max(1, S.opt.la_streams)) : 1;
-        if (NS > 1 && L.count >= 64 * NS) {
-            const int per = (L.count / NS + 7) / 8 * 8;
-            const double fl_all = L.flops, by_all = L.bytes;
-            const int n_all = L.count;
-            const int ev = push_record(1);
-            int q = 0;
-            for (int t0 = 0; t0 < n_all; t0 += per, ++q) {
-                Launch Q = L;
-                Q.strm = q == 0 ? 1 : 2 + q;
-                Q.toff = L.toff + t0;
-                Q.count = std::min(per, n_all - t0);
-                Q.flops = fl_all * Q.count / n_all;
-                Q.bytes = by_all * Q.count / n_all;
-                if (q > 0) push_wait(Q.strm, ev);
-                N.sched.push_back(Q);
-            }
-            for (int r = 1; r < q; ++r) push_wait(1, push_record(2 + r));
-            return;
-        }
         // la_split: a big lookahead-stream update as P back-to-back launches over consecutive
         // parts of its tile list (each a multiple of 8 tiles: the XCD mapping holds), so a
         // chain launch on the main stream waits for one part's dispatch, not the whole grid's
@@ -362,6 +323,22 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             }
             return;
         }
+        N.sched.push_back(L);
+    };
+    // cross-stream dependencies: record an event on a stream / make a stream wait on it
+    auto push_record = [&](int strm) -> int {
+        Launch L {};
+        L.kind = L_RECORD;
+        L.strm = strm;
+        L.count = N.n_sync_events++;
+        N.sched.push_back(L);
+        return L.count;
+    };
+    auto push_wait = [&](int strm, int ev) {
+        Launch L {};
+        L.kind = L_WAIT;
+        L.strm = strm;
+        L.count = ev;
         N.sched.push_back(L);
     };
     // The hosted ranks' part of comm step `id` on the comm stream (strm 2), emitted
