@@ -181,3 +181,26 @@ def test_distributed_panel_plan(k, nranks, sb):
             assert slr[v] == 0
     s0 = sc.Symbolic(sc.laplacian3d(k), panel_nb_outer=128, dist_cbb=64, small_front_max=32, dist_panel=0)
     assert (s0.dist_plan_info(nranks)["slab_ranks"] == 0).all()
+
+
+def test_early_delivery_groups_can_be_empty():
+    # with distributed assembly, an early-delivery child's column group whose columns all
+    # map into parent columns its own rank assembles moves nothing, and the plan drops its
+    # step: at 20^3 on 2 ranks child 263 has two 256-column groups but one DELIVER step.
+    # The schedule must look the steps up per (child, group) -- the round-4 bug paired the
+    # remaining group with the wrong CB column event (wrong factor, GPU parity
+    # test_partitioned_split_fronts_emulated[2-False-opts0]; and in a multi-process run a
+    # send/recv order hazard).
+    A = sc.laplacian3d(20)
+    counts = {}
+    for asm in (1, 0):
+        s = sc.Symbolic(A, panel_nb_outer=128, dist_cbb=64, small_front_max=32, dist_asm=asm)
+        st = s.dist_steps(2)
+        sn = s.supernodes()
+        fr = st["front"][(st["kind"] == 2) & (st["front"] >= 0)]
+        early = np.unique(fr)
+        assert len(early) > 0
+        groups = {int(c): -(-int(sn["m"][c] - sn["w"][c]) // (4 * s.opt.dist_cbb)) for c in early}
+        counts[asm] = {int(c): (int((fr == c).sum()), groups[int(c)]) for c in early}
+    assert any(n < g for n, g in counts[1].values())      # a dropped group with dist_asm
+    assert all(n == g for n, g in counts[0].values())     # every group moves data without it
