@@ -1,3 +1,4 @@
 export TMPDIR=/tmp; mkdir -p gpurun_out
-# the whole GPU suite and one default bench line (the round-end driver runs the same)
-timeout -k 10 1100 bash scripts/gpu.sh suite
+# bench.py's N > 1 branch on the one GPU with the round-4 defaults (distributed assembly, slab
+# pieces): host-staged transport (real multi-process protocol) and dry
+timeout -k 10 900 bash scripts/gpu.sh rehearse 64 2 4
