@@ -142,6 +142,11 @@ typedef struct sc_options {
                                 consecutive parts of its tile list (default 1: one launch) */
     int32_t la_after;        /* 1: at a slab end the lookahead stream's trailing update starts after the next slab's
                                 update (main stream) has finished instead of beside it (default 0) */
+    int32_t cb_lean_kmin;    /* CB launches on 64 x 64 tiles use the lean instance only when their deepest K is at
+                                least this (and at most syrk_lean_kmax; default 65: the K <= 64 launches are
+                                gather-bound and keep the full gather batches) */
+    int32_t cb_small_kmax;   /* CB launches whose deepest K is below this run on 64 x 64 tiles however wide their
+                                fronts (default 0: 128 x 128 tiles for fronts at least 256 wide) */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

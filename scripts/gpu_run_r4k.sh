@@ -1,7 +1,7 @@
 export TMPDIR=/tmp; mkdir -p gpurun_out
-# N=8 projection sweep of plan options around the round-4 defaults
-for o in dist_slab_block=1 dist_slab_block=3 dist_pieces=3 dist_cbb=2048 dist_cbb=512; do
-  timeout -k 10 300 python -u scripts/dist_project.py --k 128 --n 8 --reps 2 --timeline --opt $o > gpurun_out/proj_$o.log 2>&1 || { tail -5 gpurun_out/proj_$o.log; exit 1; }
-  grep '^{' gpurun_out/proj_$o.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$o', d['max_rank_ms'], d['max_rank_ms_with_comm_serial'], d['max_critical_path_ms_50GBs'], d['max_critical_path_ms_100GBs'])"
-done
+# short-K CB launch shapes (levels 4-9): lean instance for K <= 64, 64-tiles below K = 256
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider -k "panel_schedule and (cb_lean_kmin or cb_small_kmax)" > gpurun_out/pytest_cbk.log 2>&1
+rc=$?; echo pytest cbk rc=$rc; tail -2 gpurun_out/pytest_cbk.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 bash scripts/gpu_ab.sh base cb_lean_kmin=0 cb_small_kmax=256 || exit 1
+timeout -k 10 300 python3 scripts/panel_breakdown.py 128 > gpurun_out/breakdown_final.txt 2>&1 || exit 1
 echo done

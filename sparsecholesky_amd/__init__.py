@@ -75,7 +75,8 @@ class Options(C.Structure):
         ("syrk_lean_kmax", C.c_int32), ("cb_tail_split", C.c_int32), ("tiny_dense", C.c_int32),
         ("dist_asm", C.c_int32), ("la_grid", C.c_int32),
         ("dist_pieces", C.c_int32), ("cb_slab", C.c_int32), ("cb_gather_min_w", C.c_int32),
-        ("la_split", C.c_int32), ("la_after", C.c_int32),
+        ("la_split", C.c_int32), ("la_after", C.c_int32), ("cb_lean_kmin", C.c_int32),
+        ("cb_small_kmax", C.c_int32),
     ]
 
 

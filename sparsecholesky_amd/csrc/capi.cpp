@@ -101,6 +101,8 @@ void sc_default_options(sc_options* opt) {
     opt->cb_gather_min_w = 0;
     opt->la_split = 1;
     opt->la_after = 0;
+    opt->cb_lean_kmin = 65;
+    opt->cb_small_kmax = 0;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,

@@ -225,6 +225,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         }
         const bool wide = minN >= 256;
         L.bt = (S.opt.syrk_tile == 128 || (S.opt.syrk_tile == 0 && wide)) ? SYRK_BT_LARGE : SYRK_BT_SMALL;
+        if (kind == L_CB && S.opt.syrk_tile == 0 && maxK < S.opt.cb_small_kmax) L.bt = SYRK_BT_SMALL;
         // batched C epilogue on the critical path (main-stream panel updates) and where
         // K is short enough that the epilogue dominates a tile (CB of levels 4-7 at
         // 128^3); deep-K CB updates and the lookahead stream keep the trickle epilogue
@@ -232,7 +233,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // (CB launches with K <= 64 -- levels 4-6 at 128^3 -- are gather-bound and lose
         // more to the lean instance's smaller gather batches than they gain in occupancy)
         L.lean = L.bt == SYRK_BT_SMALL && S.opt.syrk_lean_kmax > 0 && maxK <= S.opt.syrk_lean_kmax &&
-                 (kind == L_PANEL || maxK > 64);
+                 (kind == L_PANEL || maxK >= S.opt.cb_lean_kmin);
         // lookahead-stream updates as a resident grid (la_grid): all its workgroups are
         // dispatched at once, so the chain's launches on the main stream are not queued
         // behind the rest of the grid

@@ -766,7 +766,8 @@ PANEL_OPTS = [dict(inner_order=0), dict(inner_order=0, lookahead=0), dict(lookah
               dict(lookahead=2), dict(lookahead=2, panel_nb_outer=128), dict(lookahead=2, panel_nb_outer=192, inner_order=0),
               dict(lookahead=2, panel_tall=1, panel_nb_outer=128), dict(lookahead=3), dict(lookahead=3, panel_nb_outer=128),
               dict(lookahead=3, panel_nb_outer=192, inner_order=0), dict(la_split=4, panel_nb_outer=128),
-              dict(la_split=3), dict(la_after=1), dict(la_after=1, panel_nb_outer=128), dict(cb_gather_min_w=64),
+              dict(la_split=3), dict(la_after=1), dict(la_after=1, panel_nb_outer=128), dict(cb_lean_kmin=0),
+              dict(cb_small_kmax=256), dict(cb_gather_min_w=64),
               dict(cb_gather_min_w=100000)]
 
 
