@@ -231,6 +231,21 @@ __global__ __launch_bounds__(256) void assemble_tile_kernel(DevPlan P, const int
     }
 }
 
+// Buffer-resource access for the panel kernels: one VGPR lane offset plus an
+// SGPR column offset per access, so 64 column addresses never occupy VGPRs.
+// Raw buffers (stride 0) drop stores and zero loads at offsets >= nbytes, so a
+// dead lane is masked by giving it an out-of-range lane offset (BUF_DEAD).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const double* base, uint32_t nbytes = 0xffffffffu) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), 0, (int)nbytes, 0x00020000);
+}
+constexpr int BUF_DEAD = 0x7ffffff0;
+__device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
+}
+__device__ __forceinline__ void buf_st(double v, __amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0)), v), rs, voff, soff, 0);
+}
+
 // Wave-uniform broadcast of lane `src`'s double (two v_readlane_b32).
 __device__ __forceinline__ double readlane_f64(double v, int src) {
     const long long b = __double_as_longlong(v);
@@ -786,6 +801,9 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
 }
+#ifndef SC_TD_BUF
+#define SC_TD_BUF 1  // 1: the A loads and panel stores as range-checked buffer accesses (no branches)
+#endif
 #ifndef SC_TD_PROBE
 #define SC_TD_PROBE 0  // timing probe (scripts/tiny_probe.py): 1 = loads and stores only, no factorization
 #endif
@@ -952,7 +970,13 @@ __global__ __launch_bounds__(64) void tiny_dense_kernel(DevPlan P, TinyPlan T, i
     double Ld[4][4], rc[4];
     int bad;
 #pragma unroll
-    for (int j = 0; j < NP; ++j) a[j] = q[j].x >= 0 ? Ax[q[j].x] : 0.0;
+    for (int j = 0; j < NP; ++j) {
+#if SC_TD_BUF  // branch-free: a missing entry reads 0 through the buffer's range check
+        a[j] = buf_ld(buf_rsrc(Ax, (uint32_t)T.nax * 8u), q[j].x >= 0 ? q[j].x * 8 : BUF_DEAD, 0);
+#else
+        a[j] = q[j].x >= 0 ? Ax[q[j].x] : 0.0;
+#endif
+    }
 #pragma unroll
     for (int j = 0; j < NP; ++j) a[j] = (i == j && i >= n) ? 1.0 : a[j];  // identity padding
     if (SC_TD_PROBE != 1) {
@@ -967,7 +991,11 @@ __global__ __launch_bounds__(64) void tiny_dense_kernel(DevPlan P, TinyPlan T, i
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
         const int o = po[j * 64 + i];
+#if SC_TD_BUF  // branch-free: an entry that is not stored goes out of the buffer's range
+        buf_st(a[j], buf_rsrc(P.panel_pool, (uint32_t)T.npan * 8u), o >= 0 ? o * 8 : BUF_DEAD, 0);
+#else
         if (o >= 0) P.panel_pool[o] = a[j];
+#endif
     }
     // one wave: lane 0's system-scope release store below waits for the wave's panel
     // stores, so the status word is seen after the factor
@@ -985,6 +1013,8 @@ __global__ __launch_bounds__(64) void tiny_dense_kernel(DevPlan P, TinyPlan T, i
 hipError_t launch_tiny_dense(const DevPlan& P, const TinyPlan& T, int n, const double* Ax, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     if (n > TINY_DENSE_N || T.na != tiny_dense_np(n) * 64) return hipErrorInvalidValue;  // the lane map's shape
+    // every A / panel byte offset in range, and the dead offset out of it
+    if ((int64_t)T.nax * 8 >= BUF_DEAD || (int64_t)T.npan * 8 >= BUF_DEAD) return hipErrorInvalidValue;
     if (n <= 16)
         hipLaunchKernelGGL(tiny_dense_kernel<16>, dim3(1), dim3(64), 0, st, P, T, n, Ax);
     else if (n <= 32)
@@ -1112,22 +1142,6 @@ __global__ __launch_bounds__(CHAIN_NT) void front_chain_kernel(DevPlan P, ChainP
 // straight-line code (panel_gen.inc, gen_panel.py) that keeps ~24 LDS operands
 // in flight per wave; a partial last block (nb < 64) uses the template path.
 // ---------------------------------------------------------------------------
-// Buffer-resource access for the panel kernels: one VGPR lane offset plus an
-// SGPR column offset per access, so 64 column addresses never occupy VGPRs.
-// Raw buffers (stride 0) drop stores and zero loads at offsets >= nbytes, so a
-// dead lane is masked by giving it an out-of-range lane offset (BUF_DEAD).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const double* base, uint32_t nbytes = 0xffffffffu) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), 0, (int)nbytes, 0x00020000);
-}
-constexpr int BUF_DEAD = 0x7ffffff0;
-__device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
-}
-__device__ __forceinline__ void buf_st(double v, __amdgpu_buffer_rsrc_t rs, int voff, int soff) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(rs, 0, 0, 0)), v), rs, voff, soff, 0);
-}
-
-
 #include "panel_gen.inc"
 
 // Diagonal block (nb <= 64) of a large front's panel: 256 threads hold its 4 x 4

@@ -212,6 +212,8 @@ struct TinyPlan {
     int32_t lds;      // doubles of images + CBs
     int32_t* host_info;  // device view of the handle's pinned status word: the kernel owns the status
                          // (no reset / copy launches around it), or null
+    int32_t nax = 0;     // tiny dense: A values (the range of the lane map's Ax indices)
+    int32_t npan = 0;    // tiny dense: panel-pool doubles (the range of its panel offsets)
 };
 constexpr int TINY_MAX_FRONTS = 16;
 constexpr int TINY_MAX_LDS = 12288;  // doubles of images + CBs (96 KB)

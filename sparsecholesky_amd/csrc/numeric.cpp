@@ -257,6 +257,8 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
         N.TP.nph = (int32_t)B.tph.size();
         N.TP.npr = (int32_t)B.tpr.size();
         N.TP.lds = B.tiny_lds;
+        N.TP.nax = (int32_t)std::min<int64_t>(S.nnzA_in, INT32_MAX);
+        N.TP.npan = (int32_t)std::min<int64_t>(N.R[0].panel_total, INT32_MAX);
         // a tiny-tree handle is one launch: the kernel owns the status word (initial
         // value, failures, the copy to pinned host memory), so a factorization is one
         // dispatch with no reset / copy around it

@@ -1332,7 +1332,8 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
     // -1 where the entry has no A value / is not stored (internal numbering: the factor
     // of the postordered matrix is the postordered factor, so the dense image is the
     // multifrontal result)
-    const bool dense = !multi && S.opt.tiny_dense && S.n > 0 && S.n <= TINY_DENSE_N && S.nnzA_in <= INT32_MAX;
+    // (A value and panel byte offsets stay inside the kernel's 32-bit buffer ranges)
+    const bool dense = !multi && S.opt.tiny_dense && S.n > 0 && S.n <= TINY_DENSE_N && S.nnzA_in < (1 << 27);
     if (dense) {
         for (int32_t s = 0; s < S.ns; ++s) {
             const int m = S.sn_m[s], w = S.w(s), c0 = S.sn_start[s];
