@@ -379,8 +379,7 @@ def main():
             "options": {"relax_wmax": symb.opt.relax_wmax, "panel_nb_outer": symb.opt.panel_nb_outer,
                         "small_front_max": symb.opt.small_front_max, "use_graph": symb.opt.use_graph,
                         "lookahead": symb.opt.lookahead, "syrk_tile": symb.opt.syrk_tile,
-                        "inner_order": symb.opt.inner_order, "panel_tall": symb.opt.panel_tall,
-                        "la_grid": symb.opt.la_grid, "cb_slab": symb.opt.cb_slab,
+                        "inner_order": symb.opt.inner_order,
                         **({"dist_asm": symb.opt.dist_asm, "dist_pieces": symb.opt.dist_pieces} if world > 1 else {}),
                         **{k: v for k, v in kw.items() if k not in ("use_graph",)}},
         },

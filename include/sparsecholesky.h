@@ -34,7 +34,7 @@ extern "C" {
 #pragma GCC visibility push(default)
 #endif
 
-#define SC_VERSION 100 /* 1.0.0 */
+#define SC_VERSION 110 /* 1.1.0: sc_options pruned to the live knobs; debug hooks in sparsecholesky_debug.h */
 
 enum sc_status {
     SC_OK = 0,
@@ -68,11 +68,9 @@ typedef struct sc_options {
     int32_t relax_wmax;      /* a child and its parent that are both wider than this are not amalgamated when
                                 the parent has other children (chains still merge; 0 = no limit; default 1) */
     int32_t syrk_tile;       /* 0 = auto (128x128/8 waves for wide, deep updates, else 64x64/4 waves); 64; 128 */
-    int32_t lookahead;       /* 0: none; 1 (default): trailing panel updates on a 2nd stream, overlapping the
-                                next slab's POTRF/TRSM chain; 2: left-looking -- at each slab end only the next
-                                slab is updated, by every slab so far (one deep-K product), on the main stream;
-                                3: the next slab by the slab just finished (main stream) and the slab after next by
-                                every slab so far (lookahead stream, one deep-K product) */
+    int32_t lookahead;       /* 1 (default): at a slab end the next slab's columns are updated on the main stream
+                                and every later column on a second stream, overlapping the next slab's
+                                POTRF/TRSM chain; 0: the whole trailing update on the main stream */
     int32_t inner_order;     /* updates inside a slab: 0 right-looking (K = 64), 1 recursive (K = 64..NBO/2) */
     int32_t asm_tile_min_m;  /* fronts with m >= this use the write-once tiled assembly (0 = default 8192) */
     int32_t dist_split;      /* multi-GPU: a shared front with a contribution block keeps its panel on one rank and
@@ -91,21 +89,6 @@ typedef struct sc_options {
     int32_t cb_gather;       /* 1 (default): a large front's contribution block is not assembled; its CB SYRK
                                 gathers the children's entries into each output tile (C = sum - L21 L21^T,
                                 written once); 0: assembly writes the whole front, the SYRK updates it */
-    int32_t panel_tall;      /* 1: in a large front wider than 64 columns the 64-column POTRF/TRSM chain runs on
-                                each slab's diagonal-block rows only and the rows below the slab are solved by
-                                one tall-TRSM launch per slab (row blocks, MFMA, block inverses); 2: the rows
-                                below each slab are solved as one MFMA product with X = inv(L11) (64-block
-                                inverses, doubling products); 3: as 2 with two-level lookahead (the near rows
-                                and the next diagonal block on the main stream, the far rows and trailing updates
-                                on the lookahead stream); 4: as 3 with a left-looking trailing update (the slab
-                                after next from every slab so far, one deep-K product); 0 (default, measured
-                                faster at 128^3: 512 vs 541 ms for 1): every chain step solves and updates all
-                                rows of the front */
-    int32_t trsm_fold;       /* 1: with the recursive inner order, the span-64 inner update after an even block
-                                of a slab is folded into the next block's fused POTRF/TRSM launch (each
-                                workgroup applies it to its rows and to the diagonal block) instead of being a
-                                launch of its own; 0 (default, measured faster at 128^3: 516 vs 533 ms): a
-                                separate update launch */
     int32_t dist_slab_block; /* multi-GPU distributed panels: consecutive slabs per rank in the cyclic deal
                                 (default 2: every other slab hand-over is rank-local, off the critical path;
                                 capped at slabs / ranks so that every rank of the group gets a block) */
@@ -125,28 +108,16 @@ typedef struct sc_options {
                                 assembled where its columns live (each rank its own slabs / CB blocks; child CB
                                 columns go straight to the rank owning the parent columns they map into, no
                                 assembled-front hand-out); 0: its owner assembles it and sends the pieces */
-    int32_t la_grid;         /* > 0: the lookahead stream's panel updates run as a resident grid of this many
-                                workgroups walking their tiles (dispatched at once, so the 64-column chain on the
-                                main stream finds the slots it leaves free); 0: one workgroup per tile */
     int32_t dist_pieces;     /* multi-GPU distributed panels: each final slab is handed over in this many column
                                 pieces (default 2: 512 of a 1024-column slab), each sent as soon as the chain has
                                 finished it, so the next slab's owner starts updating before the slab is done */
-    int32_t cb_slab;         /* 1: a large front's contribution block is updated slab by slab on the lookahead
-                                stream (CB -= L21_k L21_k^T, K = the slab width, the first pass gathering the
-                                children's entries) while the next slabs are factored, instead of by one K = w
-                                SYRK after the panel; 0 (default): one SYRK after the panel */
-    int32_t cb_gather_min_w; /* with cb_gather: only fronts at least this wide gather their children's entries in the
-                                CB SYRK; narrower fronts (short-K CB launches) are assembled whole and their SYRK
-                                updates C in place (default 0: every large front gathers) */
-    int32_t la_split;        /* > 1: a lookahead-stream panel update runs as this many back-to-back launches over
-                                consecutive parts of its tile list (default 1: one launch) */
-    int32_t la_after;        /* 1: at a slab end the lookahead stream's trailing update starts after the next slab's
-                                update (main stream) has finished instead of beside it (default 0) */
-    int32_t cb_lean_kmin;    /* CB launches on 64 x 64 tiles use the lean instance only when their deepest K is at
-                                least this (and at most syrk_lean_kmax; default 65: the K <= 64 launches are
-                                gather-bound and keep the full gather batches) */
-    int32_t cb_small_kmax;   /* CB launches whose deepest K is below this run on 64 x 64 tiles however wide their
-                                fronts (default 0: 128 x 128 tiles for fronts at least 256 wide) */
+    int32_t panel_psk;       /* 1: the 64-column POTRF / TRSM / inner-update chain of each 1024-column slab of the
+                                large fronts runs as ONE persistent launch per slab and level (all fronts of the
+                                level; one workgroup per psk_rows rows, steps ordered by device-scope flags)
+                                instead of two launches per 64-column step; 0: per-step launches */
+    int32_t psk_rows;        /* rows per persistent-slab workgroup: 64, 128 or 256 (default 64) */
+    int32_t psk_min_w;       /* a level runs its slabs persistently only when its widest large front is at least
+                                this wide (default 0: every level with large fronts) */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };
@@ -390,37 +361,6 @@ int64_t sc_numeric_create_dist_host(const sc_symbolic* sym, int32_t device, int3
 int64_t sc_numeric_create_dist_dry(const sc_symbolic* sym, int32_t device, int32_t rank, int32_t nranks,
                                    sc_numeric** out);
 
-/* ---------------- debug / unit-test hooks ---------------- */
-/* C[i,j] -= sum_k A[i,k] A[j,k] for i>=j over an M x N trapezoid (device
- * pointers, column-major) through the fp64 MFMA SYRK kernel. */
-int64_t sc_debug_syrk(double* dC, int32_t ldc, const double* dA, int32_t lda, int32_t M, int32_t N,
-                      int32_t K);
-/* Best wall time (ms) of reps synchronous factorizations from device values
- * (sc_factor_device(num, d_Ax, 1): launch, run, status read-back), timed in C. */
-int64_t sc_debug_time_factor(sc_numeric* num, const double* d_Ax, int32_t reps, double* best_ms);
-/* Debug: eager = 1 launches the solve sweeps directly instead of replaying their graph. */
-int64_t sc_debug_solve_eager(sc_numeric* num, int32_t eager);
-/* Chain launches (runs of single small-front levels): enable = 1 makes the next
- * eager factorizations record 8 shader-clock stamps per chained front (phase
- * boundaries); enable = 0 copies up to cap of them to out.  Returns the count. */
-int64_t sc_debug_chain_stamps(sc_numeric* num, int32_t enable, uint64_t* out, int64_t cap);
-/* Microbenchmarks: which=0 register-only fp64 MFMA probe (TFLOP/s; M blocks of
- * 4 waves, K iterations, arg accumulators); which=1/5 the SYRK kernel on an M x M
- * triangle with depth K, tile arg (64/128), with / without the XCD tile order
- * (TFLOP/s); which=2/3 the panel POTRF / TRSM kernel on an M x 64 front
- * (microseconds per launch). */
-int64_t sc_debug_bench(int32_t which, int32_t M, int32_t K, int32_t reps, int32_t arg, double* tflops);
-/* Placement probe: nwg workgroups of `threads` threads, each spinning spin_ticks of the
- * 100 MHz clock; out[2 i] = HW_ID, out[2 i + 1] = XCC_ID of workgroup i. */
-int64_t sc_debug_hwid(int32_t nwg, int32_t threads, int32_t spin_ticks, uint32_t* out);
-/* Dispatch-contention probe: a panel-update SYRK "hog" (M x M triangle, K deep) on a
- * low-priority stream against a chain of nchain fused POTRF + TRSM launches (chain_rows
- * x 64 front) on the high-priority stream.  mode bit 0: hog stream CU-masked (every
- * mask_stride-th CU off), bit 1: hog replayed from a hipGraph, bit 2: chain from a
- * hipGraph.  out[8]: chain alone, hog alone, chain under hog, hog under chain, both
- * (ms), CUs available to the hog. */
-int64_t sc_debug_contention(int32_t M, int32_t K, int32_t chain_rows, int32_t nchain, int32_t mode,
-                            int32_t mask_stride, double* out);
 int64_t sc_device_count(void);
 /* Message of the last failing call on this thread. */
 const char* sc_last_error(void);

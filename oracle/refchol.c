@@ -233,6 +233,10 @@ EXPORT int64_t oracle_symbolic(int64_t n, const int64_t* Ap, const int32_t* Ai, 
  * (natural order) whose pivot d <= 0 ("A is not positive definite.",
  * chol.hpp:849-850).
  */
+/* Rows finished by the running oracle_chol (every 4096 rows), for monitors of
+ * long runs such as tests/golden/make_lap128_sketch.py.  Not part of the result. */
+EXPORT volatile int64_t oracle_chol_rows_done = 0;
+
 EXPORT int64_t oracle_chol(int64_t n, const int64_t* Ap, const int32_t* Ai, const double* Ax,
                            const int32_t* parent, const int64_t* Lp, int32_t* Li, double* Lx,
                            int faithful_workspace) {
@@ -251,6 +255,7 @@ EXPORT int64_t oracle_chol(int64_t n, const int64_t* Ap, const int32_t* Ai, cons
     for (int64_t j = 0; j < n; ++j) c[j] = Lp[j];
     int64_t status = 0;
     for (int64_t k = 0; k < n; ++k) {
+        if ((k & 4095) == 0) oracle_chol_rows_done = k;
         if (faithful_workspace) {
             /* chol.hpp:801-803: three length-n vectors per row */
             s = (int32_t*)malloc(sizeof(int32_t) * sz);
@@ -295,6 +300,7 @@ EXPORT int64_t oracle_chol(int64_t n, const int64_t* Ap, const int32_t* Ai, cons
         free(w);
         free(x);
     }
+    oracle_chol_rows_done = n;
     free(c);
     free(path);
     return status;

@@ -23,9 +23,6 @@ def probe(M, K, rows, nchain, mode, stride):
 def main():
     M, K, nchain = 12288, 1024, 32
     cases = [(0, 0), (1, 32), (1, 16), (1, 8), (2, 0), (3, 32), (3, 8), (4, 0), (6, 0), (7, 32), (7, 8)]
-    if len(sys.argv) > 1 and sys.argv[1] == "resident":
-        # bit 3: the hog as a resident grid of G workgroups (2 per CU fill the GPU at 512)
-        cases = [(0, 0)] + [(8, g) for g in (512, 496, 480, 448, 384, 256)] + [(14, 480), (14, 448)]
     for rows in (1024, 4096, 16384):
         for mode, stride in cases:
             rc, o = probe(M, K, rows, nchain, mode, stride)

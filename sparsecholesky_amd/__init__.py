@@ -70,13 +70,12 @@ class Options(C.Structure):
         ("lookahead", C.c_int32), ("inner_order", C.c_int32),
         ("asm_tile_min_m", C.c_int32), ("dist_split", C.c_int32), ("dist_cbb", C.c_int32),
         ("ordering", C.c_int32), ("dist_early", C.c_int32), ("dist_panel", C.c_int32),
-        ("cb_gather", C.c_int32), ("panel_tall", C.c_int32), ("trsm_fold", C.c_int32),
+        ("cb_gather", C.c_int32),
         ("dist_slab_block", C.c_int32), ("trsm_split_wg", C.c_int32),
         ("syrk_lean_kmax", C.c_int32), ("cb_tail_split", C.c_int32), ("tiny_dense", C.c_int32),
-        ("dist_asm", C.c_int32), ("la_grid", C.c_int32),
-        ("dist_pieces", C.c_int32), ("cb_slab", C.c_int32), ("cb_gather_min_w", C.c_int32),
-        ("la_split", C.c_int32), ("la_after", C.c_int32), ("cb_lean_kmin", C.c_int32),
-        ("cb_small_kmax", C.c_int32),
+        ("dist_asm", C.c_int32),
+        ("dist_pieces", C.c_int32), ("panel_psk", C.c_int32), ("psk_rows", C.c_int32),
+        ("psk_min_w", C.c_int32),
     ]
 
 

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/sparsecholesky.h"
+#include "../../include/sparsecholesky_debug.h"
 #include "numeric.hpp"
 #include "symbolic.hpp"
 
@@ -87,22 +88,16 @@ void sc_default_options(sc_options* opt) {
     opt->dist_early = 1;
     opt->dist_panel = 1;
     opt->cb_gather = 1;
-    opt->panel_tall = 0;
-    opt->trsm_fold = 0;
     opt->dist_slab_block = 2;
     opt->trsm_split_wg = 1024;
     opt->syrk_lean_kmax = 128;
     opt->cb_tail_split = 1;
     opt->tiny_dense = 1;
     opt->dist_asm = 1;
-    opt->la_grid = 0;
     opt->dist_pieces = 2;
-    opt->cb_slab = 0;
-    opt->cb_gather_min_w = 0;
-    opt->la_split = 1;
-    opt->la_after = 0;
-    opt->cb_lean_kmin = 65;
-    opt->cb_small_kmax = 0;
+    opt->panel_psk = 0;
+    opt->psk_rows = 64;
+    opt->psk_min_w = 0;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,
@@ -122,6 +117,8 @@ int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_opt
     }
     if (o.small_front_max > 128) o.small_front_max = 128;
     if (o.small_front_max < 0) o.small_front_max = 0;
+    if (o.lookahead != 0) o.lookahead = 1;
+    if (o.psk_rows != 128 && o.psk_rows != 256) o.psk_rows = 64;
     sc_symbolic* h = new (std::nothrow) sc_symbolic();
     if (!h) return SC_ERR_NOMEM;
     std::string err;

@@ -113,8 +113,7 @@ static int64_t bench_panel(int which, int M, int reps, double* out) {
 // on a low-priority stream -- and a "chain" of nchain dependent fused POTRF + TRSM
 // launches on a chain_rows x 64 front, on the high-priority stream.  mode bit 0: the hog
 // stream is CU-masked (every mask_stride-th CU off); bit 1: the hog is replayed from a
-// captured hipGraph; bit 2: the chain too (its own graph); bit 3: the hog is a resident
-// grid of mask_stride workgroups walking its tiles (no CU mask).  out[0] chain alone, out[1] hog
+// captured hipGraph; bit 2: the chain too (its own graph).  out[0] chain alone, out[1] hog
 // alone, out[2] chain under the hog (first chain start -> last chain end), out[3] hog
 // under the chain, out[4] both (wall), all ms; out[5] CUs the hog may use.
 int64_t debug_contention(int M, int K, int chain_rows, int nchain, int mode, int mask_stride, double* out) {
@@ -129,7 +128,7 @@ int64_t debug_contention(int M, int K, int chain_rows, int nchain, int mode, int
     const int ncu = prop.multiProcessorCount;
     int used = ncu;
     if (hipStreamCreateWithPriority(&s_chain, hipStreamNonBlocking, prio_hi) != hipSuccess) return SC_ERR_HIP;
-    if ((mode & 1) && !(mode & 8)) {
+    if (mode & 1) {
         std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
         used = 0;
         for (int c = 0; c < ncu; ++c)
@@ -157,12 +156,7 @@ int64_t debug_contention(int M, int K, int chain_rows, int nchain, int mode, int
     hipGraph_t g_hog = nullptr, g_chain = nullptr;
     hipGraphExec_t x_hog = nullptr, x_chain = nullptr;
     DevPlan P {};
-    const int resident = (mode & 8) ? mask_stride : 0;  // bit 3: the hog as a resident grid of this size
-    auto hog_direct = [&]() {
-        if (resident > 0)
-            return launch_syrk_resident((GemmTask*)bt, (int2*)bl, ntiles, SYRK_BT_LARGE, 0, s_hog, 0, GatherTab {}, resident);
-        return launch_syrk((GemmTask*)bt, (int2*)bl, ntiles, SYRK_BT_LARGE, 0, s_hog);
-    };
+    auto hog_direct = [&]() { return launch_syrk((GemmTask*)bt, (int2*)bl, ntiles, SYRK_BT_LARGE, 0, s_hog); };
     auto hog = [&]() {
         if (x_hog) return hipGraphLaunch(x_hog, s_hog);
         return hog_direct();
@@ -284,86 +278,12 @@ int64_t debug_contention(int M, int K, int chain_rows, int nchain, int mode, int
     return rc;
 }
 
-// General-product kernel (TAG 2) on synthetic operands: M x N output, K deep, 128 x 128
-// tiles.  arg bit 0: out = Cin - acc read from C itself (in place) instead of a plain
-// store; bit 1: B lower triangular (ktri); bit 2: the TAG 0 SYRK on the same M x N
-// trapezoid instead (reference).  TFLOP/s of the executed products.
-static int64_t bench_gemm(int M, int Nn, int K, int reps, int arg, double* out) {
-    const size_t na = (size_t)M * K, nb = (size_t)Nn * K, nc = (size_t)M * Nn;
-    void *bA = nullptr, *bB = nullptr, *bC = nullptr, *bt = nullptr, *bl = nullptr;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    int64_t rc = SC_OK;
-    if (hipMalloc(&bA, na * 8) || hipMalloc(&bB, nb * 8) || hipMalloc(&bC, nc * 8) || hipEventCreate(&e0) ||
-        hipEventCreate(&e1)) {
-        rc = SC_ERR_DEVMEM;
-    } else {
-        (void)launch_fill_random((double*)bA, (int64_t)na, nullptr);
-        (void)launch_fill_random((double*)bB, (int64_t)nb, nullptr);
-        (void)launch_fill_random((double*)bC, (int64_t)nc, nullptr);
-        GemmTask t {};
-        t.A = (const double*)bA;
-        t.lda = M;
-        t.M = M;
-        t.N = Nn;
-        t.K = K;
-        t.C = (double*)bC;
-        t.ldc = M;
-        const bool syrk = arg & 4;
-        if (!syrk) {
-            t.B = (const double*)bB;
-            t.ldb = Nn;
-            t.Cin = (arg & 1) ? (const double*)bC : nullptr;
-            t.ldin = M;
-            t.sign = (arg & 1) ? -1.0 : 1.0;
-            t.ktri = (arg & 2) ? 1 : 0;
-        }
-        std::vector<int2> tiles;
-        if (syrk)
-            append_tiles(tiles, 0, M, Nn, SYRK_BT_LARGE);
-        else
-            append_tiles_full(tiles, 0, M, Nn, SYRK_BT_LARGE);
-        xcd_order(tiles.data(), (int64_t)tiles.size());
-        (void)hipMalloc(&bt, sizeof(GemmTask));
-        (void)hipMalloc(&bl, tiles.size() * sizeof(int2));
-        (void)hipMemcpy(bt, &t, sizeof(t), hipMemcpyHostToDevice);
-        (void)hipMemcpy(bl, tiles.data(), tiles.size() * sizeof(int2), hipMemcpyHostToDevice);
-        const int n = (int)tiles.size();
-        auto go = [&]() { return launch_syrk((GemmTask*)bt, (int2*)bl, n, SYRK_BT_LARGE, syrk ? 0 : 2, nullptr); };
-        (void)go();
-        (void)hipDeviceSynchronize();
-        (void)hipEventRecord(e0, nullptr);
-        for (int r = 0; r < reps; ++r) (void)go();
-        (void)hipEventRecord(e1, nullptr);
-        (void)hipEventSynchronize(e1);
-        float ms = 0.f;
-        (void)hipEventElapsedTime(&ms, e0, e1);
-        double fl = 0.0;
-        if (syrk)
-            fl = 2.0 * K * ((double)Nn * M - (double)Nn * (Nn - 1) / 2.0);
-        else if (arg & 2)
-            for (int tj = 0; tj * SYRK_BT_LARGE < Nn; ++tj)
-                fl += 2.0 * M * std::min(SYRK_BT_LARGE, Nn - tj * SYRK_BT_LARGE) *
-                      (double)std::min(K, (tj + 1) * SYRK_BT_LARGE);
-        else
-            fl = 2.0 * M * (double)Nn * K;
-        *out = fl * reps / (ms * 1e-3) / 1e12;
-        if (hipGetLastError() != hipSuccess) rc = SC_ERR_HIP;
-    }
-    for (void* p : {bA, bB, bC, bt, bl})
-        if (p) (void)hipFree(p);
-    if (e0) (void)hipEventDestroy(e0);
-    if (e1) (void)hipEventDestroy(e1);
-    return rc;
-}
-
 // which 0: register-only fp64 MFMA peak probe (M blocks of 4 waves, K iterations,
 // arg accumulators); 1 / 5: the SYRK kernel on an M x M triangle, K deep, tile arg
 // (64 / 128), with / without the XCD tile order; 2 / 3: bench_panel.  TFLOP/s or us.
 int64_t debug_bench(int which, int M, int K, int reps, int arg, double* tflops) {
     *tflops = 0.0;
     if (which == 2 || which == 3) return bench_panel(which, M, reps, tflops);
-    // which 7: general products, N = K (the tall solve / outer-update shapes), arg as bench_gemm
-    if (which == 7) return bench_gemm(M, K, K, reps, arg, tflops);
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return SC_ERR_HIP;
     double flops = 0.0;

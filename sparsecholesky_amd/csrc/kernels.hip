@@ -211,23 +211,12 @@ __global__ __launch_bounds__(256) void assemble_tile_kernel(DevPlan P, const int
                     if (rr[q][ch] >= 0) T[tc[q] * ASM_ROWS + rr[q][ch] - r0] += v[q][ch];
         }
     }
-    // own columns: store the lower part once.  A front of the tall-TRSM-by-inverse mode
-    // (tall_off >= 0) sends the rows below its first slab's diagonal block, in that
-    // slab's columns, to its staging buffer (ld m - tnb, row tnb first): the tall solve
-    // reads them from there and writes the final L21 into the panel.
-    const int64_t toff = P.tall_off ? P.tall_off[s] : -1;
-    const int tnb = toff >= 0 ? min(w, P.tall_nbo) : 0;
-    const int trow = tnb + (toff >= 0 ? P.tall_skip : 0);  // first staged row (ld m - trow)
+    // own columns: store the lower part once
     for (int j = j0 + wid; j < j1; j += 4) {
         if (j < cl.x || j >= cl.y) continue;
         double* col = (j < w) ? panel + (int64_t)j * m : cbs + (int64_t)(j - w) * mb - w;
         const double* Tc = T + (j - j0) * ASM_ROWS - r0;
-        if (j < tnb) {
-            double* tcol = P.tall_pool + toff + (int64_t)j * (m - trow) - trow;
-            for (int r = max(r0, j) + lane; r < r1; r += 64) (r < trow ? col : tcol)[r] = Tc[r];
-        } else {
-            for (int r = max(r0, j) + lane; r < r1; r += 64) col[r] = Tc[r];
-        }
+        for (int r = max(r0, j) + lane; r < r1; r += 64) col[r] = Tc[r];
     }
 }
 
@@ -1230,19 +1219,12 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_partial_kernel(DevPlan P, cons
 // every workgroup of the block has read it: t.w - 1 indexes the block's arrival
 // counter, and the last workgroup to arrive stores L11 and rearms the counter.  A
 // block with no rows below gets one task with r0 >= m (factor and store only).
-#ifndef TRSM_PRE_CH
-#define TRSM_PRE_CH 16  // previous-block values of a row in flight per chunk (VGPR budget)
-#endif
 template <int PRE>
 __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, const TrsmTask* __restrict__ tasks,
                                                                  int32_t* __restrict__ arrive) {
     static_assert(TRSM_ROWS == 256, "the fused POTRF maps 4 x 4 tiles onto 256 threads");
     __shared__ double2 S[TRSM64_STREAM / 2];
     __shared__ __attribute__((aligned(16))) double colbuf[2 * 4 * COLB];
-    // PRE: Lp[j * LPD + k] = L(k0 + j, k0 - 64 + k), the pending block's rows of this diagonal
-    // block, row-major (k contiguous: a row's update reads two k per ds_read_b128)
-    constexpr int LPD = PNB + 2;
-    __shared__ __attribute__((aligned(16))) double Lp[PRE == 1 ? PNB * LPD : 2];
     __shared__ int s_last;
     const TrsmTask t = tasks[blockIdx.x];
     const int s = t.s, k0 = t.k0, r0 = t.r0, r1 = t.r1;
@@ -1255,14 +1237,6 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
     if (nb < PNB) return;  // partial blocks: potrf_tiles_kernel + trsm_partial_kernel
     double* blk = pan + (int64_t)k0 * m + k0;
     double* Sd = reinterpret_cast<double*>(S);
-    constexpr bool pre = PRE == 1;
-    if (pre) {  // the previous block's rows of this diagonal block, final since the last launch
-#pragma unroll
-        for (int q = 0; q < PNB * PNB / 256; ++q) {
-            const int e = tid + 256 * q, k = e >> 6, j = e & 63;  // lanes along j: coalesced rows
-            Lp[j * LPD + k] = pan[(int64_t)(k0 - PNB + k) * m + k0 + j];
-        }
-    }
     SmallRegs<1> R;
     small_tiles<1>(R, PNB, PNB);
 #pragma unroll
@@ -1294,26 +1268,6 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
         for (int c = 0; c < PNB; ++c) buf_st(r[c], rs, voff, c * m * 8);
         return;
     }
-    if (pre) {  // diagonal block -= Lp^T Lp (this thread's 4 x 4 tile)
-        __syncthreads();
-        if (R.bi[0] >= 0) {
-            const int i0 = 4 * R.bi[0], j0 = 4 * R.bj[0];
-#pragma unroll 2
-            for (int k = 0; k < PNB; k += 2) {
-                double2 li[4], lj[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    li[r] = *reinterpret_cast<const double2*>(Lp + (i0 + r) * LPD + k);
-                    lj[r] = *reinterpret_cast<const double2*>(Lp + (j0 + r) * LPD + k);
-                }
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int c = 0; c < 4; ++c)
-                        R.v[0][r * 4 + c] = fma(-li[r].y, lj[c].y, fma(-li[r].x, lj[c].x, R.v[0][r * 4 + c]));
-            }
-        }
-    }
     if (SC_POTRF_FAST)  // every block load has returned
         small_steps1_fast(R, colbuf, PNB, P.info, c0 + k0);
     else
@@ -1334,24 +1288,6 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
     double r[PNB];
 #pragma unroll
     for (int c = 0; c < PNB; ++c) r[c] = buf_ld(rs, voff, c * m * 8);
-    if (pre) {  // this row -= L(row, previous block) Lp: its 64 previous-block values streamed in
-        const __amdgpu_buffer_rsrc_t rp = buf_rsrc(pan + (int64_t)(k0 - PNB) * m, (uint32_t)m * PNB * 8u);
-#pragma unroll 1
-        for (int k0c = 0; k0c < PNB; k0c += TRSM_PRE_CH) {
-            double l[TRSM_PRE_CH];
-#pragma unroll
-            for (int q = 0; q < TRSM_PRE_CH; ++q) l[q] = buf_ld(rp, voff, (k0c + q) * m * 8);
-#pragma unroll
-            for (int c = 0; c < PNB; ++c) {
-                const double* lc = Lp + c * LPD + k0c;
-#pragma unroll
-                for (int q = 0; q < TRSM_PRE_CH; q += 2) {
-                    const double2 v = *reinterpret_cast<const double2*>(lc + q);
-                    r[c] = fma(-l[q + 1], v.y, fma(-l[q], v.x, r[c]));
-                }
-            }
-        }
-    }
     __syncthreads();
     if (tid == 0) {
         const int k1 = k0 + PNB;
@@ -1510,14 +1446,9 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const in
 // over k < K (A column-major, ld lda; rows past M (i) / N (j) read as 0).  BK = 16,
 // register-staged double-buffered LDS (As / Bs: 2 stages of BK x (BT + 16) doubles
 // each, +128 B row pad: the two k-rows read by a half-wave hit disjoint banks).
-// AGLC: the row0 operand is loaded with glc (L1 bypassed: rows this workgroup
-// itself stored earlier in the same launch).
-// SEPB: the col0 operand comes from its own matrix Bm (ld ldb) instead of A (general
-// products, gemm_tile_body); SEPB = 0 compiles to exactly the single-operand loop.
-template <int BT, int WM, int WN, int AGLC = 0, int BK = 16, int SEPB = 0>
+template <int BT, int WM, int WN, int BK = 16>
 __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t lda, int K, int M, int N, int row0,
-                                           int col0, double4_t (&acc)[BT / WM / 16][BT / WN / 16], double* smem,
-                                           const double* __restrict__ Bm = nullptr, int64_t ldb = 0) {
+                                           int col0, double4_t (&acc)[BT / WM / 16][BT / WN / 16], double* smem) {
     static_assert(BK == 16 || BK == 8, "four-deep k sub-steps of the MFMA");
     constexpr int NT = 64 * WM * WN;
     constexpr int LDT = BT + 16;
@@ -1537,20 +1468,13 @@ __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t
     double ra[PER], rb[PER];
     auto gload = [&](int k0) {
         const __amdgpu_buffer_rsrc_t rs = buf_rsrc(A + (int64_t)k0 * lda, (uint32_t)(min(BK, K - k0) * lda * 8));
-        __amdgpu_buffer_rsrc_t rsb = rs;
-        if constexpr (SEPB) rsb = buf_rsrc(Bm + (int64_t)k0 * ldb, (uint32_t)(min(BK, K - k0) * ldb * 8));
-        const int64_t ldbb = SEPB ? ldb : lda;
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
             const int e = tid + q * NT;
             const int r = e % BT, kk = e / BT;
             const int gr = row0 + r, gc = col0 + r;
-            const int va = gr < M ? (int)((gr + kk * lda) * 8) : BUF_DEAD;
-            if constexpr (AGLC)
-                ra[q] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, va, 0, 1));
-            else
-                ra[q] = buf_ld(rs, va, 0);
-            rb[q] = buf_ld(rsb, gc < N ? (int)((gc + kk * ldbb) * 8) : BUF_DEAD, 0);
+            ra[q] = buf_ld(rs, gr < M ? (int)((gr + kk * lda) * 8) : BUF_DEAD, 0);
+            rb[q] = buf_ld(rs, gc < N ? (int)((gc + kk * lda) * 8) : BUF_DEAD, 0);
         }
     };
     auto sstore = [&](int buf) {
@@ -1635,7 +1559,7 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
         for (int b = 0; b < RTN; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
     // (operand stages by LDS-DMA, buffer_load_dwordx4 ... lds per 1-KB k-row, measured
     // slower: 510.5 ms with two 16-deep stages, 521.5 with four 8-deep, vs 505.7-507.3)
-    mfma_kloop<BT, WM, WN, 0, BK>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
+    mfma_kloop<BT, WM, WN, BK>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
 
     if constexpr (TAG == 1) {
         if (T.gs >= 0) {  // the front's CB is not assembled: gather the children's entries
@@ -1696,284 +1620,221 @@ __global__ __launch_bounds__(64 * WM * WN, LEAN ? (TAG ? 5 : 6) : 1) void syrk_m
     syrk_tile_body<BT, WM, WN, TAG, EPI, LEAN>(tasks, tiles, blockIdx.x, gblk, gseg);
 }
 
-// Resident-grid instance: a grid smaller than the GPU's workgroup slots walks the tile
-// list with stride gridDim.x (a multiple of 8, so workgroup b keeps XCD b % 8's tiles).
-// Every workgroup is dispatched at once and nothing stays queued behind it: a queued
-// grid holds the dispatcher, and a small critical-path launch on another stream waits
-// for all of it (the contention probe); with slots left free, it does not.
-template <int BT, int WM, int WN, int TAG, int EPI>
-__global__ __launch_bounds__(64 * WM * WN, 4) void syrk_mfma_resident_kernel(const GemmTask* __restrict__ tasks,
-                                                                           const int2* __restrict__ tiles, int ntiles,
-                                                                           const int64_t* __restrict__ gblk,
-                                                                           const GSeg* __restrict__ gseg) {
-    for (int b = blockIdx.x; b < ntiles; b += gridDim.x) {
-        if (b != (int)blockIdx.x) __syncthreads();  // the previous tile's LDS reads are done
-        syrk_tile_body<BT, WM, WN, TAG, EPI, 0>(tasks, tiles, b, gblk, gseg);
-    }
-}
+// ---------------------------------------------------------------------------
+// Persistent slab chain (PSK): the 64-column chain of one slab [s0, s1) of every large
+// front of a level in ONE launch (the reference's dpotrf_ / cblas_dtrsm / cblas_dsyrk of
+// a supernode panel, chol.hpp:1263-1322, restated per 64-column step).  The per-step
+// launches (fused POTRF + TRSM, then the recursive inner update) cost two kernel
+// boundaries per step, and under a concurrent trailing update each waits for dispatch
+// slots.  Here one workgroup owns TR rows of the slab's rows [s0, m) for
+// the whole slab and walks the steps itself:
+//   step j (columns [c, c + 64)):
+//     the OWNER of the diagonal block (its rows hold row c) factors it in registers
+//       (small_steps1_fast), stores L11, publishes flag L11 = j + 1;
+//     every other workgroup waits for that flag and streams L11 from memory;
+//     TRSM of the workgroup's rows below the block (trsm64_full, one lane per row);
+//     a workgroup whose rows lie in the slab's diagonal region publishes its step;
+//     the inner update of its own rows (recursive order: block j closes a run of
+//       2^t blocks, which updates the next 2^t blocks; K = 64 * 2^t), after waiting
+//       for the diagonal-region row blocks the update reads (always lower row blocks).
+// Every wait is on a lower row block of the same front, and the grid is row-block-major,
+// so the launch completes whatever residency it gets.  Hand-offs: plain stores ->
+// s_waitcnt vmcnt(0) -> barrier -> agent release -> relaxed flag store; consumer:
+// relaxed poll -> agent acquire -> barrier (MI355X_MICROARCH.md, inter-workgroup
+// visibility).  Same arithmetic in the same order as the per-step launches: the
+// factor is bitwise identical.
+constexpr uint64_t PSK_TIMEOUT = 400000000ull;  // 4 s of the 100 MHz clock: a lost flag ends the wait
 
-// General products of the tall-TRSM-by-inverse panel mode (GemmTask, TAG 2):
-//   the tall solve    L21 = A21 X^T       (A21 staged out of place; X = inv(L11), ktri)
-//   the next slab's   C_out = C_in - L L^T (rows below its diagonal block to the staging
-//   outer update                          buffer the next tall solve reads)
-//   the inverse's     U^T = (B Xa)^T, then E = -Xb U (stored as E and E^T)
-//   doubling steps
-// Same K loop as the SYRK (B from its own matrix); the epilogue reads Cin (if any) for a
-// whole two-MFMA-row chunk before its stores (Cin never aliases C or Ct here).
-template <int BT, int WM, int WN>
-__device__ __forceinline__ void gemm_tile_body(const GemmTask* __restrict__ tasks, const int2* __restrict__ tiles,
-                                               int bidx) {
-    constexpr int BK = 16, LDT = BT + 16;
-    constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
-    __shared__ double smem[2 * 2 * BK * LDT];
-    const int2 tl = tiles[bidx];
-    const GemmTask T = tasks[tl.x];
-    const int ti = tl.y >> 16, tj = tl.y & 0xffff;
-    const int row0 = ti * BT, col0 = tj * BT;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wr = wid / WN, wc = wid % WN;
-    if (wid >= WM * WN / 2) __builtin_amdgcn_s_setprio(1);
-    double4_t acc[RTM][RTN];
-#pragma unroll
-    for (int a = 0; a < RTM; ++a)
-#pragma unroll
-        for (int b = 0; b < RTN; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
-    const int K = T.ktri ? min(T.K, col0 + BT) : T.K;
-    if (K > 0) mfma_kloop<BT, WM, WN, 0, BK, 1>(T.A, T.lda, K, T.M, T.N, row0, col0, acc, smem, T.B, T.ldb);
-    const double* __restrict__ Cin = T.Cin;
-    double* __restrict__ C = T.C;
-    double* __restrict__ Ct = T.Ct;
-    const double sg = T.sign;
-    if (!Cin && !Ct && !T.lower) {
-        // plain store (the tall solve): through a buffer resource over the tile's columns,
-        // dead elements masked by range, no branches
-        const __amdgpu_buffer_rsrc_t rc =
-            buf_rsrc(C + (int64_t)col0 * T.ldc, (uint32_t)(min(BT, T.N - col0) * T.ldc * 8));
-#pragma unroll
-        for (int a = 0; a < RTM; ++a)
-#pragma unroll
-            for (int b = 0; b < RTN; ++b)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int gi = row0 + wr * (BT / WM) + a * 16 + MFMA_F64_ROW(lane, r);
-                    const int gj = col0 + wc * (BT / WN) + b * 16 + (lane & 15);
-                    const int off = gi < T.M ? (int)((gi + (int64_t)(gj - col0) * T.ldc) * 8) : BUF_DEAD;
-                    buf_st(sg * acc[a][b][r], rc, off, 0);
-                }
-        return;
-    }
-    constexpr int EA = 1;  // MFMA tile rows per epilogue chunk (2 spills in the resident instance)
-#pragma unroll
-    for (int a0 = 0; a0 < RTM; a0 += EA) {
-        double v[EA][RTN][4];
-#pragma unroll
-        for (int a = 0; a < EA; ++a)
-#pragma unroll
-            for (int b = 0; b < RTN; ++b)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int gi = row0 + wr * (BT / WM) + (a0 + a) * 16 + MFMA_F64_ROW(lane, r);
-                    const int gj = col0 + wc * (BT / WN) + b * 16 + (lane & 15);
-                    const bool live = gi < T.M && gj < T.N && (!T.lower || gi >= gj);
-                    v[a][b][r] = (Cin && live) ? Cin[gi + (int64_t)gj * T.ldin] : 0.0;
-                }
-#pragma unroll
-        for (int a = 0; a < EA; ++a)
-#pragma unroll
-            for (int b = 0; b < RTN; ++b)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int gi = row0 + wr * (BT / WM) + (a0 + a) * 16 + MFMA_F64_ROW(lane, r);
-                    const int gj = col0 + wc * (BT / WN) + b * 16 + (lane & 15);
-                    const bool live = gi < T.M && gj < T.N && (!T.lower || gi >= gj);
-                    if (!live) continue;
-                    const double x = fma(sg, acc[a0 + a][b][r], v[a][b][r]);
-                    if (C) C[gi + (int64_t)gj * T.ldc] = x;
-                    if (Ct) Ct[gj + (int64_t)gi * T.ldt] = x;
-                }
-    }
-}
-
-template <int BT, int WM, int WN>
-__global__ __launch_bounds__(64 * WM * WN, 4) void gemm_mfma_kernel(const GemmTask* __restrict__ tasks,
-                                                                  const int2* __restrict__ tiles) {
-    gemm_tile_body<BT, WM, WN>(tasks, tiles, blockIdx.x);
-}
-
-// resident-grid instance (see syrk_mfma_resident_kernel)
-template <int BT, int WM, int WN>
-__global__ __launch_bounds__(64 * WM * WN, 4) void gemm_mfma_resident_kernel(const GemmTask* __restrict__ tasks,
-                                                                           const int2* __restrict__ tiles, int ntiles) {
-    for (int b = blockIdx.x; b < ntiles; b += gridDim.x) {
-        if (b != (int)blockIdx.x) __syncthreads();
-        gemm_tile_body<BT, WM, WN>(tasks, tiles, b);
-    }
-}
-
-// 64-block inverses of a slab's factored diagonal block into the dense scratch X (and
-// XT = X^T) of the tall-TRSM-by-inverse mode: one wave per 64-column block q, lane j
-// solving e_j L_qq^-T (the generated TRSM code, as solve_inv_kernel) -- column j of
-// inv(L_qq).  The rest of block column q of X (rows above the block; the doubling steps
-// fill the rows below) and block row q of XT are zeroed, so the dense X is exact.
-// Wave 0 solves; waves 1-3 write the zeros meanwhile (up to 2 x 1024 x 64 doubles per
-// block: one wave alone took 0.27 ms per launch at 128^3 level 17).
-__global__ __launch_bounds__(256) void xinv64_kernel(DevPlan P, const XinvTask* __restrict__ tasks) {
-    __shared__ double2 S[TRSM64_STREAM / 2];
-    __shared__ double Lc[PNB * (PNB + 2)];
-    __shared__ double invd[PNB];
-    const XinvTask t = tasks[blockIdx.x];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int m = P.sn_m[t.s];
-    const int k0 = t.c0 + PNB * t.q;               // front column of the block
-    const int nb = min(PNB, t.nbs - PNB * t.q);    // > 0
-    const int b0 = PNB * t.q;
-    const double* blk = P.panel_pool + P.panel_off[t.s] + (int64_t)k0 * m + k0;
-    double r[PNB];
-    if (wid == 0) {
-#pragma unroll
-        for (int j = 0; j < PNB; ++j) r[j] = (j < nb && lane < nb && lane >= j) ? blk[(int64_t)j * m + lane] : 0.0;
-        if (nb == PNB) {
-            double* Sd = reinterpret_cast<double*>(S);
-#pragma unroll
-            for (int j = 0; j < PNB; ++j)
-                if (lane >= j) Sd[PNB * j - j * (j - 1) / 2 + (lane - j)] = lane == j ? 1.0 / r[j] : r[j];
-        } else {
-            constexpr int LD = PNB + 2;
-#pragma unroll
-            for (int j = 0; j < PNB; ++j) {
-                Lc[j * LD + lane] = r[j];
-                if (lane == j) invd[j] = j < nb ? 1.0 / r[j] : 0.0;
-            }
-        }
-    }
+__device__ __forceinline__ void psk_signal(int32_t* flag, int32_t value) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (wid == 0) {
-#pragma unroll
-        for (int c = 0; c < PNB; ++c) r[c] = c == lane ? 1.0 : 0.0;
-        if (nb == PNB)
-            trsm64_full(r, S);
-        else
-            trsm_steps<0>(r, Lc, invd, nb);
-        // r[c] = inv(L_qq)(c, lane) = X(b0 + c, b0 + lane) = XT(b0 + lane, b0 + c)
-#pragma unroll
-        for (int c = 0; c < PNB; ++c)
-            if (c < nb && lane < nb) {
-                const double x = c >= lane ? r[c] : 0.0;
-                t.X[b0 + c + (int64_t)(b0 + lane) * t.ldx] = x;
-                t.XT[b0 + lane + (int64_t)(b0 + c) * t.ldx] = x;  // coalesced across lanes
-            }
-    } else {
-        // zeros, threads along rows (coalesced): X above the block in its block column
-        // (X is lower triangular) and XT below the block in its block column (XT upper)
-        const int z = tid - 64;
-        for (int c = 0; c < nb; ++c) {
-            double* xc = t.X + (int64_t)(b0 + c) * t.ldx;
-            for (int i = z; i < b0; i += 192) xc[i] = 0.0;
-            double* tc = t.XT + (int64_t)(b0 + c) * t.ldx;
-            for (int i = b0 + PNB + z; i < t.nbs; i += 192) tc[i] = 0.0;
-        }
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
-hipError_t launch_xinv64(const DevPlan& P, const XinvTask* tasks, int count, hipStream_t st) {
-    if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(xinv64_kernel, dim3(count), dim3(256), 0, st, P, tasks);
-    return hipGetLastError();
+// lane 0 only: true once *flag >= target, false on timeout
+__device__ __forceinline__ bool psk_poll(const int32_t* flag, int32_t target, uint64_t t0) {
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > PSK_TIMEOUT) return false;
+    }
+    return true;
 }
 
-
-// Tall TRSM of a slab (the reference's cblas_dtrsm, chol.hpp:1292, for the rows below
-// a slab's diagonal block): rows [r0, r0 + 64) of front s against the slab's factored
-// diagonal block L_kk (columns [a, b)), in place, X = A L_kk^-T.  Per 64-column block j:
-//   Y = A(:, j) - X(:, < j) L(j, < j)^T   (MFMA, K = 64 j; X from this workgroup's own
-//                                           earlier stores, loaded with glc)
-//   X(:, j) = Y inv(L_jj)^T                (MFMA, K = 64; inv(L_jj) in the block's strict
-//                                           upper triangle, panel_inv / solve_inv_kernel)
-// A workgroup owns its rows, so a slab's whole tall part is one launch and the 64-column
-// chain runs on the diagonal block's rows only.
-__global__ __launch_bounds__(256) void panel_tall_kernel(DevPlan P, const int4* __restrict__ tasks) {
+template <int TR>
+__global__ __launch_bounds__(256, 2) void psk_kernel(DevPlan P, PskArgs A) {
+    static_assert(TR == 64 || TR == 128 || TR == 256, "row blocks of 64, 128 or 256 rows");
     constexpr int BT = 64, WM = 2, WN = 2, BK = 16, LDT = BT + 16;
     constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
-    __shared__ double smem[2 * 2 * BK * LDT];  // K-loop stages; then Y (k-major, ld LDT)
-    __shared__ double Bs[PNB * LDT];           // inv(L_jj)^T, k-major
-    const int4 t = tasks[blockIdx.x];
-    const int s = t.x, a = t.y, r0 = t.z, b = t.w;
+    __shared__ double2 S[TRSM64_STREAM / 2];
+    __shared__ __attribute__((aligned(16))) double colbuf[2 * 4 * COLB];
+    __shared__ double smem[2 * 2 * BK * LDT];
+    __shared__ int s_fail;
+    const PskWg g = A.wg[blockIdx.x];
+    const PskFront F = A.fr[g.f];
+    const int s = F.s, m = F.m;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wr = wid / WN, wc = wid % WN;
-    const int m = P.sn_m[s];
+    const int cg = P.sn_start[s];  // global column of front column 0
     double* pan = P.panel_pool + P.panel_off[s];
-    const double* A = pan + (int64_t)a * m;  // column a
-    double* Ys = smem;
-    for (int c0 = 0; a + c0 < b; c0 += PNB) {
-        const int nb = min(PNB, b - a - c0);
-        double4_t acc[RTM][RTN];
-#pragma unroll
-        for (int i = 0; i < RTM; ++i)
-#pragma unroll
-            for (int j = 0; j < RTN; ++j) acc[i][j] = (double4_t){0.0, 0.0, 0.0, 0.0};
-        if (c0 > 0) mfma_kloop<BT, WM, WN, 1>(A, m, c0, m, a + c0 + nb, r0, a + c0, acc, smem);
-        // columns a + c0 .. + nb of the rows: a buffer resource over them (dead rows / columns masked)
-        const __amdgpu_buffer_rsrc_t rc = buf_rsrc(pan + (int64_t)(a + c0) * m, (uint32_t)((int64_t)nb * m * 8));
-        // Y = A - acc into LDS, k-major (Ys[col * LDT + row]: the MFMA A-operand layout below)
-#pragma unroll
-        for (int i = 0; i < RTM; ++i)
-#pragma unroll
-            for (int j = 0; j < RTN; ++j)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int lr = wr * (BT / WM) + i * 16 + MFMA_F64_ROW(lane, r);
-                    const int lc = wc * (BT / WN) + j * 16 + (lane & 15);
-                    const bool live = r0 + lr < m && lc < nb;
-                    Ys[lc * LDT + lr] = buf_ld(rc, live ? (int)((lc * m + r0 + lr) * 8) : BUF_DEAD, 0) - acc[i][j][r];
-                }
-        // inv(L_jj)^T: Bs[k][c] = inv(c, k) = block (k, c) for k < c, 1 / L(k, k) at k = c
-        const double* blk = pan + (int64_t)(a + c0) * m + a + c0;
-#pragma unroll
-        for (int q = 0; q < PNB * PNB / 256; ++q) {
-            const int e = tid + 256 * q, c = e >> 6, k = e & 63;  // lanes along k: coalesced in column c
-            double v = 0.0;
-            if (k < nb && c < nb && k <= c) {
-                const double x = blk[(int64_t)c * m + k];
-                v = k == c ? 1.0 / x : x;
+    int32_t* fl = A.flags + F.flag0;
+    const int r0 = F.s0 + g.rb * TR, r1 = min(m, r0 + TR);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    double* Sd = reinterpret_cast<double*>(S);
+    if (tid == 0) s_fail = 0;
+    // lane 0 waits for every flag of fl[idx[0..n)] >= target, then acquires
+    auto wait_flags = [&](int lo, int hi, int target, bool l11) {
+        if (tid == 0) {
+            bool ok = true;
+            if (l11) ok = psk_poll(fl, target, t0);
+            for (int q = lo; ok && q < hi; ++q)
+                if (q != g.rb) ok = psk_poll(fl + 1 + q, target, t0);
+            if (!ok && !s_fail) {
+                s_fail = 1;
+                report_fail(P.info, cg + F.s0);  // a lost hand-off surfaces as a failed factorization
+                
             }
-            Bs[k * LDT + c] = v;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();
-        // X = Y inv^T (K = 64)
+    };
+    for (int j = 0; j < F.nfull; ++j) {
+        const int c = F.s0 + PNB * j, k1 = c + PNB;
+        if (r1 <= c) break;  // every row of this workgroup lies above column c
+        double* blk = pan + (int64_t)c * m + c;
+        if (r0 <= c) {  // owner of the diagonal block: factor it in registers
+            SmallRegs<1> R;
+            small_tiles<1>(R, PNB, PNB);
 #pragma unroll
-        for (int i = 0; i < RTM; ++i)
+            for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int j = 0; j < RTN; ++j) acc[i][j] = (double4_t){0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-        for (int kk = 0; kk < PNB; kk += 4) {
-            const int krow = kk + (lane >> 4);
-            double av[RTM], bv[RTN];
-#pragma unroll
-            for (int i = 0; i < RTM; ++i) av[i] = Ys[krow * LDT + wr * (BT / WM) + i * 16 + (lane & 15)];
-#pragma unroll
-            for (int j = 0; j < RTN; ++j) bv[j] = Bs[krow * LDT + wc * (BT / WN) + j * 16 + (lane & 15)];
-#pragma unroll
-            for (int i = 0; i < RTM; ++i)
-#pragma unroll
-                for (int j = 0; j < RTN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], bv[j], acc[i][j], 0, 0, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < RTM; ++i)
-#pragma unroll
-            for (int j = 0; j < RTN; ++j)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int lr = wr * (BT / WM) + i * 16 + MFMA_F64_ROW(lane, r);
-                    const int lc = wc * (BT / WN) + j * 16 + (lane & 15);
-                    const bool live = r0 + lr < m && lc < nb;
-                    buf_st(acc[i][j][r], rc, live ? (int)((lc * m + r0 + lr) * 8) : BUF_DEAD, 0);
+                for (int cc = 0; cc < 4; ++cc) {
+                    const int i = 4 * R.bi[0] + r, jj = 4 * R.bj[0] + cc;
+                    R.v[0][r * 4 + cc] = (R.bi[0] >= 0 && i >= jj) ? blk[(int64_t)jj * m + i] : 0.0;
                 }
-        // X(:, j) complete before the next block's K loop reads it back (glc) and before
-        // Ys / Bs are overwritten
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            small_steps1_fast(R, colbuf, PNB, P.info, cg + c);
+            if (R.bi[0] >= 0) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int cc = 0; cc < 4; ++cc) {
+                        const int i = 4 * R.bi[0] + r, jj = 4 * R.bj[0] + cc;
+                        if (i >= jj) {
+                            const double v = R.v[0][r * 4 + cc];
+                            blk[(int64_t)jj * m + i] = v;
+                            Sd[PNB * jj - jj * (jj - 1) / 2 + (i - jj)] = (i == jj) ? 1.0 / v : v;
+                        }
+                    }
+            }
+            psk_signal(fl, j + 1);
+        } else {  // wait for L11, stream it from memory (lanes along rows: coalesced)
+            wait_flags(0, 0, j + 1, true);
+#pragma unroll 4
+            for (int q = 0; q < PNB * PNB / 256; ++q) {
+                const int e = tid + 256 * q, jj = e >> 6, i = e & 63;
+                if (i >= jj) {
+                    const double v = blk[(int64_t)jj * m + i];
+                    Sd[PNB * jj - jj * (jj - 1) / 2 + (i - jj)] = (i == jj) ? 1.0 / v : v;
+                }
+            }
+        }
+        // TRSM of this workgroup's rows below the block: one lane per row
+        if (max(r0, k1) < r1) {
+            const int row = r0 + tid;
+            const bool live = tid < TR && row >= k1 && row < r1;
+            const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pan + (int64_t)c * m, (uint32_t)m * PNB * 8u);
+            const int voff = live ? row * 8 : BUF_DEAD;
+            __syncthreads();  // the L11 stream is complete
+            if (tid < TR) {
+                double r[PNB];
+#pragma unroll
+                for (int q = 0; q < PNB; ++q) r[q] = buf_ld(rs, voff, q * m * 8);
+                trsm64_full(r, S);
+#pragma unroll
+                for (int q = 0; q < PNB; ++q) buf_st(r[q], rs, voff, q * m * 8);
+            }
+            // rows of the slab's diagonal region feed other row blocks' inner updates
+            if (r0 < F.s1) psk_signal(fl + 1 + g.rb, j + 1);
+        }
+        __syncthreads();  // the stream S is read by every TRSM lane before the next step rebuilds it
+        if (k1 >= F.s1) continue;
+        // inner update of this workgroup's rows: columns [k1, cend), K = [ka, k1)
+        int ka, cend;
+        if (F.inner) {
+            const int span = PNB << __builtin_ctz((unsigned)(j + 1));
+            ka = k1 - span;
+            cend = min(F.s1, k1 + span);
+        } else {
+            ka = c;
+            cend = F.s1;
+        }
+        const int cc1 = min(cend, r1);  // columns past the workgroup's last row are above the diagonal
+        if (max(r0, k1) >= r1 || k1 >= cc1) continue;
+        // B operand: rows [k1, cc1) at columns [ka, k1), final in the row blocks holding them
+        wait_flags((k1 - F.s0) / TR, (cc1 - 1 - F.s0) / TR + 1, j + 1, false);
+        const int K = k1 - ka;
+#pragma unroll 1
+        for (int ct = k1; ct < cc1; ct += BT) {
+#pragma unroll 1
+            for (int rt = r0; rt < r1; rt += BT) {
+                if (rt + BT <= ct) continue;  // entirely above the diagonal
+                double4_t acc[RTM][RTN];
+#pragma unroll
+                for (int a = 0; a < RTM; ++a)
+#pragma unroll
+                    for (int b = 0; b < RTN; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
+                mfma_kloop<BT, WM, WN, BK>(pan + (int64_t)ka * m, m, K, r1, cend, rt, ct, acc, smem);
+                // C(i, jj) -= acc, i >= jj, i < r1, jj < cend: every load of a chunk before its stores
+                const __amdgpu_buffer_rsrc_t rc = buf_rsrc(pan + (int64_t)ct * m, (uint32_t)(min(BT, cend - ct) * m * 8));
+                double cv[RTM][RTN][4];
+                int offs[RTM][RTN][4];
+#pragma unroll
+                for (int a = 0; a < RTM; ++a)
+#pragma unroll
+                    for (int b = 0; b < RTN; ++b)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int gi = rt + wr * (BT / WM) + a * 16 + MFMA_F64_ROW(lane, r);
+                            const int gj = ct + wc * (BT / WN) + b * 16 + (lane & 15);
+                            const bool live = gi < r1 && gi >= gj;
+                            offs[a][b][r] = live ? (int)((gi + (int64_t)(gj - ct) * m) * 8) : BUF_DEAD;
+                            cv[a][b][r] = buf_ld(rc, offs[a][b][r], 0);
+                        }
+#pragma unroll
+                for (int a = 0; a < RTM; ++a)
+#pragma unroll
+                    for (int b = 0; b < RTN; ++b)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) buf_st(cv[a][b][r] - acc[a][b][r], rc, offs[a][b][r], 0);
+            }
+        }
+        // this workgroup's own C stores are read back by its next steps (same CU): drain them
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
+    // the last workgroup to finish re-arms the launch's flags (graph-replay safe)
+    __syncthreads();
+    if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(A.flags + A.nflags, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == A.nwg - 1) {
+            for (int q = 0; q <= A.nflags; ++q) __hip_atomic_store(A.flags + q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+hipError_t launch_psk(const DevPlan& P, const PskArgs& A, int rows, hipStream_t st) {
+    if (A.nwg <= 0) return hipSuccess;
+    if (rows == 256)
+        hipLaunchKernelGGL(psk_kernel<256>, dim3(A.nwg), dim3(256), 0, st, P, A);
+    else if (rows == 128)
+        hipLaunchKernelGGL(psk_kernel<128>, dim3(A.nwg), dim3(256), 0, st, P, A);
+    else
+        hipLaunchKernelGGL(psk_kernel<64>, dim3(A.nwg), dim3(256), 0, st, P, A);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -2034,8 +1895,6 @@ hipError_t launch_trsm_panel(const DevPlan& P, const TrsmTask* tasks, int count,
         hipLaunchKernelGGL(trsm_partial_kernel, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks);
     else if (pre == 2)
         hipLaunchKernelGGL(trsm_panel_g_kernel<2>, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks, arrive);
-    else if (pre)
-        hipLaunchKernelGGL(trsm_panel_g_kernel<1>, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks, arrive);
     else
         hipLaunchKernelGGL(trsm_panel_g_kernel<0>, dim3(count), dim3(TRSM_ROWS), 0, st, P, tasks, arrive);
     return hipGetLastError();
@@ -2058,48 +1917,9 @@ static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int b
                            gt.seg);
 }
 
-hipError_t launch_syrk_resident(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag,
-                                hipStream_t st, int epi, GatherTab gt, int grid) {
-    if (total_tiles <= 0) return hipSuccess;
-    grid = std::max(8, std::min(grid, (total_tiles + 7) / 8 * 8));
-    const dim3 g(grid);
-    if (tag == 2) {
-        if (bt == 128)
-            hipLaunchKernelGGL((gemm_mfma_resident_kernel<128, 2, 4>), g, dim3(512), 0, st, tasks, tiles, total_tiles);
-        else
-            hipLaunchKernelGGL((gemm_mfma_resident_kernel<64, 2, 2>), g, dim3(256), 0, st, tasks, tiles, total_tiles);
-        return hipGetLastError();
-    }
-#define SC_RES(BT_, WM_, WN_, TAG_, EPI_)                                                                          \
-    hipLaunchKernelGGL((syrk_mfma_resident_kernel<BT_, WM_, WN_, TAG_, EPI_>), g, dim3(64 * WM_ * WN_), 0, st, tasks, \
-                       tiles, total_tiles, gt.blk, gt.seg)
-    if (bt == 128) {
-        if (tag) {
-            if (epi) SC_RES(128, 2, 4, 1, 1); else SC_RES(128, 2, 4, 1, 0);
-        } else {
-            if (epi) SC_RES(128, 2, 4, 0, 1); else SC_RES(128, 2, 4, 0, 0);
-        }
-    } else {
-        if (tag) {
-            if (epi) SC_RES(64, 2, 2, 1, 1); else SC_RES(64, 2, 2, 1, 0);
-        } else {
-            if (epi) SC_RES(64, 2, 2, 0, 1); else SC_RES(64, 2, 2, 0, 0);
-        }
-    }
-#undef SC_RES
-    return hipGetLastError();
-}
-
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
                        int epi, GatherTab gt, bool lean) {
     if (total_tiles <= 0) return hipSuccess;
-    if (tag == 2) {
-        if (bt == 128)
-            hipLaunchKernelGGL((gemm_mfma_kernel<128, 2, 4>), dim3(total_tiles), dim3(512), 0, st, tasks, tiles);
-        else
-            hipLaunchKernelGGL((gemm_mfma_kernel<64, 2, 2>), dim3(total_tiles), dim3(256), 0, st, tasks, tiles);
-        return hipGetLastError();
-    }
     if (tag)
         epi ? launch_syrk_t<1, 1>(tasks, tiles, total_tiles, bt, st, gt, lean)
             : launch_syrk_t<1, 0>(tasks, tiles, total_tiles, bt, st, gt, lean);
@@ -2497,23 +2317,6 @@ hipError_t launch_solve_gemv(const SolvePlan& P, const int4* tasks, int count, h
 hipError_t launch_solve_diag(const SolvePlan& P, const int2* tasks, int count, hipStream_t st) {
     if (count <= 0) return hipSuccess;
     hipLaunchKernelGGL(solve_diag_kernel, dim3(count), dim3(256), 0, st, P, tasks);
-    return hipGetLastError();
-}
-
-hipError_t launch_panel_inv(const DevPlan& P, const int2* tasks, int count, hipStream_t st) {
-    if (count <= 0) return hipSuccess;
-    SolvePlan S {};
-    S.sn_start = P.sn_start;
-    S.sn_m = P.sn_m;
-    S.panel_off = P.panel_off;
-    S.panel_pool = P.panel_pool;
-    hipLaunchKernelGGL(solve_inv_kernel, dim3(count), dim3(64), 0, st, S, tasks);
-    return hipGetLastError();
-}
-
-hipError_t launch_panel_tall(const DevPlan& P, const int4* tasks, int count, hipStream_t st) {
-    if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(panel_tall_kernel, dim3(count), dim3(256), 0, st, P, tasks);
     return hipGetLastError();
 }
 

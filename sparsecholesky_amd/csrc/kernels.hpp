@@ -51,13 +51,6 @@ struct DevPlan {
     double* panel_pool;
     double* cb_pool;
     int32_t* info;              // min failing internal column + 1
-    // tall-TRSM-by-inverse mode (panel_tall = 2): per supernode the staging buffer of its
-    // slabs' rows below the diagonal block in tall_pool (doubles, -1 = not in the mode);
-    // the first slab (tall_nbo columns) is assembled straight into it
-    const int64_t* tall_off;
-    double* tall_pool;
-    int32_t tall_nbo;
-    int32_t tall_skip;  // rows right below the first slab that stay in the panel (panel_tall = 3)
 };
 
 // One child's share of one 64 x 64 block (rb, cb) of a parent's contribution block
@@ -94,34 +87,7 @@ struct GemmTask {
     int32_t gs = -1, gv = 0;
     int64_t gb = -1;
     int32_t gw = 0;  // gathering tasks: the front's width (the CB starts at front row gw; K may be one slab)
-    // General products (the TAG 2 launches of the tall-TRSM-by-inverse panel mode,
-    // gemm_tile_body): acc(i, j) = sum_{k < K} A(i, k) B(j, k), A and B column-major
-    // (element (r, k) at base[r + k ld]); out(i, j) = Cin(i, j) + sign acc(i, j) (no Cin:
-    // sign acc), stored at C(i, j) (ld ldc) and / or transposed at Ct(j, i) (ld ldt).
-    // lower: only j <= i (lower-trapezoid tiles), else the full M x N rectangle.  ktri: B
-    // is lower triangular in (j, k) (zero for k > j), so output column block j0 stops at
-    // K = j0 + tile.
-    const double* B = nullptr;
-    int64_t ldb = 0;
-    const double* Cin = nullptr;
-    int64_t ldin = 0;
-    double* Ct = nullptr;
-    int64_t ldt = 0;
-    double sign = -1.0;
-    int32_t lower = 0, ktri = 0;
 };
-// Inverse X = inv(L11) of a slab's factored diagonal block (the tall-TRSM-by-inverse
-// panel mode): 64-block inverses of columns [c0 + 64 q, ...) of front s into the dense
-// scratch X (and its transpose XT), ld ldx, with every other block of their block
-// column zeroed; nbs = the slab width.
-struct XinvTask {
-    double* X;
-    double* XT;
-    int64_t ldx;
-    int32_t s, c0, q, nbs;
-};
-hipError_t launch_xinv64(const DevPlan& P, const XinvTask* tasks, int count, hipStream_t st);
-
 // Strided <-> packed copy of a rows x cols block (pack: a -> b; unpack: b -> a).
 struct Copy2D {
     double* a;  // strided, leading dimension lda
@@ -242,35 +208,40 @@ hipError_t launch_potrf_diag(const DevPlan& P, const int2* tasks, int count, hip
 // [r0, min(r0 + TRSM_ROWS, r1)); ctr - 1 indexes the block's arrival counter (fused POTRF).
 struct TrsmTask {
     int32_t s, k0, r0, r1, ctr;
-    int32_t pre;  // 1: first apply the pending rank-64 update from block k0 - 64 (the recursive
-                  // order's span-64 inner update, folded into this launch; launch with pre = true)
 };
 // partial: blocks with nb < 64; else full blocks with the POTRF fused (arrive: the
 // per-block arrival counters, zeroed)
-// pre: 0 fused POTRF, 1 fused POTRF + the pending span-64 update (trsm_fold),
-// 2 the diagonal blocks already factored by their own launch (trsm_split_wg)
+// pre: 0 fused POTRF, 2 the diagonal blocks already factored by their own launch
+// (trsm_split_wg)
 hipError_t launch_trsm_panel(const DevPlan& P, const TrsmTask* tasks, int count, hipStream_t st, bool partial,
                              int32_t* arrive, int pre = 0);
-// inv(L_jj) of factored 64 x 64 diagonal blocks (s, k0) into their strict upper
-// triangles (the tall TRSM's diagonal solves; the solve's block inverses are the same)
-hipError_t launch_panel_inv(const DevPlan& P, const int2* tasks, int count, hipStream_t st);
-// Tall TRSM of a slab (columns [a, b) of front s, factored diagonal block): tasks
-// (s, a, r0, b), rows [r0, r0 + 64) below the slab solved in place, X = A L_kk^-T.
-hipError_t launch_panel_tall(const DevPlan& P, const int4* tasks, int count, hipStream_t st);
-constexpr int TALL_ROWS = 64;  // rows per tall-TRSM workgroup
+// Persistent slab chain (PSK, kernels.hip psk_kernel): the 64-column POTRF / TRSM /
+// inner-update chain of one 1024-column slab [s0, s1) of every large front of a level,
+// as one launch.  One workgroup per `rows`-row block of the slab's rows [s0, m); the
+// steps are ordered by device-scope flags (flags[flag0]: the front's factored diagonal
+// blocks; flags[flag0 + 1 + rb]: steps whose TRSM row block rb of the diagonal region
+// has finished), re-armed by the last workgroup.  nfull: full 64-column blocks (a
+// partial last block is factored by the per-step launches after it).  inner: the
+// inner update order (sc_options.inner_order).
+struct PskFront {
+    int32_t s, s0, s1, nfull;
+    int32_t m, flag0, inner, pad;
+};
+struct PskWg {
+    int32_t f, rb;
+};
+struct PskArgs {
+    const PskFront* fr;
+    const PskWg* wg;
+    int32_t* flags;   // this launch's flags; flags[nflags] = its done counter
+    int32_t nflags, nwg;
+};
+hipError_t launch_psk(const DevPlan& P, const PskArgs& A, int rows, hipStream_t st);
 
 // gt: the gather tables (CB tasks with gs >= 0 gather their children's entries)
 // lean: 64 x 64 tiles with half the LDS (BK = 8; short-K launches, syrk_lean_kmax)
-// tag 2: general products (GemmTask B / Cin / Ct / sign / lower / ktri)
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
                        int epi = 0, GatherTab gt = {}, bool lean = false);
-// the same SYRK as a resident grid of `grid` workgroups (a multiple of 8) walking the
-// tile list: dispatched at once, so a critical-path launch on another stream finds the
-// slots the grid leaves free instead of queueing behind it
-hipError_t launch_syrk_resident(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag,
-                                hipStream_t st, int epi, GatherTab gt, int grid);
-// full rectangle tiles (general products that are not lower trapezoids)
-void append_tiles_full(std::vector<int2>& out, int task, int M, int N, int bt, int G = 8);
 hipError_t launch_stamp(uint64_t* slot, hipStream_t st);
 
 hipError_t launch_hwid(uint32_t* out, int nwg, int threads, int spin, hipStream_t st);

@@ -192,22 +192,6 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
         R.P.cb_off = dp;
     }
     if (!multi || N.emulated) N.gpanel = pbase;  // gathered layout == the arenas
-    {  // tall-TRSM-by-inverse scratch (panel_tall = 2): levels run one after another, so
-       // every hosted rank's fronts of a level share one pool from offset 0
-        int64_t tneed = 0;
-        for (RankMem& R : N.R) tneed = std::max(tneed, plan_tall_scratch(S, multi ? &N.D : nullptr, R.rank, R.tall_off));
-        if (tneed > 0) {
-            if ((rc = dalloc(N, (size_t)tneed * sizeof(double), p))) return fail(rc);
-            for (RankMem& R : N.R) {
-                int64_t* dp = nullptr;
-                if ((rc = upload(N, R.tall_off, dp))) return fail(rc);
-                R.P.tall_off = dp;
-                R.P.tall_pool = (double*)p;
-                R.P.tall_nbo = std::max(PNB, (S.opt.panel_nb_outer / PNB) * PNB);
-                R.P.tall_skip = S.opt.panel_tall >= 3 ? R.P.tall_nbo : 0;
-            }
-        }
-    }
 
     SchedBuild B;
     if ((rc = build_schedule(N, B))) return fail(rc);
@@ -281,9 +265,10 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     }
     if ((rc = upload(N, B.small, N.d_small)) || (rc = upload(N, B.asmv, N.d_asm)) || (rc = upload(N, B.asml, N.d_asml)) ||
         (rc = upload(N, B.potrf, N.d_potrf)) || (rc = upload(N, B.trsm, N.d_trsm)) ||
-        (rc = upload(N, B.inv, N.d_inv)) || (rc = upload(N, B.tall, N.d_tall)) || (rc = upload(N, B.xinv, N.d_xinv)) ||
         (rc = upload(N, std::vector<int32_t>(B.trsm.size() + 1, 0), N.d_arrive)) ||
-        (rc = upload(N, B.gemm, N.d_gemm)) || (rc = upload(N, B.tiles, N.d_tiles)))
+        (rc = upload(N, B.gemm, N.d_gemm)) || (rc = upload(N, B.tiles, N.d_tiles)) ||
+        (rc = upload(N, B.pskf, N.d_pskf)) || (rc = upload(N, B.pskw, N.d_pskw)) ||
+        (rc = upload(N, std::vector<int32_t>((size_t)B.psk_flags + 1, 0), N.d_pskflags)))
         return fail(rc);
     (void)ns;
     return SC_OK;
@@ -317,23 +302,14 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
                                      L.epi);
         case L_PANEL:
         case L_CB:
-            if (L.res > 0)
-                return launch_syrk_resident(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0,
-                                            st, L.epi, N.gtab, L.res);
             return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st, L.epi,
                                N.gtab, L.lean != 0);
         case L_COMM:
             return comm_launch(N, L);
-        case L_INV:
-            return launch_panel_inv(N.R[L.vr].P, N.d_inv + L.off, L.count, st);
-        case L_TALL:
-            return launch_panel_tall(N.R[L.vr].P, N.d_tall + L.off, L.count, st);
-        case L_XINV:
-            return launch_xinv64(N.R[L.vr].P, N.d_xinv + L.off, L.count, st);
-        case L_GEMM:
-            if (L.res > 0) return launch_syrk_resident(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, 2, st, 0,
-                                                       GatherTab {}, L.res);
-            return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, 2, st);
+        case L_PSK: {
+            PskArgs A {N.d_pskf + L.off, N.d_pskw + L.toff, N.d_pskflags + L.foff, L.fcount, L.count};
+            return launch_psk(N.R[L.vr].P, A, N.S->opt.psk_rows, st);
+        }
     }
     return hipErrorInvalidValue;
 }
@@ -386,6 +362,10 @@ static std::vector<uint64_t> read_stamps(Numeric& N) {
 
 int64_t numeric_factor(Numeric& N, const double* d_Ax, bool sync) {
     HIP_TRY(hipSetDevice(N.device));
+    // tiny path: an earlier factorization still in flight (async, status never read) may
+    // store its status word after the host re-arms it below, and that word would then be
+    // read as this factorization's status -- drain it first
+    if (N.TP.host_info && N.factored && !N.status_valid) HIP_TRY(hipStreamSynchronize(N.stream));
     N.status_valid = false;
     N.last_Ax = d_Ax;
     if (N.profile == 1 && N.ev.size() != 2 * N.sched.size()) {
@@ -473,10 +453,7 @@ int64_t numeric_status(Numeric& N) {
                 case L_ASM: slot = 3; break;
                 case L_POTRF: slot = 4; break;
                 case L_TRSM:
-                case L_INV:
-                case L_XINV:
-                case L_TALL: slot = 5; break;
-                case L_GEMM:
+                case L_PSK: slot = 5; break;
                 case L_PANEL: slot = 6; break;
                 case L_CB: slot = 7; break;
                 case L_COMM: slot = 1; break;

@@ -19,10 +19,7 @@ enum LaunchKind : int32_t {
     L_PANEL = 4,
     L_CB = 5,
     L_COMM = 6,    // one comm step of the hosted ranks (pack, transfer group, unpack)
-    L_INV = 7,     // inverses of a slab's factored 64 x 64 diagonal blocks (tall TRSM)
-    L_TALL = 8,    // tall TRSM of a slab's rows below its diagonal block
-    L_XINV = 9,    // tall-by-inverse mode: 64-block inverses of slab diagonal blocks into X / XT
-    L_GEMM = 10,   // general MFMA products (GemmTask TAG 2: inverse doubling, tall solve, staged updates)
+    L_PSK = 7,     // persistent slab chain: a slab's 64-column POTRF / TRSM / inner updates, all fronts of a level
     L_RECORD = 11, // record sync event `count` on stream `strm`
     L_WAIT = 12,   // stream `strm` waits for sync event `count`
     L_KINDS = 13
@@ -117,7 +114,6 @@ struct RankMem {
     std::vector<int64_t> panel_off;  // per supernode: doubles into the panel arena, -1 = not here
     std::vector<int64_t> cb_off;     // per supernode: full-square CB in the work arena, -1
     std::vector<int64_t> land_off;   // per supernode: R_LAND slab (ld = mb) in the work arena, -1
-    std::vector<int64_t> tall_off;   // per supernode: tall-mode scratch in the handle's tall pool, -1
     int64_t panel_total = 0;     // doubles (incl. the PNB tail the TRSM reads past)
     int64_t work_total = 0;      // doubles: high-water mark of the interval plan
     int64_t work_live_max = 0;   // doubles: max over levels of the live region sizes (lower bound)
@@ -169,7 +165,6 @@ struct Launch {
     int32_t bt;       // SYRK tile edge (64 or 128)
     int32_t epi;      // SYRK epilogue with its C loads batched (short-K and critical-path launches)
     int32_t lean;     // SYRK on 64 x 64 tiles with half the LDS (deepest K <= syrk_lean_kmax)
-    int32_t res;      // > 0: SYRK as a resident grid of this many workgroups (launch_syrk_resident)
     int32_t strm;     // 0 = main stream, 1 = lookahead stream, 2 = comm stream
     int32_t vr;       // hosted rank whose DevPlan the kernel uses
     double flops;     // algorithmic SYRK flops (CB launches: mb*(mb+1)*w)
@@ -179,6 +174,10 @@ struct Launch {
     int64_t poff, uoff;
     int32_t pcount, ucount;
     int32_t step;
+    // L_PSK: fronts [off, off + ntasks) of Numeric::d_pskf, workgroups [toff, toff + count) of
+    // d_pskw, flags [foff, foff + fcount] of d_pskflags (the last one: the done counter)
+    int64_t foff;
+    int32_t fcount;
 };
 
 struct Numeric {
@@ -202,10 +201,10 @@ struct Numeric {
     int2* d_asml = nullptr;  // per assembly task: owned front columns (distributed-assembly launches)
     int2* d_potrf = nullptr;
     TrsmTask* d_trsm = nullptr;
-    int2* d_inv = nullptr;   // L_INV tasks (s, k0)
-    int4* d_tall = nullptr;  // L_TALL tasks (s, a, r0, b)
-    XinvTask* d_xinv = nullptr;  // L_XINV tasks
     int32_t* d_arrive = nullptr;  // fused POTRF + TRSM: per-block arrival counters
+    PskFront* d_pskf = nullptr;   // persistent slab chains (L_PSK)
+    PskWg* d_pskw = nullptr;
+    int32_t* d_pskflags = nullptr;
     GemmTask* d_gemm = nullptr;
     int2* d_tiles = nullptr;
     GatherTab gtab;              // the CB SYRK extend-add gather's segment tables (schedule.cpp)

@@ -27,47 +27,6 @@ static int wbucket_of(int w) {
     return 128;
 }
 
-static int nbo_of(const Symbolic& S) { return std::max(PNB, (S.opt.panel_nb_outer / PNB) * PNB); }
-static int64_t al64(int64_t x) { return (x + 63) / 64 * 64; }
-
-TallLayout tall_layout(const Symbolic& S, int32_t s, int nbo) {
-    TallLayout T;
-    const int w = S.w(s), m = S.sn_m[s];
-    T.nbs0 = std::min(w, nbo);
-    T.skip = S.opt.panel_tall >= 3 ? nbo : 0;  // near rows solved in place on the main stream
-    T.lds = std::max<int64_t>(1, m - T.nbs0 - T.skip);
-    const int64_t nn = (int64_t)T.nbs0 * T.nbs0;
-    T.x = al64(T.lds * T.nbs0);
-    T.xt = T.x + al64(nn);
-    T.u = T.xt + al64(nn);
-    T.total = T.u + al64(nn);
-    return T;
-}
-
-bool tallx_front(const Symbolic& S, const DistPlan* D, int rank, int32_t s) {
-    if ((S.opt.panel_tall < 2 || S.opt.panel_tall > 4) || S.fclass[s] != FRONT_LARGE) return false;
-    if (D && (D->owner[s] != rank || D->pd[s] >= 0)) return false;
-    // panel_tall = 3 solves the far rows on the lookahead stream: a split front sends its
-    // final slabs from the main stream's point of view (STEP_SLAB): it keeps the default path
-    if (D && S.opt.panel_tall >= 3 && D->split[s] >= 0) return false;
-    const int w = S.w(s), m = S.sn_m[s];
-    return w >= 2 * PNB && m > std::min(w, nbo_of(S));
-}
-
-int64_t plan_tall_scratch(const Symbolic& S, const DistPlan* D, int rank, std::vector<int64_t>& off) {
-    off.assign((size_t)S.ns, -1);
-    std::vector<int64_t> used((size_t)std::max(S.nlevels, 1), 0);
-    const int nbo = nbo_of(S);
-    int64_t peak = 0;
-    for (int32_t s = 0; s < S.ns; ++s) {
-        if (!tallx_front(S, D, rank, s)) continue;
-        int64_t& u = used[S.level[s]];
-        off[s] = u;
-        u += tall_layout(S, s, nbo).total;
-        peak = std::max(peak, u);
-    }
-    return peak;
-}
 
 // Build the static launch schedule (host).  Task pointers into the pools are
 // final device addresses, so the schedule can be replayed or graph-captured.
@@ -78,14 +37,6 @@ void append_tiles(std::vector<int2>& out, int task, int M, int N, int bt, int G)
             for (int tj = sj; tj < std::min(TN, sj + G); ++tj)
                 for (int ti = std::max(si, tj); ti < std::min(TM, si + G); ++ti)
                     out.push_back(make_int2(task, (ti << 16) | tj));
-}
-
-void append_tiles_full(std::vector<int2>& out, int task, int M, int N, int bt, int G) {
-    const int TM = (M + bt - 1) / bt, TN = (N + bt - 1) / bt;
-    for (int sj = 0; sj < TN; sj += G)
-        for (int si = 0; si < TM; si += G)
-            for (int tj = sj; tj < std::min(TN, sj + G); ++tj)
-                for (int ti = si; ti < std::min(TM, si + G); ++ti) out.push_back(make_int2(task, (ti << 16) | tj));
 }
 
 void xcd_order(int2* tiles, int64_t n) {
@@ -195,10 +146,6 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
     // and written
     auto task_bytes = [&](const GemmTask& t) {
         const double pairs = (double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0;
-        if (t.B) {  // general product: both operands once, the output (and Cin) once
-            const double outs = t.lower ? pairs : (double)t.M * t.N;
-            return 8.0 * (t.M + (double)t.N) * t.K + 8.0 * outs * ((t.C ? 1 : 0) + (t.Ct ? 1 : 0) + (t.Cin ? 1 : 0));
-        }
         double b = 8.0 * t.M * (double)t.K;
         if (t.gs < 0) return b + 16.0 * pairs;
         b += 8.0 * pairs;
@@ -225,34 +172,18 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         }
         const bool wide = minN >= 256;
         L.bt = (S.opt.syrk_tile == 128 || (S.opt.syrk_tile == 0 && wide)) ? SYRK_BT_LARGE : SYRK_BT_SMALL;
-        if (kind == L_CB && S.opt.syrk_tile == 0 && maxK < S.opt.cb_small_kmax) L.bt = SYRK_BT_SMALL;
         // batched C epilogue on the critical path (main-stream panel updates) and where
         // K is short enough that the epilogue dominates a tile (CB of levels 4-7 at
         // 128^3); deep-K CB updates and the lookahead stream keep the trickle epilogue
-        L.epi = (kind == L_PANEL && (strm == 0 || SC_LA_EPI)) || (kind == L_CB && maxK < SC_EPI_KMAX);
+        L.epi = (kind == L_PANEL && strm == 0) || (kind == L_CB && maxK < SC_EPI_KMAX);
         // (CB launches with K <= 64 -- levels 4-6 at 128^3 -- are gather-bound and lose
         // more to the lean instance's smaller gather batches than they gain in occupancy)
         L.lean = L.bt == SYRK_BT_SMALL && S.opt.syrk_lean_kmax > 0 && maxK <= S.opt.syrk_lean_kmax &&
-                 (kind == L_PANEL || maxK >= S.opt.cb_lean_kmin);
-        // lookahead-stream updates as a resident grid (la_grid): all its workgroups are
-        // dispatched at once, so the chain's launches on the main stream are not queued
-        // behind the rest of the grid
-        L.res = ((kind == L_PANEL || kind == L_GEMM || kind == L_CB) && strm == 1 && S.opt.la_grid > 0) ? S.opt.la_grid : 0;
-        if (L.res) L.lean = 0;
-        if (kind == L_GEMM) {  // general products: tile by the smaller output edge
-            int minMN = INT32_MAX;
-            for (auto& t : tasks) minMN = std::min(minMN, std::min((int)t.M, (int)t.N));
-            L.bt = minMN >= 256 ? SYRK_BT_LARGE : SYRK_BT_SMALL;
-            L.epi = 0;
-            L.lean = 0;
-        }
+                 (kind == L_PANEL || maxK > 64);
         L.toff = (int64_t)tiles.size();
         L.bytes = 0.0;
         for (size_t q = 0; q < tasks.size(); ++q) {
-            if (kind == L_GEMM && !tasks[q].lower)
-                append_tiles_full(tiles, (int)q, tasks[q].M, tasks[q].N, L.bt);
-            else
-                append_tiles(tiles, (int)q, tasks[q].M, tasks[q].N, L.bt);
+            append_tiles(tiles, (int)q, tasks[q].M, tasks[q].N, L.bt);
             gemm.push_back(tasks[q]);
             L.bytes += task_bytes(tasks[q]);
         }
@@ -304,24 +235,6 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             L.flops -= tfl;
             N.sched.push_back(L);
             N.sched.push_back(T);
-            return;
-        }
-        // la_split: a big lookahead-stream update as P back-to-back launches over consecutive
-        // parts of its tile list (each a multiple of 8 tiles: the XCD mapping holds), so a
-        // chain launch on the main stream waits for one part's dispatch, not the whole grid's
-        const int P = (strm == 1 && kind == L_PANEL && !L.res) ? std::max(1, S.opt.la_split) : 1;
-        if (P > 1 && L.count >= 64 * P) {
-            const int per = (L.count / P + 7) / 8 * 8;
-            const double fl_all = L.flops, by_all = L.bytes;
-            const int n_all = L.count;
-            for (int t0 = 0; t0 < n_all; t0 += per) {
-                Launch Q = L;
-                Q.toff = L.toff + t0;
-                Q.count = std::min(per, n_all - t0);
-                Q.flops = fl_all * Q.count / n_all;
-                Q.bytes = by_all * Q.count / n_all;
-                N.sched.push_back(Q);
-            }
             return;
         }
         N.sched.push_back(L);
@@ -557,140 +470,6 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             push_gemm_launch(L_CB, lev, cbt, w >= 256 ? 1 : 0, fl);
         }
     };
-    // general product task (L_GEMM): out(i, j) = Cin(i, j) - sum_k A(i, k) B(j, k), i < M,
-    // j < N (lower: j <= i only), stored at C
-    auto gen_update = [&](std::vector<GemmTask>& vec, double& fl, double* C, int64_t ldc, const double* Cin,
-                          int64_t ldin, const double* A, int64_t lda, const double* Bm, int64_t ldb, int M, int Nn,
-                          int K, bool lower) {
-        if (M <= 0 || Nn <= 0 || K <= 0) return;
-        GemmTask t {};
-        t.C = C;
-        t.ldc = ldc;
-        t.Cin = Cin;
-        t.ldin = ldin;
-        t.A = A;
-        t.lda = lda;
-        t.B = Bm;
-        t.ldb = ldb;
-        t.M = M;
-        t.N = Nn;
-        t.K = K;
-        t.lower = lower ? 1 : 0;
-        t.sign = -1.0;
-        vec.push_back(t);
-        fl += 2.0 * K * (lower ? ((double)Nn * M - (double)Nn * (Nn - 1) / 2.0) : (double)Nn * M);
-    };
-    // Slab end of tall-by-inverse fronts tx = (s, slab0) on hosted rank v, after the
-    // chain has factored the slabs' diagonal blocks (the reference's cblas_dtrsm,
-    // chol.hpp:1292, for the rows below them, as products):
-    //   1. xinv64: the 64-block inverses of each diagonal block into X / XT
-    //   2. per doubling width b = 64, 128, ...: X = [Xa 0; E Xb] for every pair of
-    //      b-blocks, E = -Xb (B Xa), B = L(c-block rows, a-block columns), as two general
-    //      products (U^T = (B Xa)^T, then E and E^T)
-    //   3. the tall solve L21 = A21 X^T (K trimmed to the triangle), A21 from the staging
-    //      buffer, L21 written into the panel
-    //   (panel_tall = 3: on stream strm, and the tall solve covers only the rows from
-    //   slab end + skip on -- the near rows were solved in place on the main stream)
-    auto emit_tallx = [&](int32_t lev, int v, const std::vector<int2>& tx, int strm) {
-        const RankMem& R = N.R[v];
-        struct F {
-            int32_t s, c0, nbs, m, skip;
-            double *pan, *base, *X, *XT, *U;
-            int64_t ldx, lds;
-        };
-        std::vector<F> fr;
-        int maxnb = 0;
-        for (const int2& e : tx) {
-            F f {};
-            f.s = e.x;
-            f.c0 = e.y;
-            f.nbs = std::min(S.w(f.s), f.c0 + NBO) - f.c0;
-            f.m = S.sn_m[f.s];
-            const TallLayout TL = tall_layout(S, f.s, NBO);
-            f.pan = R.P.panel_pool + R.panel_off[f.s];
-            f.base = R.P.tall_pool + R.tall_off[f.s];
-            f.X = f.base + TL.x;
-            f.XT = f.base + TL.xt;
-            f.U = f.base + TL.u;
-            f.ldx = TL.nbs0;
-            f.lds = TL.lds;
-            f.skip = TL.skip;
-            fr.push_back(f);
-            maxnb = std::max(maxnb, f.nbs);
-        }
-        Launch Lx {};
-        Lx.kind = L_XINV;
-        Lx.level = lev;
-        Lx.vr = v;
-        Lx.strm = strm;
-        Lx.off = (int64_t)B.xinv.size();
-        for (const F& f : fr)
-            for (int q = 0; q * PNB < f.nbs; ++q)
-                B.xinv.push_back(XinvTask {f.X, f.XT, f.ldx, f.s, f.c0, q, f.nbs});
-        Lx.count = (int32_t)((int64_t)B.xinv.size() - Lx.off);
-        N.sched.push_back(Lx);
-        for (int b = PNB; b < maxnb; b *= 2) {
-            std::vector<GemmTask> ut, et;
-            double fu = 0.0, fe = 0.0;
-            for (const F& f : fr)
-                for (int pb = 0, pi = 0; pb + b < f.nbs; pb += 2 * b, ++pi) {
-                    const int valid = std::min(b, f.nbs - pb - b);
-                    double* Ui = f.U + (int64_t)pi * b * b;
-                    GemmTask u {};
-                    u.A = f.pan + (int64_t)(f.c0 + pb) * f.m + (f.c0 + pb + b);  // B = L(c rows, a columns)
-                    u.lda = f.m;
-                    u.B = f.XT + pb + (int64_t)pb * f.ldx;  // Xa(k, j) = XT(pb + j, pb + k)
-                    u.ldb = f.ldx;
-                    u.M = valid;
-                    u.N = b;
-                    u.K = b;
-                    u.C = nullptr;
-                    u.Ct = Ui;  // U(i, j) at Ui[j + i b]
-                    u.ldt = b;
-                    u.sign = 1.0;
-                    ut.push_back(u);
-                    fu += 2.0 * valid * (double)b * b;
-                    GemmTask q {};
-                    q.A = f.X + (pb + b) + (int64_t)(pb + b) * f.ldx;  // Xb
-                    q.lda = f.ldx;
-                    q.B = Ui;  // U(k, j) = Ui[j + k b]
-                    q.ldb = b;
-                    q.M = valid;
-                    q.N = b;
-                    q.K = valid;
-                    q.C = f.X + (pb + b) + (int64_t)pb * f.ldx;     // E into X
-                    q.ldc = f.ldx;
-                    q.Ct = f.XT + pb + (int64_t)(pb + b) * f.ldx;   // and E^T into XT
-                    q.ldt = f.ldx;
-                    q.sign = -1.0;
-                    et.push_back(q);
-                    fe += 2.0 * valid * (double)b * valid;
-                }
-            push_gemm_launch(L_GEMM, lev, ut, 0, fu, strm);
-            push_gemm_launch(L_GEMM, lev, et, 0, fe, strm);
-        }
-        std::vector<GemmTask> tt;
-        double ft = 0.0;
-        for (const F& f : fr) {
-            const int r0 = f.c0 + f.nbs + f.skip;  // first row of the tall solve
-            if (f.m <= r0) continue;
-            GemmTask t {};
-            t.A = f.base;  // S: rows [r0, m) of the slab's columns
-            t.lda = f.lds;
-            t.B = f.X;
-            t.ldb = f.ldx;
-            t.M = f.m - r0;
-            t.N = f.nbs;
-            t.K = f.nbs;
-            t.C = f.pan + (int64_t)f.c0 * f.m + r0;
-            t.ldc = f.m;
-            t.sign = 1.0;
-            t.ktri = 1;
-            tt.push_back(t);
-            ft += (double)(f.m - r0) * f.nbs * (double)f.nbs;
-        }
-        push_gemm_launch(L_GEMM, lev, tt, 0, ft, strm);
-    };
     // one level's fronts of hosted rank v
     auto emit_level = [&](int32_t lev, const std::vector<int32_t>& nodes, int v) {
         double* panel_pool = N.R[v].P.panel_pool;
@@ -730,16 +509,12 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // fronts whose CB SYRK gathers the children's CB entries itself (one CB launch
         // task covering the whole CB): their assembly stops at the panel columns
         auto gather = [&](int32_t s) {
-            return S.opt.cb_gather && S.mb(s) > 0 && S.w(s) >= S.opt.cb_gather_min_w && !is_split(s) &&
-                   !is_early_sender(s, v);
+            return S.opt.cb_gather && S.mb(s) > 0 && !is_split(s) && !is_early_sender(s, v);
         };
         // assembly: fronts with m >= ASM_TILE_MIN_M one workgroup per (front, 16
         // columns, 256-row tile), write-once (big = 1); smaller fronts one workgroup per
         // (front, 16 columns) streaming child columns (measured faster below ~8k rows)
         const int tile_min_m = S.opt.asm_tile_min_m > 0 ? S.opt.asm_tile_min_m : ASM_TILE_MIN_M;
-        // tall-by-inverse fronts (tall_layout): the tile assembly stages their first slab's
-        // rows below its diagonal block in the scratch the slab's tall solve reads
-        auto tallx = [&](int32_t s) { return N.R[v].tall_off.size() > (size_t)s && N.R[v].tall_off[s] >= 0; };
         for (int tiled = 1; tiled >= 0; --tiled) {
             Launch L {};
             L.kind = L_ASM;
@@ -749,7 +524,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             L.off = (int64_t)asmv.size();
             for (int32_t s : large) {
                 const int m = S.sn_m[s];
-                if ((m >= tile_min_m || tallx(s)) != (tiled == 1) || is_dasm(s)) continue;
+                if ((m >= tile_min_m) != (tiled == 1) || is_dasm(s)) continue;
                 const int ncol = gather(s) ? S.w(s) : m;  // assembled columns
                 for (int cb = 0; cb * ASM_COLS < ncol; ++cb) {
                     if (!tiled) {
@@ -791,27 +566,116 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             vec.push_back(t);
             fl += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
         };
-        // tall modes (a front of more than one 64-column block): the 64-column chain
-        // (POTRF / TRSM / inner updates) runs on the slab's diagonal-block rows only; at
-        // the slab end every row below the slab is solved -- panel_tall = 1: block
-        // inverses and one row-blocked tall-TRSM launch (panel_tall_kernel); panel_tall =
-        // 2 (tallx fronts): X = inv(L11) and one MFMA product L21 = A21 X^T -- then the
-        // outer updates as before
-        auto tall = [&](int32_t s) { return (S.opt.panel_tall == 1 && S.w(s) > PNB) || tallx(s); };
-        // fronts whose next TRSM launch folds in the pending span-64 inner update (recursive
-        // order, an even block of the slab followed by a full block): the update launch of
-        // that step is dropped, one dispatch fewer on the chain per two steps
-        std::vector<char> pre_next((size_t)S.ns, 0);
-        auto fold = [&](int32_t s) { return S.opt.trsm_fold && S.opt.inner_order == 1 && !tall(s); };
-        const bool tall3 = S.opt.panel_tall >= 3;
-        int a3_ev = -1, b3_ev = -1;  // lookahead-stream events of the last slab end (panel_tall = 3)
-        int cb_pending = -1;         // cb_slab: the lookahead stream's last CB pass
-        // cb_slab: fronts whose CB is updated slab by slab on the lookahead stream (the
-        // first pass gathers the children's entries, later passes read C)
-        auto cb_slab = [&](int32_t s) {
-            return S.opt.cb_slab && S.mb(s) > 0 && !is_split(s) && !is_early_sender(s, v) && !tall(s);
+        // persistent slab chains (panel_psk): per slab one L_PSK launch for the level's
+        // fronts (the 64-column steps inside it), then the partial last blocks, then the
+        // slab-end outer updates exactly as the per-step schedule below emits them
+        const bool psk = S.opt.panel_psk && maxw >= S.opt.psk_min_w;
+        auto outer_updates = [&](int s0) {
+            std::vector<GemmTask> outer_a, outer_b;
+            double afl = 0.0, bfl = 0.0;
+            for (int32_t s : large) {
+                const int w = S.w(s), m = S.sn_m[s];
+                const int slab1 = std::min(w, s0 + NBO);
+                if (w <= s0 || slab1 >= w) continue;
+                double* pan = panel_pool + poff[s];
+                const int nxt = S.opt.lookahead ? std::min(w, slab1 + NBO) : w;
+                add_update(outer_a, afl, pan, m, m, slab1, nxt, s0, slab1);
+                add_update(outer_b, bfl, pan, m, m, nxt, w, s0, slab1);
+            }
+            int e_trsm = -1;
+            if (!outer_b.empty()) e_trsm = push_record(0);
+            if (!outer_a.empty()) {
+                if (b_pending >= 0) {
+                    push_wait(0, b_pending);
+                    b_pending = -1;
+                }
+                push_gemm_launch(L_PANEL, lev, outer_a, 0, afl);
+            }
+            if (!outer_b.empty()) {
+                push_wait(1, e_trsm);
+                push_gemm_launch(L_PANEL, lev, outer_b, 0, bfl, 1);
+                b_pending = push_record(1);
+            }
         };
-        for (int k0 = 0; k0 < maxw; k0 += PNB) {
+        for (int s0 = 0; psk && s0 < maxw; s0 += NBO) {
+            const int TR = S.opt.psk_rows;
+            Launch Lk {};
+            Lk.kind = L_PSK;
+            Lk.level = lev;
+            Lk.vr = v;
+            Lk.off = (int64_t)B.pskf.size();
+            Lk.toff = (int64_t)B.pskw.size();
+            Lk.foff = B.psk_flags;
+            std::vector<int> nrb;
+            double fl = 0.0;
+            for (int32_t s : large) {
+                const int w = S.w(s), m = S.sn_m[s];
+                if (w <= s0) continue;
+                const int slab1 = std::min(w, s0 + NBO), nfull = (slab1 - s0) / PNB;
+                if (nfull == 0) continue;
+                PskFront f {};
+                f.s = s;
+                f.s0 = s0;
+                f.s1 = slab1;
+                f.nfull = nfull;
+                f.m = m;
+                f.flag0 = (int32_t)(B.psk_flags - Lk.foff);
+                f.inner = S.opt.inner_order;
+                B.psk_flags += 1 + (slab1 - s0 + TR - 1) / TR;
+                B.pskf.push_back(f);
+                nrb.push_back((m - s0 + TR - 1) / TR);
+                for (int j = 0; j < nfull; ++j) {  // the inner updates' flops (as add_update counts them)
+                    const int k1 = s0 + PNB * (j + 1);
+                    if (k1 >= slab1) break;
+                    const int span = S.opt.inner_order ? PNB << __builtin_ctz((unsigned)(j + 1)) : slab1 - k1;
+                    const int K = S.opt.inner_order ? span : PNB;
+                    const double Nn = std::min(slab1, k1 + span) - k1, M = m - k1;
+                    fl += 2.0 * K * (Nn * M - Nn * (Nn - 1) / 2.0);
+                }
+            }
+            const int maxrb = nrb.empty() ? 0 : *std::max_element(nrb.begin(), nrb.end());
+            for (int rb = 0; rb < maxrb; ++rb)  // row-block-major: every wait is on an earlier workgroup
+                for (int fi = 0; fi < (int)nrb.size(); ++fi)
+                    if (rb < nrb[fi]) B.pskw.push_back(PskWg {fi, rb});
+            Lk.ntasks = (int32_t)nrb.size();
+            Lk.count = (int32_t)((int64_t)B.pskw.size() - Lk.toff);
+            Lk.fcount = (int32_t)(B.psk_flags - Lk.foff);
+            Lk.flops = fl;
+            B.psk_flags += 1;  // the launch's done counter
+            if (Lk.count > 0) N.sched.push_back(Lk);
+            // partial last blocks (w not a multiple of 64): their POTRF and the TRSM below
+            Launch Lp {};
+            Lp.kind = L_POTRF;
+            Lp.level = lev;
+            Lp.vr = v;
+            Lp.off = (int64_t)potrf.size();
+            Launch Lq {};
+            Lq.kind = L_TRSM;
+            Lq.level = lev;
+            Lq.vr = v;
+            Lq.big = 1;
+            for (int32_t s : large) {
+                const int w = S.w(s), kp = w - w % PNB;
+                if (w % PNB == 0 || kp < s0 || kp >= s0 + NBO) continue;
+                potrf.push_back(make_int2(s, kp));
+            }
+            Lq.off = (int64_t)trsm.size();
+            for (int32_t s : large) {
+                const int w = S.w(s), m = S.sn_m[s];
+                const int kp = w - w % PNB;
+                if (w % PNB == 0 || kp < s0 || kp >= s0 + NBO) continue;
+                for (int r0 = w; r0 < m; r0 += TRSM_ROWS) trsm.push_back(TrsmTask {s, kp, r0, m, 0});
+            }
+            Lp.count = (int32_t)((int64_t)potrf.size() - Lp.off);
+            Lq.count = (int32_t)((int64_t)trsm.size() - Lq.off);
+            if (Lp.count > 0) N.sched.push_back(Lp);
+            if (Lq.count > 0) N.sched.push_back(Lq);
+            // split fronts: the slab is final
+            for (int32_t s : large)
+                if (is_split(s) && S.w(s) > s0) emit_slab(s, s0 / D.nbo);
+            outer_updates(s0);
+        }
+        for (int k0 = 0; !psk && k0 < maxw; k0 += PNB) {
             Launch Lp {};
             Lp.kind = L_POTRF;
             Lp.level = lev;
@@ -823,28 +687,18 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             Lt.vr = v;
             Lt.off = (int64_t)trsm.size();
             std::vector<GemmTask> upd, outer_a, outer_b;
-            std::vector<TrsmTask> trsm_part;  // partial last blocks: own launch (big = 1)
-            std::vector<TrsmTask> trsm_pre;   // full blocks folding the pending update in (own launch)
-            std::vector<TrsmTask> trsm_split; // full blocks factored by the POTRF launch (own launch)
+            std::vector<TrsmTask> trsm_part;   // partial last blocks: own launch (big = 1)
+            std::vector<TrsmTask> trsm_split;  // full blocks factored by the POTRF launch (own launch)
             // a step whose fused launch would exceed trsm_split_wg workgroups (more than the GPU
             // holds at once) factors each diagonal block once, in the POTRF launch, instead of
             // in every workgroup of every round
             int64_t step_wg = 0;
             for (int32_t s : large) {
-                const int w = S.w(s);
-                if (w < k0 + PNB) continue;
-                const int slab1 = std::min(w, (k0 / NBO) * NBO + NBO);
-                const int rend = tall(s) ? slab1 : S.sn_m[s];
-                step_wg += (std::max(rend, k0 + PNB + 1) - (k0 + PNB) + TRSM_ROWS - 1) / TRSM_ROWS;
+                if (S.w(s) < k0 + PNB) continue;
+                step_wg += (std::max(S.sn_m[s], k0 + PNB + 1) - (k0 + PNB) + TRSM_ROWS - 1) / TRSM_ROWS;
             }
             const bool split_step = S.opt.trsm_split_wg > 0 && step_wg > S.opt.trsm_split_wg;
-            std::vector<int2> inv_t;           // tall mode, slab end: diagonal-block inverses
-            std::vector<int4> tall_t;          // ... and the tall TRSM of the rows below
-            std::vector<int2> tx;              // tall-by-inverse fronts at a slab end: (s, slab0)
-            std::vector<GemmTask> outer_a2;    // ... their next-slab updates (general products)
-            std::vector<GemmTask> d3, a3, b3;  // panel_tall = 3: next diagonal block, next slab, the rest
-            std::vector<GemmTask> cbs;         // cb_slab: this slab's CB passes
-            double uflops = 0.0, afl = 0.0, bfl = 0.0, d3fl = 0.0, a3fl = 0.0, b3fl = 0.0, cbfl = 0.0;
+            double uflops = 0.0, afl = 0.0, bfl = 0.0;
             for (int32_t s : large) {
                 const int w = S.w(s), m = S.sn_m[s];
                 if (w <= k0) continue;
@@ -852,20 +706,16 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 const int k1 = k0 + nb;
                 const int slab0 = (k0 / NBO) * NBO;
                 const int slab1 = std::min(w, slab0 + NBO);
-                const int rend = tall(s) ? slab1 : m;  // rows of this step's TRSM and inner update
                 if (nb < PNB) {
                     potrf.push_back(make_int2(s, k0));
-                    for (int r0 = k1; r0 < rend; r0 += TRSM_ROWS) trsm_part.push_back(TrsmTask {s, k0, r0, rend, 0});
-                } else if (split_step && !pre_next[s]) {
+                    for (int r0 = k1; r0 < m; r0 += TRSM_ROWS) trsm_part.push_back(TrsmTask {s, k0, r0, m, 0});
+                } else if (split_step) {
                     potrf.push_back(make_int2(s, k0));
-                    for (int r0 = k1; r0 < rend; r0 += TRSM_ROWS) trsm_split.push_back(TrsmTask {s, k0, r0, rend, 0, 0});
+                    for (int r0 = k1; r0 < m; r0 += TRSM_ROWS) trsm_split.push_back(TrsmTask {s, k0, r0, m, 0});
                 } else {  // fused POTRF (one task if no rows below); ctr - 1: arrival counter
-                    const int ctr = (int)(trsm.size() + trsm_pre.size()) + 1;
-                    const int pre = pre_next[s];
-                    for (int r0 = k1; r0 < std::max(rend, k1 + 1); r0 += TRSM_ROWS)
-                        (pre ? trsm_pre : trsm).push_back(TrsmTask {s, k0, r0, rend, ctr, pre});
+                    const int ctr = (int)trsm.size() + 1;
+                    for (int r0 = k1; r0 < std::max(m, k1 + 1); r0 += TRSM_ROWS) trsm.push_back(TrsmTask {s, k0, r0, m, ctr});
                 }
-                pre_next[s] = 0;
                 double* pan = panel_pool + poff[s];
                 if (k1 < slab1 && S.opt.inner_order == 1) {
                     // recursive order: block b of the slab closes a run of 2^t blocks
@@ -874,107 +724,15 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     // right-looking, 768 instead of 1792 C columns rewritten per slab.
                     const int b = (k0 - slab0) / PNB;
                     const int span = PNB << __builtin_ctz((unsigned)(b + 1));
-                    if (span == PNB && nb == PNB && std::min(PNB, w - k1) == PNB && fold(s))
-                        pre_next[s] = 1;  // folded into the next TRSM launch
-                    else
-                        add_update(upd, uflops, pan, m, rend, k1, std::min(slab1, k1 + span), k1 - span, k1);
+                    add_update(upd, uflops, pan, m, m, k1, std::min(slab1, k1 + span), k1 - span, k1);
                 } else if (k1 < slab1) {
-                    add_update(upd, uflops, pan, m, rend, k1, slab1, k0, k1);
-                }
-                if (k1 == slab1 && tall(s) && !tallx(s)) {
-                    for (int kb = slab0; kb < slab1; kb += PNB) inv_t.push_back(make_int2(s, kb));
-                    for (int r0 = slab1; r0 < m; r0 += TALL_ROWS) tall_t.push_back(make_int4(s, slab0, r0, slab1));
-                }
-                if (k1 == slab1 && tallx(s) && tall3) {
-                    // panel_tall = 3 (see below): the near rows [slab1, slab1 + NBO) on the main
-                    // stream by the row-blocked tall TRSM; X, the far rows and the updates on
-                    // the lookahead stream
-                    const int ne = std::min(m, slab1 + NBO);
-                    for (int kb = slab0; kb < slab1 && ne > slab1; kb += PNB) inv_t.push_back(make_int2(s, kb));
-                    for (int r0 = slab1; r0 < ne; r0 += TALL_ROWS) tall_t.push_back(make_int4(s, slab0, r0, slab1));
-                    tx.push_back(make_int2(s, slab0));
-                    if (slab1 < w) {
-                        const int n1 = std::min(w, slab1 + NBO), nf = std::min(m, n1 + NBO);
-                        const int K = slab1 - slab0;
-                        // the next slab's diagonal block (main stream, critical path)
-                        add_update(d3, d3fl, pan, m, n1, slab1, n1, slab0, slab1);
-                        // the next slab's near rows in place, its far rows to the staging buffer
-                        gen_update(a3, a3fl, pan + (int64_t)slab1 * m + n1, m, pan + (int64_t)slab1 * m + n1, m,
-                                   pan + (int64_t)slab0 * m + n1, m, pan + (int64_t)slab0 * m + slab1, m, nf - n1,
-                                   n1 - slab1, K, false);
-                        if (m > nf) {
-                            const TallLayout TL = tall_layout(S, s, NBO);
-                            gen_update(a3, a3fl, N.R[v].P.tall_pool + N.R[v].tall_off[s], TL.lds,
-                                       pan + (int64_t)slab1 * m + nf, m, pan + (int64_t)slab0 * m + nf, m,
-                                       pan + (int64_t)slab0 * m + slab1, m, m - nf, n1 - slab1, K, false);
-                        }
-                        // every later column, in place (panel_tall = 4, left-looking: only the
-                        // slab after next, from every slab so far -- one deep-K product per
-                        // slab instead of a rank-NBO pass over every later column)
-                        if (S.opt.panel_tall == 4)
-                            add_update(b3, b3fl, pan, m, m, n1, std::min(w, n1 + NBO), 0, slab1);
-                        else
-                            add_update(b3, b3fl, pan, m, m, n1, w, slab0, slab1);
-                    }
-                    continue;
-                }
-                if (k1 == slab1 && tallx(s)) tx.push_back(make_int2(s, slab0));
-                if (k1 == slab1 && cb_slab(s)) {  // CB -= L21_k L21_k^T (K = the slab)
-                    const int mb = m - w;
-                    GemmTask t {};
-                    t.C = cb_pool + coff[s];
-                    t.A = pan + (int64_t)slab0 * m + w;
-                    t.ldc = mb;
-                    t.lda = m;
-                    t.M = mb;
-                    t.N = mb;
-                    t.K = slab1 - slab0;
-                    if (slab0 == 0 && gather(s)) {
-                        t.gs = s;
-                        t.gv = v;
-                        t.gb = gather_segments(s, v);
-                        t.gw = w;
-                    }
-                    cbs.push_back(t);
-                    cbfl += (double)mb * (mb + 1.0) * t.K;
+                    add_update(upd, uflops, pan, m, m, k1, slab1, k0, k1);
                 }
                 if (k1 == slab1 && slab1 < w) {
                     // outer_a is the last update of block slab1: a pending stream-1 outer
                     // update of those columns is waited for before outer_a runs
                     const int nxt = S.opt.lookahead ? std::min(w, slab1 + NBO) : w;
-                    if (tallx(s)) {
-                        // the next slab's columns: its diagonal block in place, its rows below
-                        // (final after this update) to the staging buffer its tall solve reads
-                        const int n1 = std::min(w, slab1 + NBO);
-                        const TallLayout TL = tall_layout(S, s, NBO);
-                        double* Sb = N.R[v].P.tall_pool + N.R[v].tall_off[s];
-                        const int K = slab1 - slab0;
-                        gen_update(outer_a2, afl, pan + (int64_t)slab1 * m + slab1, m, pan + (int64_t)slab1 * m + slab1,
-                                   m, pan + (int64_t)slab0 * m + slab1, m, pan + (int64_t)slab0 * m + slab1, m,
-                                   n1 - slab1, n1 - slab1, K, true);
-                        gen_update(outer_a2, afl, Sb, TL.lds, pan + (int64_t)slab1 * m + n1, m,
-                                   pan + (int64_t)slab0 * m + n1, m, pan + (int64_t)slab0 * m + slab1, m, m - n1,
-                                   n1 - slab1, K, false);
-                        if (nxt > n1)  // no lookahead: the rest of the trailing columns, in place
-                            gen_update(outer_a2, afl, pan + (int64_t)n1 * m + n1, m, pan + (int64_t)n1 * m + n1, m,
-                                       pan + (int64_t)slab0 * m + n1, m, pan + (int64_t)slab0 * m + n1, m, m - n1,
-                                       nxt - n1, K, true);
-                    } else if (S.opt.lookahead == 2) {
-                        // left-looking: only the next slab, by every slab so far (one deep-K
-                        // product on the main stream; the chain then has the GPU to itself)
-                        add_update(outer_a, afl, pan, m, m, slab1, std::min(w, slab1 + NBO), 0, slab1);
-                        continue;
-                    } else if (S.opt.lookahead == 3) {
-                        // the next slab by this slab (main stream), and only the slab after next
-                        // by every slab so far (lookahead stream: one deep-K product whose grid
-                        // fits the GPU at once, so the chain's launches do not queue behind it)
-                        const int n1 = std::min(w, slab1 + NBO);
-                        add_update(outer_a, afl, pan, m, m, slab1, n1, slab0, slab1);
-                        add_update(outer_b, bfl, pan, m, m, n1, std::min(w, n1 + NBO), 0, slab1);
-                        continue;
-                    } else {
-                        add_update(outer_a, afl, pan, m, m, slab1, nxt, slab0, slab1);
-                    }
+                    add_update(outer_a, afl, pan, m, m, slab1, nxt, slab0, slab1);
                     add_update(outer_b, bfl, pan, m, m, nxt, w, slab0, slab1);
                 }
             }
@@ -982,14 +740,6 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             Lt.count = (int32_t)((int64_t)trsm.size() - Lt.off);
             if (Lp.count > 0) N.sched.push_back(Lp);
             if (Lt.count > 0) N.sched.push_back(Lt);
-            if (!trsm_pre.empty()) {
-                Launch Lr = Lt;
-                Lr.off = (int64_t)trsm.size();
-                Lr.count = (int32_t)trsm_pre.size();
-                Lr.epi = 1;  // the folding kernel instance
-                trsm.insert(trsm.end(), trsm_pre.begin(), trsm_pre.end());
-                N.sched.push_back(Lr);
-            }
             if (!trsm_split.empty()) {
                 Launch Ls = Lt;
                 Ls.off = (int64_t)trsm.size();
@@ -1007,58 +757,8 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 N.sched.push_back(Lq);
             }
             push_gemm_launch(L_PANEL, lev, upd, 0, uflops);
-            // panel_tall = 3, a slab end (two lookahead levels, every big product on the
-            // lookahead stream, as resident grids with la_grid):
-            //   main      [wait A(j-1)] near rows of slab j (row-blocked tall TRSM, 16
-            //             workgroups per 1024 rows) -> [wait B(j-1)] slab j+1's diagonal
-            //             block -= its product (K = NBO) -> the chain of slab j+1
-            //   lookahead X = inv(L_jj), the far rows L = S X^T, then slab j+1's near rows
-            //             (in place) and far rows (into S) -= their products -> A(j), then
-            //             every later column -> B(j)
-            // so the main stream carries only small launches (the chain and its near rows)
-            // and never waits for a big product of the slab it follows.
-            int e_chain = -1;
-            if (tall3 && !tx.empty()) {
-                e_chain = push_record(0);  // slab j's diagonal blocks factored
-                if (a3_ev >= 0) push_wait(0, a3_ev);
-            } else if (!tx.empty()) {
-                emit_tallx(lev, v, tx, 0);
-            }
-            if (!tall_t.empty() || !inv_t.empty()) {
-                Launch Li {};
-                Li.kind = L_INV;
-                Li.level = lev;
-                Li.vr = v;
-                Li.off = (int64_t)B.inv.size();
-                Li.count = (int32_t)inv_t.size();
-                B.inv.insert(B.inv.end(), inv_t.begin(), inv_t.end());
-                if (Li.count > 0) N.sched.push_back(Li);
-                Launch Lt2 {};
-                Lt2.kind = L_TALL;
-                Lt2.level = lev;
-                Lt2.vr = v;
-                Lt2.off = (int64_t)B.tall.size();
-                Lt2.count = (int32_t)tall_t.size();
-                B.tall.insert(B.tall.end(), tall_t.begin(), tall_t.end());
-                if (Lt2.count > 0) N.sched.push_back(Lt2);
-            }
-            if (tall3 && !tx.empty()) {
-                const int e_near = push_record(0);  // slab j's near rows solved
-                push_wait(1, e_chain);
-                emit_tallx(lev, v, tx, 1);  // X and the far rows
-                push_wait(1, e_near);
-                push_gemm_launch(L_GEMM, lev, a3, 0, a3fl, 1);
-                if (!a3.empty()) a3_ev = push_record(1);
-                const int b_prev = b3_ev;
-                push_gemm_launch(L_PANEL, lev, b3, 0, b3fl, 1);
-                b3_ev = push_record(1);
-                if (!d3.empty()) {
-                    if (b_prev >= 0) push_wait(0, b_prev);
-                    push_gemm_launch(L_PANEL, lev, d3, 0, d3fl);
-                }
-            }
-            // split fronts: a slab is final after the TRSM of its last block (tall mode:
-            // after the slab's tall TRSM); at a slab end no inner update is pending
+            // split fronts: a slab is final after the TRSM of its last block; at a slab end
+            // no inner update is pending
             for (int32_t s : large) {
                 const int w = S.w(s);
                 if (!is_split(s) || w <= k0) continue;
@@ -1067,34 +767,20 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             }
             int e_trsm = -1;
             if (!outer_b.empty()) e_trsm = push_record(0);
-            if (!outer_a.empty() || !outer_a2.empty()) {
+            if (!outer_a.empty()) {
                 if (b_pending >= 0) {
                     push_wait(0, b_pending);
                     b_pending = -1;
                 }
-                double fa = 0.0, fa2 = 0.0;
-                for (const GemmTask& t : outer_a) fa += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
-                fa2 = afl - fa;
-                push_gemm_launch(L_PANEL, lev, outer_a, 0, fa);
-                push_gemm_launch(L_GEMM, lev, outer_a2, 0, fa2);
-                // la_after: the lookahead stream's rest starts once the next slab's update is
-                // done (that update runs alone; the rest overlaps the next slab's chain only)
-                if (S.opt.la_after && !outer_b.empty()) e_trsm = push_record(0);
+                push_gemm_launch(L_PANEL, lev, outer_a, 0, afl);
             }
             if (!outer_b.empty()) {
                 push_wait(1, e_trsm);
                 push_gemm_launch(L_PANEL, lev, outer_b, 0, bfl, 1);
                 b_pending = push_record(1);
             }
-            if (!cbs.empty()) {  // after this slab's outer update, on the lookahead stream
-                if (outer_b.empty()) push_wait(1, push_record(0));
-                push_gemm_launch(L_CB, lev, cbs, 1, cbfl, 1);
-                cb_pending = push_record(1);  // joined at the level end (the chain never waits for it)
-            }
         }
         if (b_pending >= 0) push_wait(0, b_pending);
-        if (b3_ev >= 0) push_wait(0, b3_ev);  // panel_tall = 3: the lookahead stream's last far rows
-        if (cb_pending >= 0) push_wait(0, cb_pending);
         // early-delivery children: the CB SYRK in column groups, an event after each
         // (the group's comm sub-step waits for exactly that event)
         for (int32_t s : large) {
@@ -1120,7 +806,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             double fl = 0.0;
             for (int32_t s : large) {
                 const int w = S.w(s), m = S.sn_m[s], mb = m - w;
-                if (mb <= 0 || (w >= 256) != (big == 1) || is_split(s) || is_early_sender(s, v) || cb_slab(s)) continue;
+                if (mb <= 0 || (w >= 256) != (big == 1) || is_split(s) || is_early_sender(s, v)) continue;
                 GemmTask t {};
                 t.C = cb_pool + coff[s];
                 t.A = panel_pool + poff[s] + w;

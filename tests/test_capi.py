@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_version_and_status_strings():
     L = sc.lib()
-    assert L.sc_version() == 100
+    assert L.sc_version() == 110
     assert L.sc_status_string(3) == b"A is not positive definite."
     assert L.sc_status_string(0) == b"ok"
     assert L.sc_status_string(-1) == b"invalid argument"
@@ -43,12 +43,21 @@ def test_default_options():
     o = sc.default_options()
     assert o.relax == 1 and list(o.nrelax) == [4, 16, 48] and o.small_front_max == 128
     assert o.panel_nb == 64 and o.panel_nb_outer == 1024 and o.syrk_tile == 0
-    # round-4 fields: distributed assembly and two slab pieces on; the measured-slower
-    # schedule knobs off
     assert o.dist_asm == 1 and o.dist_pieces == 2
-    assert o.la_grid == 0 and o.cb_slab == 0 and o.la_split == 1 and o.la_after == 0 and o.cb_gather_min_w == 0
-    assert o.lookahead == 1 and o.panel_tall == 0
     assert o.lookahead == 1 and o.inner_order == 1 and o.asm_tile_min_m == 0
+    # round 5: the measured-slower schedule knobs are gone from the ABI
+    names = {f[0] for f in type(o)._fields_}
+    for gone in ("panel_tall", "trsm_fold", "la_grid", "cb_slab", "cb_gather_min_w", "la_split", "la_after",
+                 "cb_lean_kmin", "cb_small_kmax"):
+        assert gone not in names
+
+
+def test_debug_hooks_live_in_their_own_header():
+    inc = os.path.join(ROOT, "include")
+    main = re.sub(r"/\*.*?\*/", "", open(os.path.join(inc, "sparsecholesky.h")).read(), flags=re.S)
+    dbg = open(os.path.join(inc, "sparsecholesky_debug.h")).read()
+    assert "sc_debug_" not in main
+    assert "sc_debug_contention" in dbg and "sc_debug_syrk" in dbg
 
 
 def test_bad_arguments_return_errors():

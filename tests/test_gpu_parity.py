@@ -174,6 +174,32 @@ def test_not_positive_definite_tiny_tree(gpu, mtx, tiny_dense):
         assert num.factor(A.x) == 0
 
 
+@pytest.mark.parametrize("tiny_dense", [0, 1])
+def test_async_factor_then_status_tiny(gpu, mtx, tiny_dense):
+    # an async factorization whose status is never read, followed by another
+    # factorization through the same handle, must not leak its status word into the
+    # second one's (the tiny launches store the word to pinned memory themselves)
+    torch = pytest.importorskip("torch")
+    A = mtx("bcsstk01")
+    num = sc.Numeric(sc.Symbolic(A, tiny_dense=tiny_dense))
+    x = A.x.copy()
+    diag = A.p[41] - 1
+    x[diag] = -1.0
+    st_bad, *_ = oracle.chol(sc.csc_matrix(A.n_rows, A.n_cols, A.p, A.i, x))
+    assert st_bad > 0
+    good = torch.from_numpy(A.x.copy()).to("cuda:0")
+    bad = torch.from_numpy(x).to("cuda:0")
+    torch.cuda.synchronize()
+    for _ in range(3):
+        assert num.factor_device(good.data_ptr(), sync=False) == 0
+        assert num.factor_device(bad.data_ptr()) == st_bad
+        assert num.factor_device(bad.data_ptr(), sync=False) == 0
+        assert num.factor_device(good.data_ptr(), sync=False) == 0
+        assert num.status() == 0
+        assert num.factor_device(bad.data_ptr(), sync=False) == 0
+        assert num.status() == st_bad
+
+
 def test_repeat_factorization_bitwise_deterministic(gpu):
     A = sc.laplacian3d(16)
     s = sc.Symbolic(A)
@@ -392,16 +418,11 @@ def lap48_oracle():
     return A, Lp, Li, Lx
 
 
-@pytest.mark.parametrize("opts", [{}, dict(asm_tile_min_m=1024), dict(cb_gather=0), dict(panel_tall=1),
-                                  dict(trsm_split_wg=1), dict(panel_tall=2), dict(panel_tall=2, lookahead=0),
-                                  dict(la_grid=448), dict(panel_tall=3), dict(panel_tall=3, la_grid=448),
-                                  dict(panel_tall=4, la_grid=448), dict(cb_slab=1), dict(cb_slab=1, la_grid=448),
-                                  dict(cb_slab=1, cb_gather=0, panel_nb_outer=256), dict(lookahead=2),
-                                  dict(lookahead=3)],
-                         ids=["default", "tiled_asm", "assembled_cb", "tall_trsm", "split_potrf", "tall_inv",
-                              "tall_inv_nolookahead", "resident_lookahead", "two_level", "two_level_resident",
-                              "two_level_left_looking", "cb_by_slab", "cb_by_slab_resident", "cb_by_slab_assembled",
-                              "left_looking", "left_looking_lookahead"])
+@pytest.mark.parametrize("opts", [{}, dict(asm_tile_min_m=1024), dict(cb_gather=0), dict(trsm_split_wg=1),
+                                  dict(lookahead=0), dict(cb_gather=0, panel_nb_outer=256), dict(panel_psk=1),
+                                  dict(panel_psk=1, psk_rows=128, lookahead=0)],
+                         ids=["default", "tiled_asm", "assembled_cb", "split_potrf", "no_lookahead",
+                              "assembled_cb_nbo256", "psk", "psk128_no_lookahead"])
 def test_lap48_full_parity(gpu, lap48_oracle, opts):
     # the whole 48^3 factor (n = 110592, F = 7.07e10: a 2304-wide root, CB SYRK with K
     # up to 1152 on 128 x 128 tiles) against the oracle, exact pattern and rel-Fro;
@@ -419,10 +440,8 @@ def test_lap48_full_parity(gpu, lap48_oracle, opts):
 
 
 @pytest.mark.parametrize("nranks,rccl,opts", [(2, False, {}), (4, False, {}), (8, False, {}), (2, True, {}),
-                                               (4, True, {}), (8, True, {}), (8, False, dict(panel_tall=1)),
-                                               (8, False, dict(panel_tall=2)), (2, True, dict(panel_tall=2)),
+                                               (4, True, {}), (8, True, {}),
                                                (8, False, dict(dist_asm=0)), (4, True, dict(dist_asm=0)),
-                                               (8, False, dict(panel_tall=3, la_grid=448)),
                                                (4, False, dict(dist_pieces=1)), (8, True, dict(dist_pieces=16)),
                                                (4, True, dict(dist_pieces=3))])
 def test_partitioned_defaults_lap48(gpu, lap48_oracle, nranks, rccl, opts):
@@ -461,11 +480,8 @@ def lap64_oracle():
     return A, Lp, Li, Lx
 
 
-@pytest.mark.parametrize("opts", [{}, dict(asm_tile_min_m=1024), dict(panel_tall=2),
-                                  dict(panel_tall=3, la_grid=448), dict(panel_tall=4, la_grid=448),
-                                  dict(cb_slab=1, la_grid=448), dict(lookahead=2)],
-                         ids=["default", "tiled_asm", "tall_inv", "two_level_resident", "two_level_left_looking",
-                              "cb_by_slab_resident", "left_looking"])
+@pytest.mark.parametrize("opts", [{}, dict(asm_tile_min_m=1024), dict(panel_psk=1)],
+                         ids=["default", "tiled_asm", "psk"])
 def test_lap64_full_parity(gpu, lap64_oracle, opts):
     # the whole 64^3 factor (n = 262144, F = 4.15e11) against the oracle: a root of about
     # 4096 columns in four 1024-column slabs (lookahead-stream outer updates, recursive
@@ -751,24 +767,9 @@ def test_dense_matrix_large_front(gpu):
 # large-front schedule options: inner slab update order (0 right-looking, 1
 # recursive), lookahead (0 none, 1 trailing updates on a second stream), tiled assembly
 PANEL_OPTS = [dict(inner_order=0), dict(inner_order=0, lookahead=0), dict(lookahead=0), dict(asm_tile_min_m=1),
-              dict(asm_tile_min_m=300), dict(panel_nb_outer=128, lookahead=0), dict(panel_tall=1),
-              dict(panel_tall=1, panel_nb_outer=128), dict(trsm_fold=1), dict(trsm_fold=1, panel_nb_outer=128),
-              dict(trsm_split_wg=1), dict(trsm_split_wg=1, panel_nb_outer=128), dict(trsm_split_wg=1, panel_tall=1),
-              dict(panel_tall=2), dict(panel_tall=2, panel_nb_outer=128), dict(panel_tall=2, lookahead=0),
-              dict(panel_tall=2, panel_nb_outer=192, lookahead=0), dict(panel_tall=2, asm_tile_min_m=100000),
-              dict(panel_tall=2, inner_order=0), dict(la_grid=448), dict(la_grid=8, panel_nb_outer=128),
-              dict(la_grid=64, panel_tall=2, panel_nb_outer=128), dict(panel_tall=3), dict(panel_tall=3, la_grid=448),
-              dict(panel_tall=3, panel_nb_outer=128), dict(panel_tall=3, panel_nb_outer=192, la_grid=64),
-              dict(panel_tall=3, panel_nb_outer=128, asm_tile_min_m=100000), dict(panel_tall=4, la_grid=448),
-              dict(panel_tall=4, panel_nb_outer=128), dict(panel_tall=4, panel_nb_outer=192, la_grid=64),
-              dict(cb_slab=1), dict(cb_slab=1, panel_nb_outer=128), dict(cb_slab=1, cb_gather=0, panel_nb_outer=128),
-              dict(cb_slab=1, la_grid=64, panel_nb_outer=192), dict(cb_slab=1, lookahead=0, panel_nb_outer=128),
-              dict(lookahead=2), dict(lookahead=2, panel_nb_outer=128), dict(lookahead=2, panel_nb_outer=192, inner_order=0),
-              dict(lookahead=2, panel_tall=1, panel_nb_outer=128), dict(lookahead=3), dict(lookahead=3, panel_nb_outer=128),
-              dict(lookahead=3, panel_nb_outer=192, inner_order=0), dict(la_split=4, panel_nb_outer=128),
-              dict(la_split=3), dict(la_after=1), dict(la_after=1, panel_nb_outer=128), dict(cb_lean_kmin=0),
-              dict(cb_small_kmax=256), dict(cb_gather_min_w=64),
-              dict(cb_gather_min_w=100000)]
+              dict(asm_tile_min_m=300), dict(panel_nb_outer=128, lookahead=0), dict(trsm_split_wg=1),
+              dict(trsm_split_wg=1, panel_nb_outer=128), dict(panel_nb_outer=192, inner_order=0),
+              dict(syrk_lean_kmax=0), dict(cb_tail_split=0)]
 
 
 @pytest.mark.parametrize("opts", PANEL_OPTS, ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()))
@@ -804,3 +805,69 @@ def test_missing_diagonal_not_pd(gpu):
     A = sc.triplet_to_csc_matrix([0, 0], [0, 1], [4.0, 1.0], 2)
     r = sc.chol(A)
     assert not r.has_value() and r.status == 2
+
+
+def _dense_spd(n, seed):
+    rng = np.random.default_rng(seed)
+    M = rng.standard_normal((n, n))
+    D = M @ M.T + n * np.eye(n)
+    iu = np.triu_indices(n)
+    return sc.triplet_to_csc_matrix(iu[0], iu[1], D[iu], n)
+
+
+PSK_CASES = [("lap16_allfronts", dict(small_front_max=0)), ("lap16_allfronts_rl", dict(small_front_max=0, inner_order=0)),
+             ("dense1350", {}), ("dense1350_nbo128", dict(panel_nb_outer=128)),
+             ("dense1350_nbo192_rl", dict(panel_nb_outer=192, inner_order=0)), ("lap24", {}),
+             ("lap24_nolookahead", dict(lookahead=0))]
+
+
+@pytest.mark.parametrize("rows", [64, 128, 256])
+@pytest.mark.parametrize("case,opts", PSK_CASES, ids=[c for c, _ in PSK_CASES])
+def test_psk_bitwise_equal_per_step(gpu, case, opts, rows):
+    # the persistent slab chain (one launch per slab and level, steps ordered by device-
+    # scope flags) forms the same sums in the same order as the per-step launches: the
+    # factor is bitwise identical, and so is a second factorization through the same
+    # handle (flags re-armed) and a hipGraph replay
+    A = _dense_spd(1350, 5) if case.startswith("dense") else sc.laplacian3d(int(case[3:5]))
+    facs = []
+    for psk in (0, 1):
+        for graph in ((0,) if psk == 0 else (0, 1)):
+            num = sc.Numeric(sc.Symbolic(A, panel_psk=psk, psk_rows=rows, use_graph=graph, **opts))
+            for _ in range(2):
+                assert num.factor(A.x) == 0
+                facs.append(num.export()[1].x.copy())
+    for f in facs[1:]:
+        assert np.array_equal(facs[0], f)
+    st, Lp, Li, Lx = oracle.chol(A)
+    assert rel_fro(facs[0], Lx) < TOL
+
+
+def test_psk_not_positive_definite(gpu):
+    # a broken pivot inside a persistent slab: the owner's POTRF reports the oracle's
+    # column, the other workgroups still finish (no hang), and a good refactorization
+    # through the same handle clears it
+    A = _dense_spd(700, 9)
+    x = A.x.copy()
+    k = 333
+    diag = A.p[k + 1] - 1
+    assert A.i[diag] == k
+    x[diag] = -1.0
+    st, *_ = oracle.chol(sc.csc_matrix(A.n_rows, A.n_cols, A.p, A.i, x))
+    assert st > 0
+    num = sc.Numeric(sc.Symbolic(A, panel_psk=1))
+    assert num.factor(x) == st
+    assert num.factor(A.x) == 0
+    _, L = num.export()
+    assert rel_fro(L.x, oracle.chol(A)[3]) < TOL
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_psk_partitioned_lap24(gpu, nranks):
+    # emulated multi-rank plan with the persistent slab chains on every rank's own fronts
+    A = sc.laplacian3d(24)
+    ref = sc.Numeric(sc.Symbolic(A, panel_nb_outer=128, dist_cbb=128))
+    assert ref.factor(A.x) == 0
+    v = sc.Numeric(sc.Symbolic(A, panel_psk=1, panel_nb_outer=128, dist_cbb=128), nranks=nranks, virtual=True)
+    assert v.factor(A.x) == 0
+    st, Lp, Li, Lx = oracle.chol(A)
+    assert rel_fro(v.export()[1].x, Lx) < TOL
