@@ -338,10 +338,12 @@ int64_t sc_dist_schedule(const sc_symbolic* sym, int32_t nranks, int32_t rank, i
                          int32_t* peer, int64_t* bytes, int32_t* is_send, int64_t cap);
 /* The plan's comm steps in their global order: kind (0 INIT: assembled columns to
  * the ranks that factor / update them, 1 SLAB: a final panel slab to its users,
- * 2 DELIVER: contribution blocks to the parent's owner), assembly-tree level and
- * front (-1: a level's collective delivery).  Returns the step count. */
+ * 2 DELIVER: contribution blocks to the parent's owner), assembly-tree level, front
+ * (-1: a level's collective delivery), k (SLAB: the slab; DELIVER of an early child:
+ * its column group) and p (SLAB: the column piece of the slab).  Any array may be
+ * NULL.  Returns the step count. */
 int64_t sc_dist_steps(const sc_symbolic* sym, int32_t nranks, int32_t* kind, int32_t* level, int32_t* front,
-                      int64_t cap);
+                      int32_t* k, int32_t* p, int64_t cap);
 /* Plan summary: per supernode the rank-group size (1 = inside one rank's subtree),
  * for split fronts the number of ranks computing its contribution block (0 = not
  * split), for distributed panels the number of ranks factoring its slabs (0 = the

@@ -97,8 +97,9 @@ def comm_by_kind(symb, n, link_gbs, msg_us):
 
 def rank_timeline(num):
     """From one eager profiled factorization of a dry handle: (total ms, post[step],
-    need[step]) -- the step's comm-stream start, and the start of the first main-stream
-    launch after it in schedule order (the point the main stream waits for the step)."""
+    need[step], main-stream launches [(t0, t1, kind)]) -- the step's comm-stream start,
+    and the start of the first main-stream launch after it in schedule order (the point
+    the main stream waits for the step)."""
     tl = num.launch_times()
     t0, t1, kind, step, strm = tl["t0"], tl["t1"], tl["kind"], tl["step"], tl["stream"]
     total = float(max(t1.max(), 0.0)) if len(t1) else 0.0
@@ -110,12 +111,14 @@ def rank_timeline(num):
         post[st] = float(t0[i])
         nxt = next((float(t0[j]) for j in range(i + 1, len(t0)) if strm[j] == 0), total)
         need[st] = max(nxt, float(t1[i]))
-    return total, post, need
+    main = [(float(a), float(b), int(k)) for a, b, k, q in zip(t0, t1, kind, strm) if q == 0 and k != 6]
+    return total, post, need, main
 
 
-def critical_path(symb, n, timelines, link_gbs, msg_us):
+def critical_path(symb, n, timelines, link_gbs, msg_us, explain=False):
     """Discrete-event replay of the plan's comm steps over the ranks' dry timelines (see
-    the module docstring).  Returns per-rank finish times (ms)."""
+    the module docstring).  Returns per-rank finish times (ms); with explain=True also
+    the critical path as a chain of segments (see explain_chain)."""
     sends = {}  # step -> [(src, dst, bytes)] in plan order
     for r in range(n):
         step, peer, nb, snd = symb.dist_schedule(n, r)
@@ -125,27 +128,103 @@ def critical_path(symb, n, timelines, link_gbs, msg_us):
     delay = [0.0] * n      # accumulated wait of each rank's main stream
     comm_free = [0.0] * n  # each rank's comm stream
     link_free = {}
+    # per rank, the waits that raised its delay, in order: the step, its need point (in
+    # the rank's own dry timeline), the delay after it, and the message that arrived last
+    # (source rank, its post point, how many of the source's own waits preceded it, what
+    # bounded the transfer's start, the transfer time)
+    events = [[] for _ in range(n)]
     for st in sorted(sends):
         msgs = sends[st]
         parts = sorted({m[0] for m in msgs} | {m[1] for m in msgs})
         start = {}
         for r in parts:
-            _, post, _ = timelines[r]
+            post = timelines[r][1]
             start[r] = max(post.get(st, 0.0) + delay[r], comm_free[r])
         done = dict(start)
+        last = {}
         for src, dst, b in msgs:
-            t = max(start[src], start[dst], link_free.get((src, dst), 0.0))
-            t += b / (link_gbs * 1e9) * 1e3 + msg_us * 1e-3
+            lf = link_free.get((src, dst), 0.0)
+            t0 = max(start[src], start[dst], lf)
+            xfer = b / (link_gbs * 1e9) * 1e3 + msg_us * 1e-3
+            t = t0 + xfer
             link_free[(src, dst)] = t
             done[src] = max(done[src], t)
             done[dst] = max(done[dst], t)
+            if t > last.get(dst, (-1.0,))[0]:
+                bound = "src" if t0 == start[src] else ("link" if t0 == lf else "dst")
+                last[dst] = (t, src, bound, xfer, len(events[src]))
         for r in parts:
             comm_free[r] = done[r]
-            if any(m[1] == r for m in msgs):  # a receiver waits at its need point
-                _, _, need = timelines[r]
-                nd = need.get(st, 0.0)
-                delay[r] = max(delay[r], done[r] - nd)
-    return [round(max(timelines[r][0] + delay[r], comm_free[r]), 2) for r in range(n)]
+            if r in last:  # a receiver waits at its need point
+                nd = timelines[r][2].get(st, 0.0)
+                nw = done[r] - nd
+                if nw > delay[r]:
+                    t, src, bound, xfer, nsrc = last[r]
+                    events[r].append(dict(step=st, need=nd, delay=nw, prev=delay[r], src=src,
+                                          src_post=timelines[src][1].get(st, 0.0), src_events=nsrc, bound=bound,
+                                          xfer=xfer))
+                    delay[r] = nw
+    finish = [round(max(timelines[r][0] + delay[r], comm_free[r]), 2) for r in range(n)]
+    if not explain:
+        return finish
+    return finish, explain_chain(symb, n, timelines, events, finish)
+
+
+KIND_NAMES = {0: "small", 1: "asm", 2: "potrf", 3: "trsm", 4: "panel", 5: "cb", 6: "comm", 7: "psk"}
+
+
+def explain_chain(symb, n, timelines, events, finish):
+    """Backtrack the critical path from the rank that finishes last.  Each element: a
+    compute segment on one rank (its dry timeline between two points, with the main-
+    stream kernel time in it by launch kind) and the hand-off that preceded it (step id,
+    kind, level, front, slab / group k, piece p; wait ms = from the source's post point,
+    delayed as the source ran, to the data's arrival: transfer plus link / comm-stream
+    queueing, `bound` says which limited the start).  The chain continues on the source
+    rank at its post point, so finish = sum(compute) + sum(wait) when the last rank ends
+    on its own compute."""
+    steps = symb.dist_steps(n)
+    r = max(range(n), key=lambda q: finish[q])
+    t_end = timelines[r][0]
+    nev = len(events[r])  # the replay applies a rank's latest delay to everything after it
+    chain = []
+
+    def by_kind(rank, a, b):
+        out = {}
+        for t0, t1, k in timelines[rank][3]:
+            lo, hi = max(t0, a), min(t1, b)
+            if hi > lo:
+                nm = KIND_NAMES.get(k, str(k))
+                out[nm] = out.get(nm, 0.0) + hi - lo
+        return {k: round(v, 3) for k, v in out.items()}
+
+    guard = 0
+    while guard < 100000:
+        guard += 1
+        if nev == 0:
+            chain.append(dict(rank=r, compute_ms=round(t_end, 3), compute_by_kind=by_kind(r, 0.0, t_end),
+                              wait_ms=0.0))
+            break
+        e = events[r][nev - 1]  # the wait that set the delay this point of the rank runs behind
+        st = e["step"]
+        src, ns = e["src"], e["src_events"]
+        src_at = e["src_post"] + (events[src][ns - 1]["delay"] if ns > 0 else 0.0)
+        chain.append(dict(rank=r, compute_ms=round(t_end - e["need"], 3), compute_by_kind=by_kind(r, e["need"], t_end),
+                          step=st, step_kind={0: "INIT", 1: "SLAB", 2: "DELIVER"}.get(int(steps["kind"][st])),
+                          level=int(steps["level"][st]), front=int(steps["front"][st]), k=int(steps["k"][st]),
+                          p=int(steps["p"][st]), wait_ms=round(e["need"] + e["delay"] - src_at, 3), src=src,
+                          bound=e["bound"], transfer_ms=round(e["xfer"], 3)))
+        r, t_end, nev = src, e["src_post"], ns
+    chain.reverse()
+    tot = {"compute_ms": round(sum(c["compute_ms"] for c in chain), 3),
+           "wait_ms": round(sum(c["wait_ms"] for c in chain), 3)}
+    by_step_kind, by_launch = {}, {}
+    for c in chain:
+        if "step_kind" in c:
+            by_step_kind[c["step_kind"]] = round(by_step_kind.get(c["step_kind"], 0.0) + c["wait_ms"], 3)
+        for k, v in c["compute_by_kind"].items():
+            by_launch[k] = round(by_launch.get(k, 0.0) + v, 3)
+    return dict(chain=chain, totals=tot, wait_by_step_kind=by_step_kind, compute_by_launch_kind=by_launch,
+                finish_ms=max(finish))
 
 
 def main():
@@ -213,9 +292,10 @@ def main():
             if args.timeline:
                 num.set_profile(1)
                 num.factor_device(d_Ax.data_ptr(), sync=True)
-                tot, post, need = rank_timeline(num)
+                tot, post, need, main = rank_timeline(num)
                 f = best / tot if tot > 0 else 1.0  # the event-bracketed run is slower: rescale
-                tls.append((best, {k: v * f for k, v in post.items()}, {k: v * f for k, v in need.items()}))
+                tls.append((best, {k: v * f for k, v in post.items()}, {k: v * f for k, v in need.items()},
+                            [(a * f, b * f, k) for a, b, k in main]))
             del num
             gc.collect()
             msg = f"  n={n} rank {r}: {best:.1f} ms"
@@ -241,8 +321,9 @@ def main():
             rec["max_rank_ms_graph"] = max(per_g)
         if tls:
             for gbs in sorted({args.link_gbs, 100.0}):
-                cp = critical_path(symb, n, tls, gbs, args.msg_us)
+                cp, why = critical_path(symb, n, tls, gbs, args.msg_us, explain=True)
                 rec[f"critical_path_ms_{int(gbs)}GBs"] = cp
+                rec[f"critical_path_explained_{int(gbs)}GBs"] = why
                 rec[f"max_critical_path_ms_{int(gbs)}GBs"] = max(cp)
                 rec[f"projected_gflops_critical_path_{int(gbs)}GBs"] = round(F / (max(cp) * 1e-3) / 1e9, 1)
             rec["timeline_total_ms"] = [round(t[0], 2) for t in tls]

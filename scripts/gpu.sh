@@ -7,6 +7,8 @@
 #   scripts/gpu.sh breakdown [variant ...]  per-level eager breakdown (in-tree, or gpurun_var/<variant>)
 #   scripts/gpu.sh ab SPEC ...              interleaved A/B bench of variants (build_variants.sh);
 #                                           SPEC = NAME[@key=val[@key=val...]] (sc_options via --opt)
+#   scripts/gpu.sh abopt SPEC ...           interleaved A/B bench of option sets on the in-tree build;
+#                                           SPEC = NAME[@key=val[@key=val...]]
 #   scripts/gpu.sh rehearse [k] [ranks...]  bench.py's N>1 branch on this one GPU (host / dry transport)
 #   scripts/gpu.sh project [--opt k=v ...]  per-rank dry projection of the N-GPU plan + comm term
 #   scripts/gpu.sh rccl                     emulated ranks over real RCCL send/recv to self, kernel trace
@@ -75,6 +77,20 @@ case "$task" in
         timeout -k 10 300 python3 gpurun_var/$v/bench.py --steps 5 --warmup 2 --no-cpu-baseline "${opts[@]}" \
           > gpurun_out/var_$tag.log 2>&1 || { tail -5 gpurun_out/var_$tag.log; exit 1; }
         python3 -c "import json; d=json.loads([l for l in open('gpurun_out/var_$tag.log') if l.startswith('{')][-1]); print('$spec', d['ms_per_step'], d['roofline']['achieved'], d['validation']['backward_error'])"
+      done
+    done ;;
+  abopt)
+    for rep in 1 2; do
+      for spec in "$@"; do
+        v=${spec%%@*}
+        opts=()
+        if [ "$spec" != "$v" ]; then
+          IFS='@' read -ra kv <<< "${spec#*@}"
+          for o in "${kv[@]}"; do opts+=(--opt "$o"); done
+        fi
+        timeout -k 10 300 python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline "${opts[@]}" \
+          > gpurun_out/abopt_${v}_$rep.log 2>&1 || { tail -5 gpurun_out/abopt_${v}_$rep.log; exit 1; }
+        python3 -c "import json; d=json.loads([l for l in open('gpurun_out/abopt_${v}_$rep.log') if l.startswith('{')][-1]); print('$spec', d['ms_per_step'], d['roofline']['achieved'], d['validation']['backward_error'])"
       done
     done ;;
   rehearse)

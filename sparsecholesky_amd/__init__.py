@@ -144,7 +144,7 @@ _SIGS = [
     ("sc_numeric_create_dist", _I64, [_P, _I32, _I32, _I32, _P, C.POINTER(_P)]),
     ("sc_dist_schedule", _I64, [_P, _I32, _I32, _P, _P, _P, _P, _I64]),
     ("sc_dist_plan_info", _I64, [_P, _I32, _P, _P, _P, C.POINTER(_I64)]),
-    ("sc_dist_steps", _I64, [_P, _I32, _P, _P, _P, _I64]),
+    ("sc_dist_steps", _I64, [_P, _I32, _P, _P, _P, _P, _P, _I64]),
     ("sc_numeric_create_dist_host", _I64, [_P, _I32, _I32, _I32, C.c_void_p, _P, C.POINTER(_P)]),
     ("sc_numeric_create_dist_dry", _I64, [_P, _I32, _I32, _I32, C.POINTER(_P)]),
     ("sc_numeric_create_dist_emulated", _I64, [_P, _I32, _I32, _I32, C.POINTER(_P)]),
@@ -531,11 +531,12 @@ class Symbolic:
         return dict(panel=pb, work=wb, work_lower_bound=lb)
 
     def dist_steps(self, nranks: int) -> dict:
-        """The plan's comm steps in order: kind (0 INIT, 1 SLAB, 2 DELIVER), level, front."""
-        n = _check(lib().sc_dist_steps(self.h, nranks, None, None, None, 0), "dist_steps")
-        k, l, f = (np.zeros(max(n, 1), dtype=np.int32) for _ in range(3))
-        _check(lib().sc_dist_steps(self.h, nranks, _ptr(k), _ptr(l), _ptr(f), n), "dist_steps")
-        return dict(kind=k[:n], level=l[:n], front=f[:n])
+        """The plan's comm steps in order: kind (0 INIT, 1 SLAB, 2 DELIVER), level, front,
+        slab / column group k and slab piece p."""
+        n = _check(lib().sc_dist_steps(self.h, nranks, None, None, None, None, None, 0), "dist_steps")
+        k, l, f, sk, sp = (np.zeros(max(n, 1), dtype=np.int32) for _ in range(5))
+        _check(lib().sc_dist_steps(self.h, nranks, _ptr(k), _ptr(l), _ptr(f), _ptr(sk), _ptr(sp), n), "dist_steps")
+        return dict(kind=k[:n], level=l[:n], front=f[:n], k=sk[:n], p=sp[:n])
 
     def dist_schedule(self, nranks: int, rank: int):
         """This rank's messages in posting order: (comm step, peer, bytes, is_send)."""

@@ -548,7 +548,7 @@ int64_t sc_numeric_memory(sc_numeric* num, int64_t* info, int32_t n) {
 }
 
 int64_t sc_dist_steps(const sc_symbolic* sym, int32_t nranks, int32_t* kind, int32_t* level, int32_t* front,
-                      int64_t cap) {
+                      int32_t* k, int32_t* p, int64_t cap) {
     if (!sym || nranks <= 0) return SC_ERR_ARG;
     sc::DistPlan D;
     int64_t rc = sc::dist_plan(sym->S, nranks, D);
@@ -557,6 +557,8 @@ int64_t sc_dist_steps(const sc_symbolic* sym, int32_t nranks, int32_t* kind, int
         if (kind) kind[i] = D.steps[i].kind;
         if (level) level[i] = D.steps[i].level;
         if (front) front[i] = D.steps[i].s;
+        if (k) k[i] = D.steps[i].k;
+        if (p) p[i] = D.steps[i].p;
     }
     return (int64_t)D.steps.size();
 }
