@@ -115,4 +115,5 @@ def compare(got: dict, ref: dict) -> dict:
                 group_norm_rel=float(np.max(np.abs(gs_g - gs_o) / gs_o)),
                 sketch_J_rel_fro=float(sketch_J),
                 sketch_chunk_rel_fro_max=float(per_chunk.max()),
-                nnz_equal=bool(int(got["nnz"]) == int(ref["nnz"])))
+                # the GPU export keeps the relaxed supernodes' explicit zeros (never equal)
+                entries=(int(got["nnz"]), int(ref["nnz"])))

@@ -37,3 +37,38 @@ def test_dominant_name_forms():
                  "void sc::syrk_mfma_kernel<128, 2, 4, 0, 0, 0>(sc::GemmTask const*",
                  "void sc::syrk_mfma_kernel<64, 2, 2, 1, 0, 0>(sc::GemmTask const*"]:
         assert bench._dominant_entry({name: 1}) is None, name
+
+
+def _summary_mod():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("mfma_util_summary",
+                                                  os.path.join(ROOT, "scripts", "mfma_util_summary.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_mfma_summary_never_reports_a_clock_above_the_part():
+    # GRBM_GUI_ACTIVE / 8 / duration gave 2.8-3.7 GHz for short panel
+    # kernels; such rows must fall back to the time-based busy fraction at 2.4 GHz
+    m = _summary_mod()
+    long_k = {"ns": 25e6, "GRBM_GUI_ACTIVE": 8 * 2.32 * 25e6, "SQ_VALU_MFMA_BUSY_CYCLES": 0.88 * 2.32 * 25e6 * 1024}
+    b, clk, basis = m.busy(long_k)
+    assert abs(clk - 2.32) < 1e-3 and abs(b - 0.88) < 1e-3 and basis == "GRBM_GUI_ACTIVE"
+    short = {"ns": 40e3, "GRBM_GUI_ACTIVE": 8 * 2.87 * 40e3, "SQ_VALU_MFMA_BUSY_CYCLES": 0.25 * 2.4 * 40e3 * 1024}
+    b, clk, basis = m.busy(short)
+    assert clk is None and abs(b - 0.25) < 1e-3 and "2.4" in basis
+
+
+def test_newest_mfma_util_clocks_physical():
+    import json
+
+    p = bench._latest_profile("mfma_util.json")
+    d = json.load(open(p))
+    rows = d["step_kernels"].values()
+    if not any("busy_basis" in r for r in rows):
+        return  # written before the clock check (round 4 and earlier)
+    for r in rows:
+        assert r["clock_GHz"] is None or r["clock_GHz"] <= 2.4 * 1.01, r
+        assert 0.0 <= r["raw_mfma_ratio"] <= 1.0, r
