@@ -155,6 +155,7 @@ _SIGS = [
     ("sc_debug_bench", _I64, [_I32, _I32, _I32, _I32, _I32, C.POINTER(_D)]),
     ("sc_device_count", _I64, []),
     ("sc_debug_chain_stamps", _I64, [_P, _I32, _P, _I64]),
+    ("sc_debug_psk_stamps", _I64, [_P, _I32, _P, _P, _I64]),
     ("sc_debug_time_factor", _I64, [_P, C.c_void_p, _I32, C.POINTER(_D)]),
     ("sc_debug_solve_eager", _I64, [_P, _I32]),
     ("sc_debug_hwid", _I64, [_I32, _I32, _I32, _P]),

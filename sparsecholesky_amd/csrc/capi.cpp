@@ -348,6 +348,11 @@ int64_t sc_debug_chain_stamps(sc_numeric* num, int32_t enable, uint64_t* out, in
     return sc::numeric_chain_stamps(*num->N, enable, out, cap);
 }
 
+int64_t sc_debug_psk_stamps(sc_numeric* num, int32_t enable, int32_t* info, uint64_t* out, int64_t cap) {
+    if (!num || !num->N) return SC_ERR_ARG;
+    return sc::numeric_psk_stamps(*num->N, enable, info, out, cap);
+}
+
 void sc_free_numeric(sc_numeric* num) {
     if (!num) return;
     sc::numeric_free(num->N);

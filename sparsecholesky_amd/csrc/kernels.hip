@@ -1685,6 +1685,11 @@ __global__ __launch_bounds__(256, 2) void psk_kernel(DevPlan P, PskArgs A) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     double* Sd = reinterpret_cast<double*>(S);
     if (tid == 0) s_fail = 0;
+    uint64_t* stamp = A.stamps ? A.stamps + (int64_t)blockIdx.x * PSK_STAMPS : nullptr;
+    auto mark = [&](int q) {
+        if (stamp && tid == 0 && q < PSK_STAMPS) stamp[q] = __builtin_amdgcn_s_memrealtime();
+    };
+    mark(0);
     // lane 0 waits for every flag of fl[idx[0..n)] >= target, then acquires
     auto wait_flags = [&](int lo, int hi, int target, bool l11) {
         if (tid == 0) {
@@ -1731,8 +1736,10 @@ __global__ __launch_bounds__(256, 2) void psk_kernel(DevPlan P, PskArgs A) {
                     }
             }
             psk_signal(fl, j + 1);
+            mark(1 + 3 * j);
         } else {  // wait for L11, stream it from memory (lanes along rows: coalesced)
             wait_flags(0, 0, j + 1, true);
+            mark(1 + 3 * j);
 #pragma unroll 4
             for (int q = 0; q < PNB * PNB / 256; ++q) {
                 const int e = tid + 256 * q, jj = e >> 6, i = e & 63;
@@ -1760,6 +1767,7 @@ __global__ __launch_bounds__(256, 2) void psk_kernel(DevPlan P, PskArgs A) {
             // rows of the slab's diagonal region feed other row blocks' inner updates
             if (r0 < F.s1) psk_signal(fl + 1 + g.rb, j + 1);
         }
+        mark(2 + 3 * j);
         __syncthreads();  // the stream S is read by every TRSM lane before the next step rebuilds it
         if (k1 >= F.s1) continue;
         // inner update of this workgroup's rows: columns [k1, cend), K = [ka, k1)
@@ -1815,6 +1823,7 @@ __global__ __launch_bounds__(256, 2) void psk_kernel(DevPlan P, PskArgs A) {
         // this workgroup's own C stores are read back by its next steps (same CU): drain them
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        mark(3 + 3 * j);
     }
     // the last workgroup to finish re-arms the launch's flags (graph-replay safe)
     __syncthreads();

@@ -235,7 +235,11 @@ struct PskArgs {
     const PskWg* wg;
     int32_t* flags;   // this launch's flags; flags[nflags] = its done counter
     int32_t nflags, nwg;
+    uint64_t* stamps = nullptr;  // debug (sc_debug_psk_stamps): PSK_STAMPS per workgroup, or null
 };
+// debug stamps per workgroup: [0] start, then per step j: L11 ready, TRSM done, update done
+// (s_memrealtime, 100 MHz), at 1 + 3 j
+constexpr int PSK_STAMPS = 1 + 3 * 16;
 hipError_t launch_psk(const DevPlan& P, const PskArgs& A, int rows, hipStream_t st);
 
 // gt: the gather tables (CB tasks with gs >= 0 gather their children's entries)

@@ -205,6 +205,9 @@ struct Numeric {
     PskFront* d_pskf = nullptr;   // persistent slab chains (L_PSK)
     PskWg* d_pskw = nullptr;
     int32_t* d_pskflags = nullptr;
+    std::vector<PskFront> h_pskf;   // host copies (debug stamps)
+    std::vector<PskWg> h_pskw;
+    uint64_t* d_pskstamps = nullptr;  // debug: PSK_STAMPS per workgroup (sc_debug_psk_stamps)
     GemmTask* d_gemm = nullptr;
     int2* d_tiles = nullptr;
     GatherTab gtab;              // the CB SYRK extend-add gather's segment tables (schedule.cpp)
@@ -317,6 +320,7 @@ int64_t numeric_solve_device(Numeric& N, const double* d_b, double* d_x);
 int64_t numeric_solve_host(Numeric& N, const double* b, double* x);
 int64_t debug_syrk(double* dC, int ldc, const double* dA, int lda, int M, int N, int K);
 int64_t numeric_chain_stamps(Numeric& N, int enable, uint64_t* out, int64_t cap);
+int64_t numeric_psk_stamps(Numeric& N, int enable, int32_t* info, uint64_t* out, int64_t cap);
 int64_t debug_bench(int which, int M, int K, int reps, int arg, double* tflops);
 int64_t debug_contention(int M, int K, int chain_rows, int nchain, int mode, int mask_stride, double* out);
 
