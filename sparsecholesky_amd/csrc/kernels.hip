@@ -1613,7 +1613,7 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
 }
 
 template <int BT, int WM, int WN, int TAG, int EPI, int LEAN = 0>
-__global__ __launch_bounds__(64 * WM * WN, LEAN ? (TAG ? 5 : 6) : 1) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
+__global__ __launch_bounds__(64 * WM * WN, LEAN ? (TAG ? 5 : 6) : (BT == 128 && WM * WN == 4 ? 2 : 1)) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
                                                                   const int2* __restrict__ tiles,
                                                                   const int64_t* __restrict__ gblk,
                                                                   const GSeg* __restrict__ gseg) {
@@ -1918,6 +1918,9 @@ static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int b
     if (bt == 64 && lean)
         hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG, EPI, 1>), dim3(n), dim3(256), 0, st, tasks, tiles, gt.blk,
                            gt.seg);
+    else if (bt == SYRK_BT_LARGE4)  // 128 x 128 tiles on 4 waves (64 x 64 per wave)
+        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 2, TAG, EPI>), dim3(n), dim3(256), 0, st, tasks, tiles, gt.blk,
+                           gt.seg);
     else if (bt == 128)
         hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, EPI>), dim3(n), dim3(512), 0, st, tasks, tiles, gt.blk,
                            gt.seg);
@@ -1979,21 +1982,27 @@ hipError_t launch_stamp(uint64_t* slot, hipStream_t st) {
 }
 
 // Multi-GPU staging: strided <-> packed copy of contribution-block / panel column
-// blocks around the RCCL transfers.  One workgroup per COPY_COLS columns of one
-// block, one wave per column, 64 consecutive doubles per wave access (HBM-bound).
+// blocks around the RCCL transfers.  One workgroup per (COPY_COLS columns, COPY_ROWS
+// rows) of one block, one wave per column; every lane keeps 8 loads in flight before
+// its stores (HBM-bound; round 4's one-load-then-one-store loop over whole columns was
+// latency-bound: 0.74 ms per launch, 35 ms of a dry 8-rank step at 128^3).
 __global__ __launch_bounds__(256) void copy2d_kernel(const Copy2D* __restrict__ descs, const int2* __restrict__ tiles,
                                                      int unpack) {
     const int2 t = tiles[blockIdx.x];
     const Copy2D d = descs[t.x];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int j1 = min(d.cols, t.y + COPY_COLS);
-    for (int j = t.y + wid; j < j1; j += 4) {
-        double* a = d.a + (int64_t)j * d.lda;
-        double* b = d.b + (int64_t)j * d.rows;
-        if (unpack) {
-            for (int r = lane; r < d.rows; r += 64) a[r] = b[r];
-        } else {
-            for (int r = lane; r < d.rows; r += 64) b[r] = a[r];
+    const int j0 = t.y & 0xffff, r0 = (t.y >> 16) * COPY_ROWS;
+    const int j1 = min(d.cols, j0 + COPY_COLS), r1 = min(d.rows, r0 + COPY_ROWS);
+    for (int j = j0 + wid; j < j1; j += 4) {
+        const double* __restrict__ src = unpack ? d.b + (int64_t)j * d.rows : d.a + (int64_t)j * d.lda;
+        double* __restrict__ dst = unpack ? d.a + (int64_t)j * d.lda : d.b + (int64_t)j * d.rows;
+        for (int r = r0 + lane; r < r1; r += 64 * 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = r + 64 * u < r1 ? src[r + 64 * u] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (r + 64 * u < r1) dst[r + 64 * u] = v[u];
         }
     }
 }

@@ -19,6 +19,7 @@ constexpr int ASM_TILE_MIN_M = 512;   // fronts at least this tall use the write
 // Output tile edges of the MFMA SYRK kernel (per launch).
 constexpr int SYRK_BT_SMALL = 64;
 constexpr int SYRK_BT_LARGE = 128;
+constexpr int SYRK_BT_LARGE4 = 129;  // launch code: 128 x 128 tiles (tile lists as SYRK_BT_LARGE) on 4 waves
 
 // C/D register map of v_mfma_f64_16x16x4_f64 on gfx950 (cdna_hip_programming.md
 // section 3): col = lane & 15, row = (lane >> 4) + 4 * reg.
@@ -96,8 +97,9 @@ struct Copy2D {
     int32_t rows, cols;
 };
 
-constexpr int COPY_COLS = 16;  // columns per copy workgroup
-// tiles: (descriptor, first column) per workgroup
+constexpr int COPY_COLS = 16;    // columns per copy workgroup
+constexpr int COPY_ROWS = 2048;  // rows per copy workgroup
+// tiles: (descriptor, first column | row chunk << 16) per workgroup
 hipError_t launch_copy2d(const Copy2D* descs, const int2* tiles, int count, bool unpack, hipStream_t st);
 
 // ---- triangular solves with the supernodal factor ----

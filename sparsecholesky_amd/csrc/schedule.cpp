@@ -342,7 +342,9 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         if (L.count == 0) return;
         auto add_tiles = [&](const std::vector<int32_t>& ds) {
             for (int32_t d : ds)
-                for (int j = 0; j < cbld.copies[d].cols; j += COPY_COLS) cbld.ctiles.push_back(make_int2(d, j));
+                for (int j = 0; j < cbld.copies[d].cols; j += COPY_COLS)
+                    for (int rc = 0; rc * COPY_ROWS < cbld.copies[d].rows; ++rc)
+                        cbld.ctiles.push_back(make_int2(d, j | (rc << 16)));
         };
         L.poff = (int64_t)cbld.ctiles.size();
         add_tiles(pack_d);
