@@ -314,9 +314,9 @@ int64_t debug_bench(int which, int M, int K, int reps, int arg, double* tflops) 
             t.M = M;
             t.N = M;
             t.K = K;
-            const int tb = arg == 128 ? 128 : arg == SYRK_BT_LARGE4 ? SYRK_BT_LARGE4 : 64;
+            const int tb = arg == 128 ? 128 : 64;
             std::vector<int2> tiles;
-            append_tiles(tiles, 0, M, M, tb == SYRK_BT_LARGE4 ? 128 : tb);
+            append_tiles(tiles, 0, M, M, tb);
             if (which != 5) xcd_order(tiles.data(), (int64_t)tiles.size());
             (void)hipMalloc(&bt, sizeof(GemmTask));
             (void)hipMalloc(&bl, tiles.size() * sizeof(int2));

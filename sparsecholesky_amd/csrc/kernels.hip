@@ -1613,7 +1613,7 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
 }
 
 template <int BT, int WM, int WN, int TAG, int EPI, int LEAN = 0>
-__global__ __launch_bounds__(64 * WM * WN, LEAN ? (TAG ? 5 : 6) : (BT == 128 && WM * WN == 4 ? 2 : 1)) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
+__global__ __launch_bounds__(64 * WM * WN, LEAN ? (TAG ? 5 : 6) : 1) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
                                                                   const int2* __restrict__ tiles,
                                                                   const int64_t* __restrict__ gblk,
                                                                   const GSeg* __restrict__ gseg) {
@@ -1917,9 +1917,6 @@ static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int b
                           bool lean) {
     if (bt == 64 && lean)
         hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG, EPI, 1>), dim3(n), dim3(256), 0, st, tasks, tiles, gt.blk,
-                           gt.seg);
-    else if (bt == SYRK_BT_LARGE4)  // 128 x 128 tiles on 4 waves (64 x 64 per wave)
-        hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 2, TAG, EPI>), dim3(n), dim3(256), 0, st, tasks, tiles, gt.blk,
                            gt.seg);
     else if (bt == 128)
         hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, EPI>), dim3(n), dim3(512), 0, st, tasks, tiles, gt.blk,

@@ -19,7 +19,6 @@ constexpr int ASM_TILE_MIN_M = 512;   // fronts at least this tall use the write
 // Output tile edges of the MFMA SYRK kernel (per launch).
 constexpr int SYRK_BT_SMALL = 64;
 constexpr int SYRK_BT_LARGE = 128;
-constexpr int SYRK_BT_LARGE4 = 129;  // launch code: 128 x 128 tiles (tile lists as SYRK_BT_LARGE) on 4 waves
 
 // C/D register map of v_mfma_f64_16x16x4_f64 on gfx950 (cdna_hip_programming.md
 // section 3): col = lane & 15, row = (lane >> 4) + 4 * reg.
