@@ -903,7 +903,57 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 const int e = last_ev1(vk, k - 2);
                 if (e >= 0) push_wait(0, e);
                 double* pan = pan_of(vk);
-                for (int k0 = k0s; k0 < k1s; k0 += PNB) {
+                if (S.opt.panel_psk) {  // the slab's chain as one persistent launch, then its pieces
+                    const int TR = S.opt.psk_rows, nfull = (k1s - k0s) / PNB;
+                    if (nfull > 0) {
+                        Launch Lk {};
+                        Lk.kind = L_PSK;
+                        Lk.level = lev;
+                        Lk.vr = vk;
+                        Lk.off = (int64_t)B.pskf.size();
+                        Lk.toff = (int64_t)B.pskw.size();
+                        Lk.foff = B.psk_flags;
+                        PskFront f {};
+                        f.s = s;
+                        f.s0 = k0s;
+                        f.s1 = k1s;
+                        f.nfull = nfull;
+                        f.m = m;
+                        f.flag0 = 0;
+                        f.inner = S.opt.inner_order;
+                        B.pskf.push_back(f);
+                        B.psk_flags += 1 + (k1s - k0s + TR - 1) / TR;
+                        const int nrb = (m - k0s + TR - 1) / TR;
+                        for (int rb = 0; rb < nrb; ++rb) B.pskw.push_back(PskWg {0, rb});
+                        Lk.ntasks = 1;
+                        Lk.count = nrb;
+                        Lk.fcount = (int32_t)(B.psk_flags - Lk.foff);
+                        B.psk_flags += 1;
+                        N.sched.push_back(Lk);
+                    }
+                    if ((k1s - k0s) % PNB) {  // the front's partial last block
+                        const int kp = k0s + nfull * PNB;
+                        Launch Lp {};
+                        Lp.kind = L_POTRF;
+                        Lp.level = lev;
+                        Lp.vr = vk;
+                        Lp.off = (int64_t)potrf.size();
+                        Lp.count = 1;
+                        potrf.push_back(make_int2(s, kp));
+                        N.sched.push_back(Lp);
+                        Launch Lq {};
+                        Lq.kind = L_TRSM;
+                        Lq.level = lev;
+                        Lq.vr = vk;
+                        Lq.big = 1;
+                        Lq.off = (int64_t)trsm.size();
+                        for (int r0 = k1s; r0 < m; r0 += TRSM_ROWS) trsm.push_back(TrsmTask {s, kp, r0, m, 0});
+                        Lq.count = (int32_t)((int64_t)trsm.size() - Lq.off);
+                        if (Lq.count > 0) N.sched.push_back(Lq);
+                    }
+                    for (int p = 0; k0s + p * D.pw < k1s; ++p) emit_step(slab_piece(s, k, p));
+                }
+                for (int k0 = k0s; !S.opt.panel_psk && k0 < k1s; k0 += PNB) {
                     const int nb = std::min(PNB, k1s - k0), k1 = k0 + nb;
                     Launch Lp {};
                     Lp.kind = L_POTRF;
