@@ -1033,7 +1033,6 @@ __global__ __launch_bounds__(256) void chain_init_kernel(DevPlan P, ChainPlan C,
 // image and CB relind, factors front i, stores its panel, and adds its CB into the
 // buffer at the parent's positions (the last front's CB goes to HBM).
 constexpr int CHAIN_IMG = (128 * 129 / 2 + CHAIN_NT - 1) / CHAIN_NT;  // image doubles per thread
-constexpr int CHAIN_ZSLOT = 128 * 129 / 2;  // LDS zero slot (reads outside a front) and, after it, the dummy add slot
 __global__ __launch_bounds__(CHAIN_NT) void front_chain_kernel(DevPlan P, ChainPlan C, int first, int count) {
     extern __shared__ double F[];
     __shared__ __attribute__((aligned(16))) double colbuf[2 * 4 * COLB];
