@@ -109,7 +109,7 @@ typedef struct sc_options {
                                 columns go straight to the rank owning the parent columns they map into, no
                                 assembled-front hand-out); 0: its owner assembles it and sends the pieces */
     int32_t dist_pieces;     /* multi-GPU distributed panels: each final slab is handed over in this many column
-                                pieces (default 2: 512 of a 1024-column slab), each sent as soon as the chain has
+                                pieces (default 4: 256 of a 1024-column slab), each sent as soon as the chain has
                                 finished it, so the next slab's owner starts updating before the slab is done */
     int32_t panel_psk;       /* 1: the 64-column POTRF / TRSM / inner-update chain of each 1024-column slab of the
                                 large fronts runs as ONE persistent launch per slab and level (all fronts of the

@@ -94,7 +94,7 @@ void sc_default_options(sc_options* opt) {
     opt->cb_tail_split = 1;
     opt->tiny_dense = 1;
     opt->dist_asm = 1;
-    opt->dist_pieces = 2;
+    opt->dist_pieces = 4;
     opt->panel_psk = 0;
     opt->psk_rows = 64;
     opt->psk_min_w = 0;

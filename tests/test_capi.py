@@ -43,7 +43,7 @@ def test_default_options():
     o = sc.default_options()
     assert o.relax == 1 and list(o.nrelax) == [4, 16, 48] and o.small_front_max == 128
     assert o.panel_nb == 64 and o.panel_nb_outer == 1024 and o.syrk_tile == 0
-    assert o.dist_asm == 1 and o.dist_pieces == 2
+    assert o.dist_asm == 1 and o.dist_pieces == 4
     assert o.lookahead == 1 and o.inner_order == 1 and o.asm_tile_min_m == 0
     # round 5: the measured-slower schedule knobs are gone from the ABI
     names = {f[0] for f in type(o)._fields_}
