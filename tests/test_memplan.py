@@ -51,3 +51,21 @@ def test_plan_lap128_budgets():
     # with owner assembly), well inside the 288 GB of one MI355X
     assert per_rank.max() <= 0.4 * single, (per_rank / 1e9).round(1)
     assert sc.lib().sc_memory_plan_check(s.h, 8) == 0
+
+
+@pytest.mark.parametrize("k", [48, 64])
+def test_per_rank_memory_shrinks_with_ranks(k):
+    # a rank holding part of a split front's contribution block keeps the whole
+    # mb x mb square (distributed assembly: child CB columns go to the rank assembling the
+    # parent columns they map into).  The per-rank total still falls with every doubling
+    # of the ranks (panels are dealt out); the work arena alone stops shrinking between 4
+    # and 8 ranks (48^3: 0.228 -> 0.235 GB, 64^3: 0.645 -> 0.720 GB; 128^3: 10.5 -> 11.4
+    # GB), bounded here.
+    s = sc.Symbolic(sc.laplacian3d(k))
+    tot, work = [], []
+    for n in (1, 2, 4, 8):
+        mp = s.memory_plan(n)
+        tot.append(float((mp["panel"] + mp["work"]).max()))
+        work.append(float(mp["work"].max()))
+    assert all(b < a for a, b in zip(tot, tot[1:])), tot
+    assert work[3] <= 0.55 * work[0] and work[3] <= 1.15 * work[2], work
