@@ -1700,7 +1700,6 @@ __global__ __launch_bounds__(256, 2) void psk_kernel(DevPlan P, PskArgs A) {
             if (!ok && !s_fail) {
                 s_fail = 1;
                 report_fail(P.info, cg + F.s0);  // a lost hand-off surfaces as a failed factorization
-                
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
