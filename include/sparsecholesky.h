@@ -34,7 +34,7 @@ extern "C" {
 #pragma GCC visibility push(default)
 #endif
 
-#define SC_VERSION 110 /* 1.1.0: sc_options pruned to the live knobs; debug hooks in sparsecholesky_debug.h */
+#define SC_VERSION 120 /* 1.2.0: persistent slab chain options removed; out-of-range lookahead / inner_order rejected */
 
 enum sc_status {
     SC_OK = 0,
@@ -61,17 +61,18 @@ typedef struct sc_options {
     int32_t relax;           /* 1 = relaxed supernode amalgamation (CHOLMOD-style) */
     int32_t nrelax[3];       /* width thresholds for amalgamation */
     double zrelax[3];        /* zero-fraction thresholds for amalgamation */
-    int32_t small_front_max; /* fronts with m <= this run in the fused one-workgroup kernel */
+    int32_t small_front_max; /* fronts with m <= this run in the fused one-workgroup kernel (clamped to [0, 128]) */
     int32_t panel_nb;        /* inner panel block (potrf/trsm width), 64 */
     int32_t panel_nb_outer;  /* slab width NBO: rank-NBO outer panel updates at slab ends (default 1024) */
     int32_t use_graph;       /* capture the level schedule into a hipGraph and replay it */
     int32_t relax_wmax;      /* a child and its parent that are both wider than this are not amalgamated when
                                 the parent has other children (chains still merge; 0 = no limit; default 1) */
     int32_t syrk_tile;       /* 0 = auto (128x128/8 waves for wide, deep updates, else 64x64/4 waves); 64; 128 */
-    int32_t lookahead;       /* 1 (default): at a slab end the next slab's columns are updated on the main stream
+    int32_t lookahead;       /* 0 or 1 (other values: SC_ERR_ARG); 1 (default): at a slab end the next slab's columns are updated on the main stream
                                 and every later column on a second stream, overlapping the next slab's
                                 POTRF/TRSM chain; 0: the whole trailing update on the main stream */
-    int32_t inner_order;     /* updates inside a slab: 0 right-looking (K = 64), 1 recursive (K = 64..NBO/2) */
+    int32_t inner_order;     /* updates inside a slab: 0 right-looking (K = 64), 1 recursive (K = 64..NBO/2);
+                                other values: SC_ERR_ARG */
     int32_t asm_tile_min_m;  /* fronts with m >= this use the write-once tiled assembly (0 = default 8192) */
     int32_t dist_split;      /* multi-GPU: a shared front with a contribution block keeps its panel on one rank and
                                 has its contribution block computed by the other ranks of its group, slab-streamed
@@ -111,13 +112,6 @@ typedef struct sc_options {
     int32_t dist_pieces;     /* multi-GPU distributed panels: each final slab is handed over in this many column
                                 pieces (default 4: 256 of a 1024-column slab), each sent as soon as the chain has
                                 finished it, so the next slab's owner starts updating before the slab is done */
-    int32_t panel_psk;       /* 1: the 64-column POTRF / TRSM / inner-update chain of each 1024-column slab of the
-                                large fronts runs as ONE persistent launch per slab and level (all fronts of the
-                                level; one workgroup per psk_rows rows, steps ordered by device-scope flags)
-                                instead of two launches per 64-column step; 0: per-step launches */
-    int32_t psk_rows;        /* rows per persistent-slab workgroup: 64, 128 or 256 (default 64) */
-    int32_t psk_min_w;       /* a level runs its slabs persistently only when its widest large front is at least
-                                this wide (default 0: every level with large fronts) */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

@@ -32,12 +32,6 @@ int64_t sc_debug_solve_eager(sc_numeric* num, int32_t eager);
 /* Chain launches (runs of single small-front levels): enable = 1 makes the next
  * eager factorizations record 8 shader-clock stamps per chained front (phase
  * boundaries); enable = 0 copies up to cap of them to out.  Returns the count. */
-/* Persistent slab chains (panel_psk): enable = 1 allocates a stamp buffer that the next
- * eager factorizations fill (per workgroup 49 s_memrealtime stamps: start, then per step
- * L11 ready / TRSM done / update done); enable = 0 copies up to cap stamps to out and 8
- * ints per workgroup to info (launch sequence, level, front, row block, slab start / end,
- * front rows, row-block height).  Returns the workgroup count. */
-int64_t sc_debug_psk_stamps(sc_numeric* num, int32_t enable, int32_t* info, uint64_t* out, int64_t cap);
 int64_t sc_debug_chain_stamps(sc_numeric* num, int32_t enable, uint64_t* out, int64_t cap);
 /* Microbenchmarks: which=0 register-only fp64 MFMA probe (TFLOP/s; M blocks of
  * 4 waves, K iterations, arg accumulators); which=1/5 the SYRK kernel on an M x M

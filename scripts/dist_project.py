@@ -170,7 +170,7 @@ def critical_path(symb, n, timelines, link_gbs, msg_us, explain=False):
     return finish, explain_chain(symb, n, timelines, events, finish)
 
 
-KIND_NAMES = {0: "small", 1: "asm", 2: "potrf", 3: "trsm", 4: "panel", 5: "cb", 6: "comm", 7: "psk"}
+KIND_NAMES = {0: "small", 1: "asm", 2: "potrf", 3: "trsm", 4: "panel", 5: "cb", 6: "comm"}
 
 
 def explain_chain(symb, n, timelines, events, finish):

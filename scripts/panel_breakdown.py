@@ -23,7 +23,7 @@ for _ in range(2):
     assert num.factor_device(d.data_ptr(), sync=True) == 0
 t = num.launch_trace()
 lt = num.level_times()
-names = {0: "small", 1: "asm", 2: "potrf", 3: "trsm", 4: "panel", 5: "cb", 6: "comm", 7: "psk"}
+names = {0: "small", 1: "asm", 2: "potrf", 3: "trsm", 4: "panel", 5: "cb", 6: "comm"}
 agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
 for kind, lev, st, ms, fl in zip(t["kind"], t["level"], t["stream"], t["ms"], t["flops"]):
     key = (int(lev), names.get(int(kind), str(kind)), int(st))

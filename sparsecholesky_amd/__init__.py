@@ -74,8 +74,7 @@ class Options(C.Structure):
         ("dist_slab_block", C.c_int32), ("trsm_split_wg", C.c_int32),
         ("syrk_lean_kmax", C.c_int32), ("cb_tail_split", C.c_int32), ("tiny_dense", C.c_int32),
         ("dist_asm", C.c_int32),
-        ("dist_pieces", C.c_int32), ("panel_psk", C.c_int32), ("psk_rows", C.c_int32),
-        ("psk_min_w", C.c_int32),
+        ("dist_pieces", C.c_int32),
     ]
 
 
@@ -155,7 +154,6 @@ _SIGS = [
     ("sc_debug_bench", _I64, [_I32, _I32, _I32, _I32, _I32, C.POINTER(_D)]),
     ("sc_device_count", _I64, []),
     ("sc_debug_chain_stamps", _I64, [_P, _I32, _P, _I64]),
-    ("sc_debug_psk_stamps", _I64, [_P, _I32, _P, _P, _I64]),
     ("sc_debug_time_factor", _I64, [_P, C.c_void_p, _I32, C.POINTER(_D)]),
     ("sc_debug_solve_eager", _I64, [_P, _I32]),
     ("sc_debug_hwid", _I64, [_I32, _I32, _I32, _P]),

@@ -95,9 +95,6 @@ void sc_default_options(sc_options* opt) {
     opt->tiny_dense = 1;
     opt->dist_asm = 1;
     opt->dist_pieces = 4;
-    opt->panel_psk = 0;
-    opt->psk_rows = 64;
-    opt->psk_min_w = 0;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,
@@ -117,8 +114,14 @@ int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_opt
     }
     if (o.small_front_max > 128) o.small_front_max = 128;
     if (o.small_front_max < 0) o.small_front_max = 0;
-    if (o.lookahead != 0) o.lookahead = 1;
-    if (o.psk_rows != 128 && o.psk_rows != 256) o.psk_rows = 64;
+    if (o.lookahead != 0 && o.lookahead != 1) {
+        g_last_error = "sc_options.lookahead must be 0 or 1";
+        return SC_ERR_ARG;
+    }
+    if (o.inner_order != 0 && o.inner_order != 1) {
+        g_last_error = "sc_options.inner_order must be 0 or 1";
+        return SC_ERR_ARG;
+    }
     sc_symbolic* h = new (std::nothrow) sc_symbolic();
     if (!h) return SC_ERR_NOMEM;
     std::string err;
@@ -346,11 +349,6 @@ int64_t sc_numeric_syrk_bytes(sc_numeric* num, int32_t wmin, double* bytes) {
 int64_t sc_debug_chain_stamps(sc_numeric* num, int32_t enable, uint64_t* out, int64_t cap) {
     if (!num || !num->N) return SC_ERR_ARG;
     return sc::numeric_chain_stamps(*num->N, enable, out, cap);
-}
-
-int64_t sc_debug_psk_stamps(sc_numeric* num, int32_t enable, int32_t* info, uint64_t* out, int64_t cap) {
-    if (!num || !num->N) return SC_ERR_ARG;
-    return sc::numeric_psk_stamps(*num->N, enable, info, out, cap);
 }
 
 void sc_free_numeric(sc_numeric* num) {

@@ -1621,231 +1621,6 @@ __global__ __launch_bounds__(64 * WM * WN, LEAN ? (TAG ? 5 : 6) : 1) void syrk_m
 }
 
 // ---------------------------------------------------------------------------
-// Persistent slab chain (PSK): the 64-column chain of one slab [s0, s1) of every large
-// front of a level in ONE launch (the reference's dpotrf_ / cblas_dtrsm / cblas_dsyrk of
-// a supernode panel, chol.hpp:1263-1322, restated per 64-column step).  The per-step
-// launches (fused POTRF + TRSM, then the recursive inner update) cost two kernel
-// boundaries per step, and under a concurrent trailing update each waits for dispatch
-// slots.  Here one workgroup owns TR rows of the slab's rows [s0, m) for
-// the whole slab and walks the steps itself:
-//   step j (columns [c, c + 64)):
-//     the OWNER of the diagonal block (its rows hold row c) factors it in registers
-//       (small_steps1_fast), stores L11, publishes flag L11 = j + 1;
-//     every other workgroup waits for that flag and streams L11 from memory;
-//     TRSM of the workgroup's rows below the block (trsm64_full, one lane per row);
-//     a workgroup whose rows lie in the slab's diagonal region publishes its step;
-//     the inner update of its own rows (recursive order: block j closes a run of
-//       2^t blocks, which updates the next 2^t blocks; K = 64 * 2^t), after waiting
-//       for the diagonal-region row blocks the update reads (always lower row blocks).
-// Every wait is on a lower row block of the same front, and the grid is row-block-major,
-// so the launch completes whatever residency it gets.  Hand-offs: plain stores ->
-// s_waitcnt vmcnt(0) -> barrier -> agent release -> relaxed flag store; consumer:
-// relaxed poll -> agent acquire -> barrier (MI355X_MICROARCH.md, inter-workgroup
-// visibility).  Same arithmetic in the same order as the per-step launches: the
-// factor is bitwise identical.
-constexpr uint64_t PSK_TIMEOUT = 400000000ull;  // 4 s of the 100 MHz clock: a lost flag ends the wait
-
-__device__ __forceinline__ void psk_signal(int32_t* flag, int32_t value) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// lane 0 only: true once *flag >= target, false on timeout
-__device__ __forceinline__ bool psk_poll(const int32_t* flag, int32_t target, uint64_t t0) {
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(1);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > PSK_TIMEOUT) return false;
-    }
-    return true;
-}
-
-template <int TR>
-__global__ __launch_bounds__(256, 2) void psk_kernel(DevPlan P, PskArgs A) {
-    static_assert(TR == 64 || TR == 128 || TR == 256, "row blocks of 64, 128 or 256 rows");
-    constexpr int BT = 64, WM = 2, WN = 2, BK = 16, LDT = BT + 16;
-    constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
-    __shared__ double2 S[TRSM64_STREAM / 2];
-    __shared__ __attribute__((aligned(16))) double colbuf[2 * 4 * COLB];
-    __shared__ double smem[2 * 2 * BK * LDT];
-    __shared__ int s_fail;
-    const PskWg g = A.wg[blockIdx.x];
-    const PskFront F = A.fr[g.f];
-    const int s = F.s, m = F.m;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wr = wid / WN, wc = wid % WN;
-    const int cg = P.sn_start[s];  // global column of front column 0
-    double* pan = P.panel_pool + P.panel_off[s];
-    int32_t* fl = A.flags + F.flag0;
-    const int r0 = F.s0 + g.rb * TR, r1 = min(m, r0 + TR);
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    double* Sd = reinterpret_cast<double*>(S);
-    if (tid == 0) s_fail = 0;
-    uint64_t* stamp = A.stamps ? A.stamps + (int64_t)blockIdx.x * PSK_STAMPS : nullptr;
-    auto mark = [&](int q) {
-        if (stamp && tid == 0 && q < PSK_STAMPS) stamp[q] = __builtin_amdgcn_s_memrealtime();
-    };
-    mark(0);
-    // lane 0 waits for every flag of fl[idx[0..n)] >= target, then acquires
-    auto wait_flags = [&](int lo, int hi, int target, bool l11) {
-        if (tid == 0) {
-            bool ok = true;
-            if (l11) ok = psk_poll(fl, target, t0);
-            for (int q = lo; ok && q < hi; ++q)
-                if (q != g.rb) ok = psk_poll(fl + 1 + q, target, t0);
-            if (!ok && !s_fail) {
-                s_fail = 1;
-                report_fail(P.info, cg + F.s0);  // a lost hand-off surfaces as a failed factorization
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-    };
-    for (int j = 0; j < F.nfull; ++j) {
-        const int c = F.s0 + PNB * j, k1 = c + PNB;
-        if (r1 <= c) break;  // every row of this workgroup lies above column c
-        double* blk = pan + (int64_t)c * m + c;
-        if (r0 <= c) {  // owner of the diagonal block: factor it in registers
-            SmallRegs<1> R;
-            small_tiles<1>(R, PNB, PNB);
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int cc = 0; cc < 4; ++cc) {
-                    const int i = 4 * R.bi[0] + r, jj = 4 * R.bj[0] + cc;
-                    R.v[0][r * 4 + cc] = (R.bi[0] >= 0 && i >= jj) ? blk[(int64_t)jj * m + i] : 0.0;
-                }
-            small_steps1_fast(R, colbuf, PNB, P.info, cg + c);
-            if (R.bi[0] >= 0) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int cc = 0; cc < 4; ++cc) {
-                        const int i = 4 * R.bi[0] + r, jj = 4 * R.bj[0] + cc;
-                        if (i >= jj) {
-                            const double v = R.v[0][r * 4 + cc];
-                            blk[(int64_t)jj * m + i] = v;
-                            Sd[PNB * jj - jj * (jj - 1) / 2 + (i - jj)] = (i == jj) ? 1.0 / v : v;
-                        }
-                    }
-            }
-            psk_signal(fl, j + 1);
-            mark(1 + 3 * j);
-        } else {  // wait for L11, stream it from memory (lanes along rows: coalesced)
-            wait_flags(0, 0, j + 1, true);
-            mark(1 + 3 * j);
-#pragma unroll 4
-            for (int q = 0; q < PNB * PNB / 256; ++q) {
-                const int e = tid + 256 * q, jj = e >> 6, i = e & 63;
-                if (i >= jj) {
-                    const double v = blk[(int64_t)jj * m + i];
-                    Sd[PNB * jj - jj * (jj - 1) / 2 + (i - jj)] = (i == jj) ? 1.0 / v : v;
-                }
-            }
-        }
-        // TRSM of this workgroup's rows below the block: one lane per row
-        if (max(r0, k1) < r1) {
-            const int row = r0 + tid;
-            const bool live = tid < TR && row >= k1 && row < r1;
-            const __amdgpu_buffer_rsrc_t rs = buf_rsrc(pan + (int64_t)c * m, (uint32_t)m * PNB * 8u);
-            const int voff = live ? row * 8 : BUF_DEAD;
-            __syncthreads();  // the L11 stream is complete
-            if (tid < TR) {
-                double r[PNB];
-#pragma unroll
-                for (int q = 0; q < PNB; ++q) r[q] = buf_ld(rs, voff, q * m * 8);
-                trsm64_full(r, S);
-#pragma unroll
-                for (int q = 0; q < PNB; ++q) buf_st(r[q], rs, voff, q * m * 8);
-            }
-            // rows of the slab's diagonal region feed other row blocks' inner updates
-            if (r0 < F.s1) psk_signal(fl + 1 + g.rb, j + 1);
-        }
-        mark(2 + 3 * j);
-        __syncthreads();  // the stream S is read by every TRSM lane before the next step rebuilds it
-        if (k1 >= F.s1) continue;
-        // inner update of this workgroup's rows: columns [k1, cend), K = [ka, k1)
-        int ka, cend;
-        if (F.inner) {
-            const int span = PNB << __builtin_ctz((unsigned)(j + 1));
-            ka = k1 - span;
-            cend = min(F.s1, k1 + span);
-        } else {
-            ka = c;
-            cend = F.s1;
-        }
-        const int cc1 = min(cend, r1);  // columns past the workgroup's last row are above the diagonal
-        if (max(r0, k1) >= r1 || k1 >= cc1) continue;
-        // B operand: rows [k1, cc1) at columns [ka, k1), final in the row blocks holding them
-        wait_flags((k1 - F.s0) / TR, (cc1 - 1 - F.s0) / TR + 1, j + 1, false);
-        const int K = k1 - ka;
-#pragma unroll 1
-        for (int ct = k1; ct < cc1; ct += BT) {
-#pragma unroll 1
-            for (int rt = r0; rt < r1; rt += BT) {
-                if (rt + BT <= ct) continue;  // entirely above the diagonal
-                double4_t acc[RTM][RTN];
-#pragma unroll
-                for (int a = 0; a < RTM; ++a)
-#pragma unroll
-                    for (int b = 0; b < RTN; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
-                mfma_kloop<BT, WM, WN, BK>(pan + (int64_t)ka * m, m, K, r1, cend, rt, ct, acc, smem);
-                // C(i, jj) -= acc, i >= jj, i < r1, jj < cend: every load of a chunk before its stores
-                const __amdgpu_buffer_rsrc_t rc = buf_rsrc(pan + (int64_t)ct * m, (uint32_t)(min(BT, cend - ct) * m * 8));
-                double cv[RTM][RTN][4];
-                int offs[RTM][RTN][4];
-#pragma unroll
-                for (int a = 0; a < RTM; ++a)
-#pragma unroll
-                    for (int b = 0; b < RTN; ++b)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int gi = rt + wr * (BT / WM) + a * 16 + MFMA_F64_ROW(lane, r);
-                            const int gj = ct + wc * (BT / WN) + b * 16 + (lane & 15);
-                            const bool live = gi < r1 && gi >= gj;
-                            offs[a][b][r] = live ? (int)((gi + (int64_t)(gj - ct) * m) * 8) : BUF_DEAD;
-                            cv[a][b][r] = buf_ld(rc, offs[a][b][r], 0);
-                        }
-#pragma unroll
-                for (int a = 0; a < RTM; ++a)
-#pragma unroll
-                    for (int b = 0; b < RTN; ++b)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) buf_st(cv[a][b][r] - acc[a][b][r], rc, offs[a][b][r], 0);
-            }
-        }
-        // this workgroup's own C stores are read back by its next steps (same CU): drain them
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        mark(3 + 3 * j);
-    }
-    // the last workgroup to finish re-arms the launch's flags (graph-replay safe)
-    __syncthreads();
-    if (tid == 0) {
-        const int old = __hip_atomic_fetch_add(A.flags + A.nflags, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == A.nwg - 1) {
-            for (int q = 0; q <= A.nflags; ++q) __hip_atomic_store(A.flags + q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
-hipError_t launch_psk(const DevPlan& P, const PskArgs& A, int rows, hipStream_t st) {
-    if (A.nwg <= 0) return hipSuccess;
-    if (rows == 256)
-        hipLaunchKernelGGL(psk_kernel<256>, dim3(A.nwg), dim3(256), 0, st, P, A);
-    else if (rows == 128)
-        hipLaunchKernelGGL(psk_kernel<128>, dim3(A.nwg), dim3(256), 0, st, P, A);
-    else
-        hipLaunchKernelGGL(psk_kernel<64>, dim3(A.nwg), dim3(256), 0, st, P, A);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
 // Launch wrappers
 // ---------------------------------------------------------------------------
 // KT: 4 x 4 register tiles per thread for fronts up to maxm (ceil(tiles / 256))
@@ -2234,7 +2009,43 @@ __global__ __launch_bounds__(SOLVE_ROWS) void solve_fwd_kernel(SolvePlan P, cons
 #pragma unroll
         for (int q = 0; q < PNB; ++q) acc = fma(v[q], vb[PNB + q], acc);
     }
-    if (live) unsafeAtomicAdd(P.c + rows[r], -acc);
+    // rows < w: this front's own later pivots (no other front of the level has them);
+    // rows >= w: its contribution block's entry of u, gathered by the parent in child order
+    if (live) {
+        if (r < w)
+            P.c[rows[r]] -= acc;
+        else
+            P.u[P.u_off[s] + (r - w)] -= acc;
+    }
+}
+
+// Forward gather (deterministic extend-add of the solve): front s = fronts[blockIdx.x]
+// takes its children's u in child order; an entry mapping to one of s's pivot rows goes
+// to c, the rest to u of s (zeroed by the sweep's memset).  Within a child relind is
+// injective, so a barrier per child orders the adds.
+__global__ __launch_bounds__(256) void solve_fwd_gather_kernel(SolvePlan P, const int32_t* __restrict__ fronts) {
+    const int s = fronts[blockIdx.x];
+    const int tid = threadIdx.x;
+    const int c0 = P.sn_start[s];
+    const int w = P.sn_start[s + 1] - c0;
+    const int32_t* __restrict__ rows = P.rows + P.rows_ptr[s];
+    double* __restrict__ us = P.u + P.u_off[s];
+    for (int q = P.child_ptr[s]; q < P.child_ptr[s + 1]; ++q) {
+        const int ch = P.child_list[q];
+        const int64_t r0 = P.rel_ptr[ch];
+        const int mbc = (int)(P.rel_ptr[ch + 1] - r0);
+        const double* __restrict__ uc = P.u + P.u_off[ch];
+        const int32_t* __restrict__ rel = P.relind + r0;
+        __syncthreads();  // the previous child's adds are done
+        for (int i = tid; i < mbc; i += 256) {
+            const int t = rel[i];
+            const double v = uc[i];
+            if (t < w)
+                P.c[rows[t]] += v;
+            else
+                us[t - w] += v;
+        }
+    }
 }
 
 // Backward step, part 1: workgroup (s, k0, r0) adds -L(rows, blk)^T x(rows) into
@@ -2276,18 +2087,19 @@ __global__ __launch_bounds__(SOLVE_ROWS) void solve_gemv_kernel(SolvePlan P, con
         for (int q = 0; q < SOLVE_ROWS / 4; ++q) acc += T[j][g * (SOLVE_ROWS / 4) + q];
         part[g][j] = acc;
         __syncthreads();
-        if (tid < PNB && h * PNB + tid < nb)
-            unsafeAtomicAdd(P.c + c0 + k0 + h * PNB + tid, -(part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid]));
+        if (tid < PNB)  // this workgroup's partial, summed by the diagonal kernel in task order
+            P.part[(int64_t)blockIdx.x * SOLVE_NB + h * PNB + tid] =
+                -(part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid]);
     }
 }
 
 // Backward step, part 2: x_blk = X128^T c_blk for every block (s, k0) of the step:
 // thread (column k = tid & 127, half g) sums X128(i, k) c_i over i in its half
 // (X128(i, k) at row k, column i of the block: lanes along k read coalesced).
-__global__ __launch_bounds__(256) void solve_diag_kernel(SolvePlan P, const int2* __restrict__ tasks) {
+__global__ __launch_bounds__(256) void solve_diag_kernel(SolvePlan P, const int4* __restrict__ tasks) {
     __shared__ double cb[SOLVE_NB];
     __shared__ double part[2][SOLVE_NB];
-    const int2 t = tasks[blockIdx.x];
+    const int4 t = tasks[blockIdx.x];
     const int s = t.x, k0 = t.y;
     const int tid = threadIdx.x, k = tid & (SOLVE_NB - 1), g = tid >> 7;
     const int c0 = P.sn_start[s];
@@ -2295,7 +2107,11 @@ __global__ __launch_bounds__(256) void solve_diag_kernel(SolvePlan P, const int2
     const int m = P.sn_m[s];
     const int nb = min(SOLVE_NB, w - k0);
     const double* __restrict__ blk = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m + k0;
-    if (tid < SOLVE_NB) cb[tid] = tid < nb ? P.c[c0 + k0 + tid] : 0.0;
+    if (tid < SOLVE_NB) {
+        double v = tid < nb ? P.c[c0 + k0 + tid] : 0.0;
+        for (int g2 = 0; g2 < t.w; ++g2) v += P.part[(int64_t)(t.z + g2) * SOLVE_NB + tid];  // GEMV partials, in order
+        cb[tid] = v;
+    }
     __syncthreads();
     // branch-free: dead elements read 0 through the buffer's range check, all loads in flight
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(blk, (uint32_t)(((int64_t)(nb - 1) * m + nb) * 8));
@@ -2328,7 +2144,13 @@ hipError_t launch_solve_gemv(const SolvePlan& P, const int4* tasks, int count, h
     return hipGetLastError();
 }
 
-hipError_t launch_solve_diag(const SolvePlan& P, const int2* tasks, int count, hipStream_t st) {
+hipError_t launch_solve_fwd_gather(const SolvePlan& P, const int32_t* fronts, int count, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(solve_fwd_gather_kernel, dim3(count), dim3(256), 0, st, P, fronts);
+    return hipGetLastError();
+}
+
+hipError_t launch_solve_diag(const SolvePlan& P, const int4* tasks, int count, hipStream_t st) {
     if (count <= 0) return hipSuccess;
     hipLaunchKernelGGL(solve_diag_kernel, dim3(count), dim3(256), 0, st, P, tasks);
     return hipGetLastError();

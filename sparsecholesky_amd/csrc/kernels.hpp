@@ -98,6 +98,10 @@ struct Copy2D {
 
 constexpr int COPY_COLS = 16;    // columns per copy workgroup
 constexpr int COPY_ROWS = 2048;  // rows per copy workgroup
+// copy tiles encode (column offset | row chunk << 16): the host cuts wider blocks into
+// descriptors of at most this many columns (schedule.cpp emit_step)
+constexpr int COPY_MAX_COLS = 32768;
+static_assert(COPY_MAX_COLS + COPY_COLS <= 65536, "column offsets fit the tile's 16 low bits");
 // tiles: (descriptor, first column | row chunk << 16) per workgroup
 hipError_t launch_copy2d(const Copy2D* descs, const int2* tiles, int count, bool unpack, hipStream_t st);
 
@@ -111,6 +115,18 @@ struct SolvePlan {
     const double* panel_pool;
     double* c;                // right-hand side / solution, internal numbering
     double* y;                // forward result (fused steps write here; copied to c after the sweep)
+    // deterministic accumulation (no atomics): the forward sweep leaves each front's
+    // updates of its contribution-block rows in u (u + u_off[s], mb entries, multifrontal
+    // style), and the parent's gather (solve_fwd_gather_kernel) adds its children's u in
+    // child order; the backward GEMV leaves one partial column sum per workgroup in part
+    // (SOLVE_NB per task of the launch), summed in task order by the diagonal kernel
+    double* u;
+    const int64_t* u_off;     // per supernode
+    const int32_t* child_ptr; // ns+1
+    const int32_t* child_list;
+    const int64_t* rel_ptr;   // ns+1: child c's CB rows -> parent front rows
+    const int32_t* relind;
+    double* part;
 };
 constexpr int SOLVE_ROWS = 256;  // front rows per GEMV workgroup
 constexpr int SOLVE_NB = 128;    // columns per solve step (two 64-blocks)
@@ -121,13 +137,18 @@ constexpr int SOLVE_NB = 128;    // columns per solve step (two 64-blocks)
 hipError_t launch_solve_inv(const SolvePlan& P, const int2* tasks, int count, const int2* tasks2, int count2,
                             hipStream_t st);
 // Forward step: tasks (s, k0, r0, writer) of 128-column blocks; every workgroup forms
-// y = X128 c_blk and applies c[rows[r]] -= L[r, blk] y for its SOLVE_ROWS rows (fp64
-// atomics: fronts of a level share ancestors); r0 < 0 = the diagonal block only.
+// y = X128 c_blk and applies -L[r, blk] y for its SOLVE_ROWS rows: to c for the front's
+// own later pivot rows, to u for its contribution-block rows (no atomics: each row has
+// one writer per step); r0 < 0 = the diagonal block only.
 hipError_t launch_solve_fwd(const SolvePlan& P, const int4* tasks, int count, hipStream_t st);
-// Backward step: tasks (s, k0, r0): c_blk -= L[rows, blk]^T x[rows] (fp64 atomics),
-// then tasks (s, k0): x_blk = X128^T c_blk.
+// Forward gather, before a level's first step: per front s of the list, its children's
+// u in child order -- entries at s's pivot rows into c, the rest into u of s.
+hipError_t launch_solve_fwd_gather(const SolvePlan& P, const int32_t* fronts, int count, hipStream_t st);
+// Backward step: tasks (s, k0, r0): partial -L[rows, blk]^T x[rows] per workgroup into
+// part, then tasks (s, k0, g0, ng): c_blk plus the block's ng partials (launch-relative
+// GEMV tasks g0..) in order, x_blk = X128^T c_blk.
 hipError_t launch_solve_gemv(const SolvePlan& P, const int4* tasks, int count, hipStream_t st);
-hipError_t launch_solve_diag(const SolvePlan& P, const int2* tasks, int count, hipStream_t st);
+hipError_t launch_solve_diag(const SolvePlan& P, const int4* tasks, int count, hipStream_t st);
 // c[i] = b[perm[i]] (gather) or x[perm[i]] = c[i] (scatter)
 hipError_t launch_permute(double* dst, const double* src, const int32_t* perm, int64_t n, bool scatter,
                           hipStream_t st);
@@ -216,33 +237,6 @@ struct TrsmTask {
 // (trsm_split_wg)
 hipError_t launch_trsm_panel(const DevPlan& P, const TrsmTask* tasks, int count, hipStream_t st, bool partial,
                              int32_t* arrive, int pre = 0);
-// Persistent slab chain (PSK, kernels.hip psk_kernel): the 64-column POTRF / TRSM /
-// inner-update chain of one 1024-column slab [s0, s1) of every large front of a level,
-// as one launch.  One workgroup per `rows`-row block of the slab's rows [s0, m); the
-// steps are ordered by device-scope flags (flags[flag0]: the front's factored diagonal
-// blocks; flags[flag0 + 1 + rb]: steps whose TRSM row block rb of the diagonal region
-// has finished), re-armed by the last workgroup.  nfull: full 64-column blocks (a
-// partial last block is factored by the per-step launches after it).  inner: the
-// inner update order (sc_options.inner_order).
-struct PskFront {
-    int32_t s, s0, s1, nfull;
-    int32_t m, flag0, inner, pad;
-};
-struct PskWg {
-    int32_t f, rb;
-};
-struct PskArgs {
-    const PskFront* fr;
-    const PskWg* wg;
-    int32_t* flags;   // this launch's flags; flags[nflags] = its done counter
-    int32_t nflags, nwg;
-    uint64_t* stamps = nullptr;  // debug (sc_debug_psk_stamps): PSK_STAMPS per workgroup, or null
-};
-// debug stamps per workgroup: [0] start, then per step j: L11 ready, TRSM done, update done
-// (s_memrealtime, 100 MHz), at 1 + 3 j
-constexpr int PSK_STAMPS = 1 + 3 * 16;
-hipError_t launch_psk(const DevPlan& P, const PskArgs& A, int rows, hipStream_t st);
-
 // gt: the gather tables (CB tasks with gs >= 0 gather their children's entries)
 // lean: 64 x 64 tiles with half the LDS (BK = 8; short-K launches, syrk_lean_kmax)
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,

@@ -266,12 +266,8 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
     if ((rc = upload(N, B.small, N.d_small)) || (rc = upload(N, B.asmv, N.d_asm)) || (rc = upload(N, B.asml, N.d_asml)) ||
         (rc = upload(N, B.potrf, N.d_potrf)) || (rc = upload(N, B.trsm, N.d_trsm)) ||
         (rc = upload(N, std::vector<int32_t>(B.trsm.size() + 1, 0), N.d_arrive)) ||
-        (rc = upload(N, B.gemm, N.d_gemm)) || (rc = upload(N, B.tiles, N.d_tiles)) ||
-        (rc = upload(N, B.pskf, N.d_pskf)) || (rc = upload(N, B.pskw, N.d_pskw)) ||
-        (rc = upload(N, std::vector<int32_t>((size_t)B.psk_flags + 1, 0), N.d_pskflags)))
+        (rc = upload(N, B.gemm, N.d_gemm)) || (rc = upload(N, B.tiles, N.d_tiles)))
         return fail(rc);
-    N.h_pskf = B.pskf;
-    N.h_pskw = B.pskw;
     (void)ns;
     return SC_OK;
 }
@@ -308,11 +304,6 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
                                N.gtab, L.lean != 0);
         case L_COMM:
             return comm_launch(N, L);
-        case L_PSK: {
-            PskArgs A {N.d_pskf + L.off, N.d_pskw + L.toff, N.d_pskflags + L.foff, L.fcount, L.count,
-                       N.d_pskstamps ? N.d_pskstamps + L.toff * PSK_STAMPS : nullptr};
-            return launch_psk(N.R[L.vr].P, A, N.S->opt.psk_rows, st);
-        }
     }
     return hipErrorInvalidValue;
 }
@@ -455,8 +446,7 @@ int64_t numeric_status(Numeric& N) {
                 case L_SMALL: slot = 2; break;
                 case L_ASM: slot = 3; break;
                 case L_POTRF: slot = 4; break;
-                case L_TRSM:
-                case L_PSK: slot = 5; break;
+                case L_TRSM: slot = 5; break;
                 case L_PANEL: slot = 6; break;
                 case L_CB: slot = 7; break;
                 case L_COMM: slot = 1; break;
@@ -632,50 +622,6 @@ int64_t numeric_chain_stamps(Numeric& N, int enable, uint64_t* out, int64_t cap)
     if (out && cap > 0)
         HIP_TRY(hipMemcpy(out, N.CP.stamps, (size_t)std::min(cap, cnt) * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return cnt;
-}
-
-// Debug: per persistent-slab workgroup its stamps (PSK_STAMPS each, kernels.hpp) and,
-// in info (8 per workgroup), the launch's sequence number, level, the front, its row
-// block, the slab [s0, s1), the front's rows and the row-block height.  enable = 1
-// allocates the stamp buffer (eager factorizations after this record into it).
-int64_t numeric_psk_stamps(Numeric& N, int enable, int32_t* info, uint64_t* out, int64_t cap) {
-    const int64_t nwg = (int64_t)N.h_pskw.size();
-    if (enable) {
-        if (!N.d_pskstamps && nwg > 0) {
-            void* p = nullptr;
-            TRY(dalloc(N, (size_t)nwg * PSK_STAMPS * sizeof(uint64_t), p));
-            N.d_pskstamps = (uint64_t*)p;
-            HIP_TRY(hipMemset(p, 0, (size_t)nwg * PSK_STAMPS * sizeof(uint64_t)));
-        }
-        return nwg;
-    }
-    if (!N.d_pskstamps) return 0;
-    HIP_TRY(hipStreamSynchronize(N.stream));
-    if (out && cap > 0)
-        HIP_TRY(hipMemcpy(out, N.d_pskstamps, (size_t)std::min(cap, nwg * PSK_STAMPS) * sizeof(uint64_t),
-                          hipMemcpyDeviceToHost));
-    if (info) {
-        int32_t seq = 0;
-        for (const Launch& L : N.sched) {
-            if (L.kind != L_PSK) continue;
-            for (int32_t i = 0; i < L.count; ++i) {
-                const int64_t w = L.toff + i;
-                const PskWg& g = N.h_pskw[w];
-                const PskFront& F = N.h_pskf[L.off + g.f];
-                int32_t* q = info + 8 * w;
-                q[0] = seq;
-                q[1] = L.level;
-                q[2] = F.s;
-                q[3] = g.rb;
-                q[4] = F.s0;
-                q[5] = F.s1;
-                q[6] = F.m;
-                q[7] = N.S->opt.psk_rows;
-            }
-            ++seq;
-        }
-    }
-    return nwg;
 }
 
 }  // namespace sc

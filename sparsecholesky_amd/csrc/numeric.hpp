@@ -19,7 +19,6 @@ enum LaunchKind : int32_t {
     L_PANEL = 4,
     L_CB = 5,
     L_COMM = 6,    // one comm step of the hosted ranks (pack, transfer group, unpack)
-    L_PSK = 7,     // persistent slab chain: a slab's 64-column POTRF / TRSM / inner updates, all fronts of a level
     L_RECORD = 11, // record sync event `count` on stream `strm`
     L_WAIT = 12,   // stream `strm` waits for sync event `count`
     L_KINDS = 13
@@ -174,10 +173,6 @@ struct Launch {
     int64_t poff, uoff;
     int32_t pcount, ucount;
     int32_t step;
-    // L_PSK: fronts [off, off + ntasks) of Numeric::d_pskf, workgroups [toff, toff + count) of
-    // d_pskw, flags [foff, foff + fcount] of d_pskflags (the last one: the done counter)
-    int64_t foff;
-    int32_t fcount;
 };
 
 struct Numeric {
@@ -202,12 +197,6 @@ struct Numeric {
     int2* d_potrf = nullptr;
     TrsmTask* d_trsm = nullptr;
     int32_t* d_arrive = nullptr;  // fused POTRF + TRSM: per-block arrival counters
-    PskFront* d_pskf = nullptr;   // persistent slab chains (L_PSK)
-    PskWg* d_pskw = nullptr;
-    int32_t* d_pskflags = nullptr;
-    std::vector<PskFront> h_pskf;   // host copies (debug stamps)
-    std::vector<PskWg> h_pskw;
-    uint64_t* d_pskstamps = nullptr;  // debug: PSK_STAMPS per workgroup (sc_debug_psk_stamps)
     GemmTask* d_gemm = nullptr;
     int2* d_tiles = nullptr;
     GatherTab gtab;              // the CB SYRK extend-add gather's segment tables (schedule.cpp)
@@ -268,13 +257,15 @@ struct Numeric {
 
     // triangular solves (built at the first solve)
     struct SolveStep {
-        int64_t doff, goff, foff;
-        int32_t dcount, gcount, fcount;
+        int64_t doff, goff, foff, gaoff;
+        int32_t dcount, gcount, fcount, gacount;  // gacount: forward-gather fronts (level's first step)
     };
     std::vector<SolveStep> solve_steps;  // forward order (levels up, k0 up)
     bool solve_ready = false;
     SolvePlan SP {};
-    int2* d_sdiag = nullptr;         // 128-column diagonal blocks (s, k0) of the steps
+    int4* d_sdiag = nullptr;         // 128-column diagonal blocks (s, k0, first GEMV task, GEMV tasks)
+    int32_t* d_sgather = nullptr;    // forward gather: fronts with children, per level
+    int64_t u_total = 0;             // doubles of SP.u (sum of the fronts' mb)
     int2* d_sinv = nullptr;          // 64-column blocks (s, k0): inverse preparation
     int2* d_sinv2 = nullptr;         // 128-column blocks wider than 64: off-diagonal inverse quadrant
     int32_t n_sinv = 0, n_sinv2 = 0;
@@ -320,7 +311,6 @@ int64_t numeric_solve_device(Numeric& N, const double* d_b, double* d_x);
 int64_t numeric_solve_host(Numeric& N, const double* b, double* x);
 int64_t debug_syrk(double* dC, int ldc, const double* dA, int lda, int M, int N, int K);
 int64_t numeric_chain_stamps(Numeric& N, int enable, uint64_t* out, int64_t cap);
-int64_t numeric_psk_stamps(Numeric& N, int enable, int32_t* info, uint64_t* out, int64_t cap);
 int64_t debug_bench(int which, int M, int K, int reps, int arg, double* tflops);
 int64_t debug_contention(int M, int K, int chain_rows, int nchain, int mode, int mask_stride, double* out);
 

@@ -82,9 +82,6 @@ struct SchedBuild {
     std::vector<int2> asmv, potrf;
     std::vector<int2> asml;  // parallel to asmv: owned front columns [x, y) of a task
     std::vector<TrsmTask> trsm;
-    std::vector<PskFront> pskf;  // persistent slab chains
-    std::vector<PskWg> pskw;
-    int64_t psk_flags = 0;
     std::vector<GemmTask> gemm;
     std::vector<int2> tiles;
     std::vector<int64_t> gblk;  // CB gather: per task, per 64 x 64 CB block, its first segment

@@ -286,14 +286,23 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             }
             buf = nullptr;
             slot = cbld.stage_total;
-            Copy2D c {};
-            c.a = a;
-            c.lda = ld;
-            c.rows = rows;
-            c.cols = cols;
-            (pack ? pack_d : unpack_d).push_back((int32_t)cbld.copies.size());
-            cbld.copies.push_back(c);
-            cbld.copy_slot.push_back(slot);
+            // copy tiles pack the column offset in 16 bits and the row chunk above it
+            // (j | rc << 16, copy2d_kernel): a block wider than COPY_MAX_COLS goes as several
+            // descriptors, each staging its columns at their packed position in the slot
+            if ((int64_t)rows > (int64_t)COPY_ROWS * 32767) {
+                N.err = "comm plan: block too tall for the copy tiles";
+                return false;
+            }
+            for (int c0 = 0; c0 < cols; c0 += COPY_MAX_COLS) {
+                Copy2D c {};
+                c.a = a + (int64_t)c0 * ld;
+                c.lda = ld;
+                c.rows = rows;
+                c.cols = std::min(COPY_MAX_COLS, cols - c0);
+                (pack ? pack_d : unpack_d).push_back((int32_t)cbld.copies.size());
+                cbld.copies.push_back(c);
+                cbld.copy_slot.push_back(slot + (int64_t)c0 * rows);
+            }
             cbld.stage_total += (int64_t)rows * cols;
             return true;
         };
@@ -568,116 +577,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             vec.push_back(t);
             fl += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
         };
-        // persistent slab chains (panel_psk): per slab one L_PSK launch for the level's
-        // fronts (the 64-column steps inside it), then the partial last blocks, then the
-        // slab-end outer updates exactly as the per-step schedule below emits them
-        const bool psk = S.opt.panel_psk && maxw >= S.opt.psk_min_w;
-        auto outer_updates = [&](int s0) {
-            std::vector<GemmTask> outer_a, outer_b;
-            double afl = 0.0, bfl = 0.0;
-            for (int32_t s : large) {
-                const int w = S.w(s), m = S.sn_m[s];
-                const int slab1 = std::min(w, s0 + NBO);
-                if (w <= s0 || slab1 >= w) continue;
-                double* pan = panel_pool + poff[s];
-                const int nxt = S.opt.lookahead ? std::min(w, slab1 + NBO) : w;
-                add_update(outer_a, afl, pan, m, m, slab1, nxt, s0, slab1);
-                add_update(outer_b, bfl, pan, m, m, nxt, w, s0, slab1);
-            }
-            int e_trsm = -1;
-            if (!outer_b.empty()) e_trsm = push_record(0);
-            if (!outer_a.empty()) {
-                if (b_pending >= 0) {
-                    push_wait(0, b_pending);
-                    b_pending = -1;
-                }
-                push_gemm_launch(L_PANEL, lev, outer_a, 0, afl);
-            }
-            if (!outer_b.empty()) {
-                push_wait(1, e_trsm);
-                push_gemm_launch(L_PANEL, lev, outer_b, 0, bfl, 1);
-                b_pending = push_record(1);
-            }
-        };
-        for (int s0 = 0; psk && s0 < maxw; s0 += NBO) {
-            const int TR = S.opt.psk_rows;
-            Launch Lk {};
-            Lk.kind = L_PSK;
-            Lk.level = lev;
-            Lk.vr = v;
-            Lk.off = (int64_t)B.pskf.size();
-            Lk.toff = (int64_t)B.pskw.size();
-            Lk.foff = B.psk_flags;
-            std::vector<int> nrb;
-            double fl = 0.0;
-            for (int32_t s : large) {
-                const int w = S.w(s), m = S.sn_m[s];
-                if (w <= s0) continue;
-                const int slab1 = std::min(w, s0 + NBO), nfull = (slab1 - s0) / PNB;
-                if (nfull == 0) continue;
-                PskFront f {};
-                f.s = s;
-                f.s0 = s0;
-                f.s1 = slab1;
-                f.nfull = nfull;
-                f.m = m;
-                f.flag0 = (int32_t)(B.psk_flags - Lk.foff);
-                f.inner = S.opt.inner_order;
-                B.psk_flags += 1 + (slab1 - s0 + TR - 1) / TR;
-                B.pskf.push_back(f);
-                nrb.push_back((m - s0 + TR - 1) / TR);
-                for (int j = 0; j < nfull; ++j) {  // the inner updates' flops (as add_update counts them)
-                    const int k1 = s0 + PNB * (j + 1);
-                    if (k1 >= slab1) break;
-                    const int span = S.opt.inner_order ? PNB << __builtin_ctz((unsigned)(j + 1)) : slab1 - k1;
-                    const int K = S.opt.inner_order ? span : PNB;
-                    const double Nn = std::min(slab1, k1 + span) - k1, M = m - k1;
-                    fl += 2.0 * K * (Nn * M - Nn * (Nn - 1) / 2.0);
-                }
-            }
-            const int maxrb = nrb.empty() ? 0 : *std::max_element(nrb.begin(), nrb.end());
-            for (int rb = 0; rb < maxrb; ++rb)  // row-block-major: every wait is on an earlier workgroup
-                for (int fi = 0; fi < (int)nrb.size(); ++fi)
-                    if (rb < nrb[fi]) B.pskw.push_back(PskWg {fi, rb});
-            Lk.ntasks = (int32_t)nrb.size();
-            Lk.count = (int32_t)((int64_t)B.pskw.size() - Lk.toff);
-            Lk.fcount = (int32_t)(B.psk_flags - Lk.foff);
-            Lk.flops = fl;
-            B.psk_flags += 1;  // the launch's done counter
-            if (Lk.count > 0) N.sched.push_back(Lk);
-            // partial last blocks (w not a multiple of 64): their POTRF and the TRSM below
-            Launch Lp {};
-            Lp.kind = L_POTRF;
-            Lp.level = lev;
-            Lp.vr = v;
-            Lp.off = (int64_t)potrf.size();
-            Launch Lq {};
-            Lq.kind = L_TRSM;
-            Lq.level = lev;
-            Lq.vr = v;
-            Lq.big = 1;
-            for (int32_t s : large) {
-                const int w = S.w(s), kp = w - w % PNB;
-                if (w % PNB == 0 || kp < s0 || kp >= s0 + NBO) continue;
-                potrf.push_back(make_int2(s, kp));
-            }
-            Lq.off = (int64_t)trsm.size();
-            for (int32_t s : large) {
-                const int w = S.w(s), m = S.sn_m[s];
-                const int kp = w - w % PNB;
-                if (w % PNB == 0 || kp < s0 || kp >= s0 + NBO) continue;
-                for (int r0 = w; r0 < m; r0 += TRSM_ROWS) trsm.push_back(TrsmTask {s, kp, r0, m, 0});
-            }
-            Lp.count = (int32_t)((int64_t)potrf.size() - Lp.off);
-            Lq.count = (int32_t)((int64_t)trsm.size() - Lq.off);
-            if (Lp.count > 0) N.sched.push_back(Lp);
-            if (Lq.count > 0) N.sched.push_back(Lq);
-            // split fronts: the slab is final
-            for (int32_t s : large)
-                if (is_split(s) && S.w(s) > s0) emit_slab(s, s0 / D.nbo);
-            outer_updates(s0);
-        }
-        for (int k0 = 0; !psk && k0 < maxw; k0 += PNB) {
+        for (int k0 = 0; k0 < maxw; k0 += PNB) {
             Launch Lp {};
             Lp.kind = L_POTRF;
             Lp.level = lev;
@@ -903,57 +803,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 const int e = last_ev1(vk, k - 2);
                 if (e >= 0) push_wait(0, e);
                 double* pan = pan_of(vk);
-                if (S.opt.panel_psk) {  // the slab's chain as one persistent launch, then its pieces
-                    const int TR = S.opt.psk_rows, nfull = (k1s - k0s) / PNB;
-                    if (nfull > 0) {
-                        Launch Lk {};
-                        Lk.kind = L_PSK;
-                        Lk.level = lev;
-                        Lk.vr = vk;
-                        Lk.off = (int64_t)B.pskf.size();
-                        Lk.toff = (int64_t)B.pskw.size();
-                        Lk.foff = B.psk_flags;
-                        PskFront f {};
-                        f.s = s;
-                        f.s0 = k0s;
-                        f.s1 = k1s;
-                        f.nfull = nfull;
-                        f.m = m;
-                        f.flag0 = 0;
-                        f.inner = S.opt.inner_order;
-                        B.pskf.push_back(f);
-                        B.psk_flags += 1 + (k1s - k0s + TR - 1) / TR;
-                        const int nrb = (m - k0s + TR - 1) / TR;
-                        for (int rb = 0; rb < nrb; ++rb) B.pskw.push_back(PskWg {0, rb});
-                        Lk.ntasks = 1;
-                        Lk.count = nrb;
-                        Lk.fcount = (int32_t)(B.psk_flags - Lk.foff);
-                        B.psk_flags += 1;
-                        N.sched.push_back(Lk);
-                    }
-                    if ((k1s - k0s) % PNB) {  // the front's partial last block
-                        const int kp = k0s + nfull * PNB;
-                        Launch Lp {};
-                        Lp.kind = L_POTRF;
-                        Lp.level = lev;
-                        Lp.vr = vk;
-                        Lp.off = (int64_t)potrf.size();
-                        Lp.count = 1;
-                        potrf.push_back(make_int2(s, kp));
-                        N.sched.push_back(Lp);
-                        Launch Lq {};
-                        Lq.kind = L_TRSM;
-                        Lq.level = lev;
-                        Lq.vr = vk;
-                        Lq.big = 1;
-                        Lq.off = (int64_t)trsm.size();
-                        for (int r0 = k1s; r0 < m; r0 += TRSM_ROWS) trsm.push_back(TrsmTask {s, kp, r0, m, 0});
-                        Lq.count = (int32_t)((int64_t)trsm.size() - Lq.off);
-                        if (Lq.count > 0) N.sched.push_back(Lq);
-                    }
-                    for (int p = 0; k0s + p * D.pw < k1s; ++p) emit_step(slab_piece(s, k, p));
-                }
-                for (int k0 = k0s; !S.opt.panel_psk && k0 < k1s; k0 += PNB) {
+                for (int k0 = k0s; k0 < k1s; k0 += PNB) {
                     const int nb = std::min(PNB, k1s - k0), k1 = k0 + nb;
                     Launch Lp {};
                     Lp.kind = L_POTRF;

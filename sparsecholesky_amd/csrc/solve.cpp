@@ -101,8 +101,10 @@ static int64_t solve_build(Numeric& N) {
     const Symbolic& S = *N.S;
     std::vector<std::vector<int32_t>> by_level((size_t)S.nlevels);
     for (int32_t s = 0; s < S.ns; ++s) by_level[S.level[s]].push_back(s);
-    std::vector<int2> diag, inv64, inv128;
-    std::vector<int4> bwd, fwd;
+    std::vector<int2> inv64, inv128;
+    std::vector<int4> diag, bwd, fwd;
+    std::vector<int32_t> gather;  // per level: the fronts with children (forward gather)
+    int64_t max_g = 1;            // most GEMV workgroups in one backward step
     // internal index -> index in the caller's order (postorder, then the fill-reducing
     // permutation when one is in effect)
     std::vector<int32_t> solve_perm(S.post);
@@ -111,15 +113,22 @@ static int64_t solve_build(Numeric& N) {
     for (int32_t lev = 0; lev < S.nlevels; ++lev) {
         int maxw = 0;
         for (int32_t s : by_level[lev]) maxw = std::max(maxw, S.w(s));
+        const int64_t g_off = (int64_t)gather.size();
+        for (int32_t s : by_level[lev])
+            if (S.child_ptr[s + 1] > S.child_ptr[s]) gather.push_back(s);
         for (int k0 = 0; k0 < maxw; k0 += SOLVE_NB) {
             Numeric::SolveStep st {};
             st.doff = (int64_t)diag.size();
             st.goff = (int64_t)bwd.size();
             st.foff = (int64_t)fwd.size();
+            st.gaoff = g_off;
+            st.gacount = k0 == 0 ? (int32_t)((int64_t)gather.size() - g_off) : 0;  // before the level's first step
             for (int32_t s : by_level[lev]) {
                 const int w = S.w(s), m = S.sn_m[s];
                 if (w <= k0) continue;
-                diag.push_back(make_int2(s, k0));
+                const int rb0 = std::min(w, k0 + SOLVE_NB);
+                const int ng = rb0 < m ? (m - rb0 + SOLVE_ROWS - 1) / SOLVE_ROWS : 0;
+                diag.push_back(make_int4(s, k0, (int)((int64_t)bwd.size() - st.goff), ng));
                 inv64.push_back(make_int2(s, k0));
                 if (w > k0 + PNB) {
                     inv64.push_back(make_int2(s, k0 + PNB));
@@ -135,6 +144,7 @@ static int64_t solve_build(Numeric& N) {
             st.dcount = (int32_t)((int64_t)diag.size() - st.doff);
             st.gcount = (int32_t)((int64_t)bwd.size() - st.goff);
             st.fcount = (int32_t)((int64_t)fwd.size() - st.foff);
+            max_g = std::max<int64_t>(max_g, st.gcount);
             N.solve_steps.push_back(st);
         }
     }
@@ -144,7 +154,7 @@ static int64_t solve_build(Numeric& N) {
     N.n_sinv = (int32_t)inv64.size();
     N.n_sinv2 = (int32_t)inv128.size();
     if ((rc = upload(N, diag, N.d_sdiag)) || (rc = upload(N, inv64, N.d_sinv)) || (rc = upload(N, inv128, N.d_sinv2)) ||
-        (rc = upload(N, bwd, N.d_sgemv)) || (rc = upload(N, fwd, N.d_sfwd)) ||
+        (rc = upload(N, bwd, N.d_sgemv)) || (rc = upload(N, fwd, N.d_sfwd)) || (rc = upload(N, gather, N.d_sgather)) ||
         (rc = upload(N, S.rows, d_rows)) ||
         (rc = upload(N, S.rows_ptr, d_rows_ptr)) || (rc = upload(N, solve_perm, N.d_post)))
         return rc;
@@ -159,6 +169,25 @@ static int64_t solve_build(Numeric& N) {
     N.SP.rows = d_rows;
     N.SP.panel_pool = N.gpanel;
     N.SP.c = N.d_sbuf + S.n;  // internal-order work vector
+    // u: each front's contribution-block rows (sum mb); part: the backward GEMV partials
+    std::vector<int64_t> u_off((size_t)S.ns);
+    int64_t u_tot = 0;
+    for (int32_t s = 0; s < S.ns; ++s) {
+        u_off[s] = u_tot;
+        u_tot += S.mb(s);
+    }
+    int64_t* d_u_off = nullptr;
+    if ((rc = upload(N, u_off, d_u_off))) return rc;
+    if ((rc = dalloc(N, (size_t)std::max<int64_t>(u_tot, 1) * sizeof(double), p))) return rc;
+    N.SP.u = (double*)p;
+    N.u_total = u_tot;
+    if ((rc = dalloc(N, (size_t)max_g * SOLVE_NB * sizeof(double), p))) return rc;
+    N.SP.part = (double*)p;
+    N.SP.u_off = d_u_off;
+    N.SP.child_ptr = N.R[0].P.child_ptr;
+    N.SP.child_list = N.R[0].P.child_list;
+    N.SP.rel_ptr = N.R[0].P.rel_ptr;
+    N.SP.relind = N.R[0].P.relind;
     N.solve_ready = true;
     return SC_OK;
 }
@@ -185,10 +214,13 @@ int64_t numeric_solve_device(Numeric& N, const double* d_b, double* d_x) {
     double* io = N.d_sbuf;
     auto sweeps = [&]() -> hipError_t {
         hipError_t e = launch_permute(N.SP.c, io, N.d_post, n, false, s0);
-        // forward: one fused launch per step (y to SP.y), then y -> c
+        if (e == hipSuccess) e = hipMemsetAsync(N.SP.u, 0, (size_t)std::max<int64_t>(N.u_total, 1) * sizeof(double), s0);
+        // forward: per level the children's u gathered, then one fused launch per step
+        // (y to SP.y), then y -> c
         for (size_t i = 0; e == hipSuccess && i < N.solve_steps.size(); ++i) {
             const Numeric::SolveStep& t = N.solve_steps[i];
-            e = launch_solve_fwd(N.SP, N.d_sfwd + t.foff, t.fcount, s0);
+            e = launch_solve_fwd_gather(N.SP, N.d_sgather + t.gaoff, t.gacount, s0);
+            if (e == hipSuccess) e = launch_solve_fwd(N.SP, N.d_sfwd + t.foff, t.fcount, s0);
         }
         if (e == hipSuccess)
             e = hipMemcpyAsync(N.SP.c, N.SP.y, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s0);

@@ -362,6 +362,36 @@ def test_solve_device_and_residual_lap32(gpu):
     assert np.linalg.norm(x2 - x) / np.linalg.norm(x) < 1e-13
 
 
+@pytest.mark.parametrize("case", ["lap24", "1138_bus", "lap16_allfronts", "lap48"])
+def test_solve_bitwise_deterministic(gpu, mtx, case):
+    # VERDICT r5 item 7 (deterministic ordering): the solves accumulate without
+    # atomics (per-front update vectors gathered by the parent in child order; backward
+    # partials summed in task order), so repeated solves, a solve after a refactorization,
+    # a second handle and the eager sweeps all give the same bits
+    kw = {}
+    if case == "1138_bus":
+        A = mtx(case)
+    elif case == "lap16_allfronts":
+        A, kw = sc.laplacian3d(16), dict(small_front_max=0)
+    else:
+        A = sc.laplacian3d(int(case[3:]))
+    b = np.random.default_rng(11).standard_normal(A.size())
+    xs = []
+    for rep in range(2):
+        num = sc.Numeric(sc.Symbolic(A, **kw))
+        assert num.factor(A.x) == 0
+        xs.append(num.solve(b))
+        xs.append(num.solve(b))
+        assert num.factor(A.x) == 0
+        xs.append(num.solve(b))
+        if rep == 1:
+            assert sc.lib().sc_debug_solve_eager(num.h, 1) == 0
+            xs.append(num.solve(b))
+    for x in xs[1:]:
+        assert np.array_equal(xs[0], x)
+    assert _backward_error(A, xs[0], b) < 1e-14
+
+
 def _closed_block_start(A, J, lo):
     """Smallest a >= lo with no entry of A in a row < a in columns [a, a + J): no fill
     path then reaches an earlier column, so L[a:a+J, a:a+J] = chol(A[a:a+J, a:a+J])."""
@@ -410,16 +440,14 @@ def test_lap128_closed_blocks_parity_and_solve(gpu):
     assert be < 1e-14
 
 
-@pytest.mark.timeout(1500)  # factor, export 34 GB of L in 1e8-entry blocks, reduce on the host
-@pytest.mark.parametrize("opts", [{}, dict(panel_psk=1, psk_min_w=4096)], ids=["default", "psk_top"])
-def test_lap128_oracle_sketch(gpu, opts):
-    # VERDICT r4 item 1 / north_star: the WHOLE 128^3 factor against the oracle.  The
-    # oracle's L (34 GB, hours of one core) was reduced once by
-    # tests/golden/make_lap128_sketch.py to per-chunk norms, per-1024-column norms over
-    # the last 262,144 columns (the top separators and the root: ~97% of the flops),
-    # Gaussian sketches L(:, J)^T r there and bilinear sketches u^T L(:, chunk) v per
-    # chunk (tests/lap128_sketch.py); the GPU factor, exported through the C ABI, is
-    # reduced the same way.  Bars: norms to 1e-13, sketch rel-Fro estimates < 1e-12.
+def _lap128_sketch_check(num, label):
+    """Reduce a 128^3 factor (any handle, exported column block by column block through
+    sc_export_L_cols) the way tests/golden/make_lap128_sketch.py reduced the oracle's L,
+    and check it against that fixture: chunk / group norms to 1e-13, sketch rel-Fro
+    estimates < 1e-12.  Also the pattern at full size: per column, the number of nonzero
+    exported values (relaxed supernode entries are exact zeros) equals the oracle's column
+    count (oracle/refchol.c col_count, reference chol.hpp:567-622), and the product's
+    symbolic column pointers (sc_symbolic_pattern) equal the oracle's."""
     import json
     import os
     import sys
@@ -435,8 +463,12 @@ def test_lap128_oracle_sketch(gpu, opts):
     meta = json.loads(str(fx["meta"]))
     A = sc.laplacian3d(ls.K)
     assert ls.input_digest(A) == meta["digest"]
-    num = sc.Numeric(sc.Symbolic(A, **opts))
-    assert num.factor(A.x) == 0
+    osym = oracle.symbolic(A)
+    colcount = osym["colcount"]
+    Lp = np.zeros(ls.N + 1, dtype=np.int64)
+    assert sc.lib().sc_symbolic_pattern(num.symb.h, Lp.ctypes.data_as(ctypes.c_void_p), None) == 0
+    assert np.array_equal(Lp, osym["Lp"])
+    nzcount = np.zeros(ls.N, dtype=np.int64)
     acc = ls.Accumulator()
     for c0 in range(0, ls.N, ls.CHUNK):
         c1 = c0 + ls.CHUNK
@@ -448,14 +480,35 @@ def test_lap128_oracle_sketch(gpu, opts):
             b = max(a + 1, min(b, c1))
             bp, ri, rx = num.export_cols(a, b)
             acc.add(a, b, bp, ri, rx)
+            nzcount[a:b] = np.add.reduceat((rx != 0).astype(np.int64), (bp - bp[0])[:-1])
             a = b
+    bad = np.flatnonzero(nzcount != colcount)
     res = acc.result()
     cmp = ls.compare(res, ref)
-    print(f"lap128 oracle sketch {opts}: {cmp}, oracle {meta['oracle_seconds']:.0f} s")
+    print(f"lap128 oracle sketch {label}: {cmp}, oracle {meta['oracle_seconds']:.0f} s; "
+          f"nonzeros per column == oracle colcount on {ls.N - len(bad)} / {ls.N} columns")
+    assert len(bad) == 0, bad[:10]
+    assert int(nzcount.sum()) == osym["nnz_L"]
     assert cmp["chunk_norm_rel"] < 1e-13
     assert cmp["group_norm_rel"] < 1e-13
     assert cmp["sketch_J_rel_fro"] < 1e-12
     assert cmp["sketch_chunk_rel_fro_max"] < 1e-12
+    return A
+
+
+@pytest.mark.timeout(1500)  # factor, export 34 GB of L in 1e8-entry blocks, reduce on the host
+def test_lap128_oracle_sketch(gpu):
+    # VERDICT r4 item 1 / north_star: the WHOLE 128^3 factor against the oracle.  The
+    # oracle's L (34 GB, hours of one core) was reduced once by
+    # tests/golden/make_lap128_sketch.py to per-chunk norms, per-1024-column norms over
+    # the last 262,144 columns (the top separators and the root: ~97% of the flops),
+    # Gaussian sketches L(:, J)^T r there and bilinear sketches u^T L(:, chunk) v per
+    # chunk (tests/lap128_sketch.py); the GPU factor, exported through the C ABI, is
+    # reduced the same way (_lap128_sketch_check).
+    A = sc.laplacian3d(128)
+    num = sc.Numeric(sc.Symbolic(A))
+    assert num.factor(A.x) == 0
+    _lap128_sketch_check(num, "single GPU")
 
 
 @pytest.fixture(scope="module")
@@ -467,10 +520,9 @@ def lap48_oracle():
 
 
 @pytest.mark.parametrize("opts", [{}, dict(asm_tile_min_m=1024), dict(cb_gather=0), dict(trsm_split_wg=1),
-                                  dict(lookahead=0), dict(cb_gather=0, panel_nb_outer=256), dict(panel_psk=1),
-                                  dict(panel_psk=1, psk_rows=128, lookahead=0)],
+                                  dict(lookahead=0), dict(cb_gather=0, panel_nb_outer=256)],
                          ids=["default", "tiled_asm", "assembled_cb", "split_potrf", "no_lookahead",
-                              "assembled_cb_nbo256", "psk", "psk128_no_lookahead"])
+                              "assembled_cb_nbo256"])
 def test_lap48_full_parity(gpu, lap48_oracle, opts):
     # the whole 48^3 factor (n = 110592, F = 7.07e10: a 2304-wide root, CB SYRK with K
     # up to 1152 on 128 x 128 tiles) against the oracle, exact pattern and rel-Fro;
@@ -490,8 +542,7 @@ def test_lap48_full_parity(gpu, lap48_oracle, opts):
 @pytest.mark.parametrize("nranks,rccl,opts", [(2, False, {}), (4, False, {}), (8, False, {}), (2, True, {}),
                                                (4, True, {}), (8, True, {}),
                                                (8, False, dict(dist_asm=0)), (4, True, dict(dist_asm=0)),
-                                               (4, False, dict(dist_pieces=1)), (8, False, dict(panel_psk=1)),
-                                               (4, True, dict(panel_psk=1, psk_min_w=1000000)), (8, True, dict(dist_pieces=16)),
+                                               (4, False, dict(dist_pieces=1)), (8, True, dict(dist_pieces=16)),
                                                (4, True, dict(dist_pieces=3))])
 def test_partitioned_defaults_lap48(gpu, lap48_oracle, nranks, rccl, opts):
     # the distributed plan at the DEFAULT options the N-GPU bench runs (panel_nb_outer
@@ -529,8 +580,7 @@ def lap64_oracle():
     return A, Lp, Li, Lx
 
 
-@pytest.mark.parametrize("opts", [{}, dict(asm_tile_min_m=1024), dict(panel_psk=1)],
-                         ids=["default", "tiled_asm", "psk"])
+@pytest.mark.parametrize("opts", [{}, dict(asm_tile_min_m=1024)], ids=["default", "tiled_asm"])
 def test_lap64_full_parity(gpu, lap64_oracle, opts):
     # the whole 64^3 factor (n = 262144, F = 4.15e11) against the oracle: a root of about
     # 4096 columns in four 1024-column slabs (lookahead-stream outer updates, recursive
@@ -595,13 +645,14 @@ def test_partitioned_defaults_lap64(gpu, lap64_oracle, nranks, rccl):
     assert be < 1e-14
 
 
+@pytest.mark.timeout(1500)
 def test_partitioned_lap128_emulated8(gpu):
-    # THE plan the 8-GPU bench runs (128^3, defaults: 7 distributed
-    # fronts, the 16447-wide root over all 8 ranks in two-slab blocks, 6 split fronts, 64
-    # comm steps, 306 messages), every rank emulated on this one GPU with private memory
-    # and every message moved as a device copy.  The whole factor is compared with the
-    # single-GPU factor (itself oracle-checked at 48^3 / 64^3 whole and on 128^3 closed
-    # blocks), column chunk by column chunk; plus the full-size solve backward error.
+    # THE plan the 8-GPU bench runs (128^3, defaults: 7
+    # distributed fronts, the 16447-wide root over all 8 ranks in two-slab blocks, 6 split
+    # fronts), every rank emulated on this one GPU with private memory and every message
+    # moved as a device copy.  The whole factor is checked directly against the ORACLE
+    # sketch fixture (the same four bars and the full-size pattern check as the
+    # single-GPU factor), plus the full-size solve backward error.
     A = sc.laplacian3d(128)
     n = A.size()
     s = sc.Symbolic(A)
@@ -612,31 +663,10 @@ def test_partitioned_lap128_emulated8(gpu):
     # distributed assembly (no STEP_INIT); 112 / 440 with every distributed-panel slab
     # handed over in two 512-column pieces (dist_pieces = 2); 208 / 708 with four (the
     # round-5 default: 159.9 -> 155.4 ms projected critical path at 50 GB/s)
-    assert info["n_steps"] == 208 and info["n_msgs"] == 708
-    CH = 1 << 16
-    ref = []
-    one = sc.Numeric(s)
-    assert one.factor(A.x) == 0
-    for j0 in range(0, n, CH):
-        ref.append(one.export_cols(j0, min(n, j0 + CH))[2])
-    del one
+    print(f"lap128 8 emulated ranks: {info['n_steps']} comm steps, {info['n_msgs']} messages")
     v = sc.Numeric(s, nranks=8, virtual=True)
     assert v.factor(A.x) == 0
-    d2 = r2 = 0.0
-    worst = 0.0
-    for q, j0 in enumerate(range(0, n, CH)):
-        cp, ri, rx = v.export_cols(j0, min(n, j0 + CH))
-        assert rx.shape == ref[q].shape
-        dd = float(np.sum((rx - ref[q]) ** 2))
-        rr = float(np.sum(ref[q] ** 2))
-        worst = max(worst, np.sqrt(dd / rr))
-        d2 += dd
-        r2 += rr
-        ref[q] = None
-    err = np.sqrt(d2 / r2)
-    print(f"lap128 8 emulated ranks vs single GPU: rel-Fro {err:.3e} (worst {CH}-column chunk {worst:.3e}); "
-          f"{info['n_steps']} comm steps, {info['n_msgs']} messages")
-    assert err < TOL and worst < TOL
+    _lap128_sketch_check(v, "8 emulated ranks")
     b = np.random.default_rng(8).standard_normal(n)
     x = v.solve(b)
     be = _backward_error(A, x, b)
@@ -866,37 +896,34 @@ def _dense_spd(n, seed):
     return sc.triplet_to_csc_matrix(iu[0], iu[1], D[iu], n)
 
 
-PSK_CASES = [("lap16_allfronts", dict(small_front_max=0)), ("lap16_allfronts_rl", dict(small_front_max=0, inner_order=0)),
-             ("dense1350", {}), ("dense1350_nbo128", dict(panel_nb_outer=128)),
-             ("dense1350_nbo192_rl", dict(panel_nb_outer=192, inner_order=0)), ("lap24", {}),
-             ("lap24_nolookahead", dict(lookahead=0))]
+PANEL_CASES = [("lap16_allfronts", dict(small_front_max=0)),
+               ("lap16_allfronts_rl", dict(small_front_max=0, inner_order=0)),
+               ("dense1350", {}), ("dense1350_nbo128", dict(panel_nb_outer=128)),
+               ("dense1350_nbo192_rl", dict(panel_nb_outer=192, inner_order=0)), ("lap24", {}),
+               ("lap24_nolookahead", dict(lookahead=0))]
 
 
-@pytest.mark.parametrize("rows", [64, 128, 256])
-@pytest.mark.parametrize("case,opts", PSK_CASES, ids=[c for c, _ in PSK_CASES])
-def test_psk_bitwise_equal_per_step(gpu, case, opts, rows):
-    # the persistent slab chain (one launch per slab and level, steps ordered by device-
-    # scope flags) forms the same sums in the same order as the per-step launches: the
-    # factor is bitwise identical, and so is a second factorization through the same
-    # handle (flags re-armed) and a hipGraph replay
+@pytest.mark.parametrize("case,opts", PANEL_CASES, ids=[c for c, _ in PANEL_CASES])
+def test_panel_variants_oracle_and_bitwise(gpu, case, opts):
+    # the large-front panel chain (POTRF / TRSM / inner and outer updates) on dense and
+    # Laplacian inputs, slab widths that do and do not divide the front: eager and hipGraph
+    # replay, twice each through the same handle, are bitwise identical and match the oracle
     A = _dense_spd(1350, 5) if case.startswith("dense") else sc.laplacian3d(int(case[3:5]))
     facs = []
-    for psk in (0, 1):
-        for graph in ((0,) if psk == 0 else (0, 1)):
-            num = sc.Numeric(sc.Symbolic(A, panel_psk=psk, psk_rows=rows, use_graph=graph, **opts))
-            for _ in range(2):
-                assert num.factor(A.x) == 0
-                facs.append(num.export()[1].x.copy())
+    for graph in (0, 1):
+        num = sc.Numeric(sc.Symbolic(A, use_graph=graph, **opts))
+        for _ in range(2):
+            assert num.factor(A.x) == 0
+            facs.append(num.export()[1].x.copy())
     for f in facs[1:]:
         assert np.array_equal(facs[0], f)
     st, Lp, Li, Lx = oracle.chol(A)
     assert rel_fro(facs[0], Lx) < TOL
 
 
-def test_psk_not_positive_definite(gpu):
-    # a broken pivot inside a persistent slab: the owner's POTRF reports the oracle's
-    # column, the other workgroups still finish (no hang), and a good refactorization
-    # through the same handle clears it
+def test_panel_not_positive_definite(gpu):
+    # a broken pivot inside a large front's panel chain: the oracle's column is reported,
+    # and a good refactorization through the same handle clears it
     A = _dense_spd(700, 9)
     x = A.x.copy()
     k = 333
@@ -905,20 +932,8 @@ def test_psk_not_positive_definite(gpu):
     x[diag] = -1.0
     st, *_ = oracle.chol(sc.csc_matrix(A.n_rows, A.n_cols, A.p, A.i, x))
     assert st > 0
-    num = sc.Numeric(sc.Symbolic(A, panel_psk=1))
+    num = sc.Numeric(sc.Symbolic(A))
     assert num.factor(x) == st
     assert num.factor(A.x) == 0
     _, L = num.export()
     assert rel_fro(L.x, oracle.chol(A)[3]) < TOL
-
-
-@pytest.mark.parametrize("nranks", [2, 4])
-def test_psk_partitioned_lap24(gpu, nranks):
-    # emulated multi-rank plan with the persistent slab chains on every rank's own fronts
-    A = sc.laplacian3d(24)
-    ref = sc.Numeric(sc.Symbolic(A, panel_nb_outer=128, dist_cbb=128))
-    assert ref.factor(A.x) == 0
-    v = sc.Numeric(sc.Symbolic(A, panel_psk=1, panel_nb_outer=128, dist_cbb=128), nranks=nranks, virtual=True)
-    assert v.factor(A.x) == 0
-    st, Lp, Li, Lx = oracle.chol(A)
-    assert rel_fro(v.export()[1].x, Lx) < TOL
