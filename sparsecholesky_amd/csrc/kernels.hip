@@ -2108,8 +2108,11 @@ __global__ __launch_bounds__(256) void solve_diag_kernel(SolvePlan P, const int4
     const int nb = min(SOLVE_NB, w - k0);
     const double* __restrict__ blk = P.panel_pool + P.panel_off[s] + (int64_t)k0 * m + k0;
     if (tid < SOLVE_NB) {
-        double v = tid < nb ? P.c[c0 + k0 + tid] : 0.0;
-        for (int g2 = 0; g2 < t.w; ++g2) v += P.part[(int64_t)(t.z + g2) * SOLVE_NB + tid];  // GEMV partials, in order
+        double v = 0.0;
+        if (tid < nb) {  // columns past nb: no partials written (dead entries must stay 0, not NaN)
+            v = P.c[c0 + k0 + tid];
+            for (int g2 = 0; g2 < t.w; ++g2) v += P.part[(int64_t)(t.z + g2) * SOLVE_NB + tid];  // GEMV partials, in order
+        }
         cb[tid] = v;
     }
     __syncthreads();
