@@ -112,6 +112,11 @@ typedef struct sc_options {
     int32_t dist_pieces;     /* multi-GPU distributed panels: each final slab is handed over in this many column
                                 pieces (default 4: 256 of a 1024-column slab), each sent as soon as the chain has
                                 finished it, so the next slab's owner starts updating before the slab is done */
+    int32_t panel_prefactor; /* 1 (default): in the 64-column panel chain, the recursive inner update after a step
+                                (K = 64 or 128) also forms and factors the NEXT step's 64 x 64 diagonal block in one
+                                extra workgroup, so that step's TRSM loads L11 instead of every TRSM workgroup
+                                factoring it (the POTRF runs beside the update's tiles, off the chain's critical
+                                path; bitwise-identical factor); 0: every full step fuses its POTRF */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };

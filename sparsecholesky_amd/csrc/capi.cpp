@@ -95,6 +95,7 @@ void sc_default_options(sc_options* opt) {
     opt->tiny_dense = 1;
     opt->dist_asm = 1;
     opt->dist_pieces = 4;
+    opt->panel_prefactor = 1;
 }
 
 int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_options* opt,

@@ -1526,21 +1526,85 @@ __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t
     }
 }
 
+// Panel chain lookahead (the pre-factor workgroup of an inner panel update, tile marker
+// y = -1): the update's tile (0, 0) is the NEXT chain step's 64 x 64 diagonal block.  This
+// workgroup forms it (C - A A^T, the same MFMA sums as the regular tile), keeps it in LDS
+// (packed lower triangle), factors it in registers (the fused TRSM kernel's POTRF,
+// small_steps1_fast) and stores L11, so the next step's TRSM launch only loads L11
+// (trsm_panel_g_kernel<2>): the 64-pivot POTRF leaves the chain's critical path and runs
+// beside the update's other tiles.  Same arithmetic in the same order: bitwise identical.
+template <int BK>
+__device__ __forceinline__ void panel_prefactor(const GemmTask& T, int32_t* info, double* smem) {
+    static_assert(2 * 2 * BK * (64 + 16) >= 64 * 65 / 2, "the packed diagonal block fits the operand LDS");
+    double4_t acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
+    mfma_kloop<64, 2, 2, BK>(T.A, T.lda, T.K, T.M, T.N, 0, 0, acc, smem);  // ends with a barrier
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wr = wid >> 1, wc = wid & 1;
+    const int64_t ldc = T.ldc;
+    double* __restrict__ F = smem;  // column j at pk_col(64, j), rows j..63
+    const __amdgpu_buffer_rsrc_t rc = buf_rsrc(T.C, (uint32_t)(64 * ldc * 8));
+    double cv[2][2][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gi = wr * 32 + a * 16 + MFMA_F64_ROW(lane, r), gj = wc * 32 + b * 16 + (lane & 15);
+                cv[a][b][r] = buf_ld(rc, gi >= gj ? (int)((gi + (int64_t)gj * ldc) * 8) : BUF_DEAD, 0);
+            }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gi = wr * 32 + a * 16 + MFMA_F64_ROW(lane, r), gj = wc * 32 + b * 16 + (lane & 15);
+                if (gi >= gj) F[pk_col(64, gj) + gi - gj] = cv[a][b][r] - acc[a][b][r];
+            }
+    __syncthreads();
+    SmallRegs<1> R;
+    small_tiles<1>(R, PNB, PNB);
+    small_load<1>(R, F, PNB);
+    __syncthreads();  // F is read: the column buffer overlays it
+    small_steps1_fast(R, smem, PNB, info, T.pf);
+    if (R.bi[0] < 0) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int i = 4 * R.bi[0] + r, j = 4 * R.bj[0] + c;
+            if (i >= j) T.C[(int64_t)j * ldc + i] = R.v[0][r * 4 + c];
+        }
+}
+
 // LEAN (short-K launches on 64 x 64 tiles): BK = 8 and 32-row gather chunks halve the
 // LDS (20 KB), so six workgroups fit a CU instead of four -- these launches are latency-
 // bound (a few K stages, then the C traffic), not MFMA-bound
-template <int BT, int WM, int WN, int TAG, int EPI, int LEAN = 0>
+// PF: panel-update launch carrying pre-factor workgroups (panel_prefactor)
+template <int BT, int WM, int WN, int TAG, int EPI, int LEAN = 0, int PF = 0>
 __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ tasks, const int2* __restrict__ tiles,
                                                int bidx, const int64_t* __restrict__ gblk,
-                                               const GSeg* __restrict__ gseg) {
+                                               const GSeg* __restrict__ gseg, int32_t* info = nullptr) {
     constexpr int BK = LEAN ? 8 : 16;
     constexpr int LDT = BT + 16;
     constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
-    __shared__ double smem[2 * 2 * BK * LDT];  // A and B stages
+    __shared__ __attribute__((aligned(16))) double smem[2 * 2 * BK * LDT];  // A and B stages
 
     // host-ordered tile list: blocks sharing an XCD walk a contiguous, L2-blocked run of tiles
     const int2 tl = tiles[bidx];
     const GemmTask T = tasks[tl.x];
+    if constexpr (PF) {
+        static_assert(BT == 64 && WM == 2 && WN == 2 && TAG == 0, "pre-factor on 64 x 64 panel-update tiles");
+        if (tl.y < 0) {
+            panel_prefactor<BK>(T, info, smem);
+            return;
+        }
+    }
     const int ti = tl.y >> 16, tj = tl.y & 0xffff;
     const int row0 = ti * BT, col0 = tj * BT;
 
@@ -1612,12 +1676,12 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
     }
 }
 
-template <int BT, int WM, int WN, int TAG, int EPI, int LEAN = 0>
+template <int BT, int WM, int WN, int TAG, int EPI, int LEAN = 0, int PF = 0>
 __global__ __launch_bounds__(64 * WM * WN, LEAN ? (TAG ? 5 : 6) : 1) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
                                                                   const int2* __restrict__ tiles,
                                                                   const int64_t* __restrict__ gblk,
-                                                                  const GSeg* __restrict__ gseg) {
-    syrk_tile_body<BT, WM, WN, TAG, EPI, LEAN>(tasks, tiles, blockIdx.x, gblk, gseg);
+                                                                  const GSeg* __restrict__ gseg, int32_t* info) {
+    syrk_tile_body<BT, WM, WN, TAG, EPI, LEAN, PF>(tasks, tiles, blockIdx.x, gblk, gseg, info);
 }
 
 // ---------------------------------------------------------------------------
@@ -1691,18 +1755,24 @@ static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int b
                           bool lean) {
     if (bt == 64 && lean)
         hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG, EPI, 1>), dim3(n), dim3(256), 0, st, tasks, tiles, gt.blk,
-                           gt.seg);
+                           gt.seg, gt.info);
     else if (bt == 128)
         hipLaunchKernelGGL((syrk_mfma_kernel<128, 2, 4, TAG, EPI>), dim3(n), dim3(512), 0, st, tasks, tiles, gt.blk,
-                           gt.seg);
+                           gt.seg, gt.info);
     else
         hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, TAG, EPI>), dim3(n), dim3(256), 0, st, tasks, tiles, gt.blk,
-                           gt.seg);
+                           gt.seg, gt.info);
 }
 
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
-                       int epi, GatherTab gt, bool lean) {
+                       int epi, GatherTab gt, bool lean, bool pf) {
     if (total_tiles <= 0) return hipSuccess;
+    if (pf) {  // panel update with pre-factor workgroups: 64 x 64 tiles, batched epilogue
+        if (bt != 64 || tag) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((syrk_mfma_kernel<64, 2, 2, 0, 1, 0, 1>), dim3(total_tiles), dim3(256), 0, st, tasks, tiles,
+                           gt.blk, gt.seg, gt.info);
+        return hipGetLastError();
+    }
     if (tag)
         epi ? launch_syrk_t<1, 1>(tasks, tiles, total_tiles, bt, st, gt, lean)
             : launch_syrk_t<1, 0>(tasks, tiles, total_tiles, bt, st, gt, lean);

@@ -68,6 +68,7 @@ struct GSeg {
 struct GatherTab {
     const int64_t* blk = nullptr;
     const GSeg* seg = nullptr;
+    int32_t* info = nullptr;  // status word (pivot failures of the panel pre-factor workgroups)
 };
 
 // One lower-trapezoid SYRK update: C[i,j] -= sum_k A[i,k] A[j,k], j < N, j <= i < M.
@@ -87,6 +88,10 @@ struct GemmTask {
     int32_t gs = -1, gv = 0;
     int64_t gb = -1;
     int32_t gw = 0;  // gathering tasks: the front's width (the CB starts at front row gw; K may be one slab)
+    // panel updates (launches with pf = 1): >= 0 = the internal column of the 64 x 64 diagonal
+    // block at C's origin, which this task's pre-factor workgroup (tile marker y = -1) updates
+    // and factors in registers, so the next chain step's TRSM loads L11 instead of factoring it
+    int32_t pf = -1;
 };
 // Strided <-> packed copy of a rows x cols block (pack: a -> b; unpack: b -> a).
 struct Copy2D {
@@ -240,7 +245,7 @@ hipError_t launch_trsm_panel(const DevPlan& P, const TrsmTask* tasks, int count,
 // gt: the gather tables (CB tasks with gs >= 0 gather their children's entries)
 // lean: 64 x 64 tiles with half the LDS (BK = 8; short-K launches, syrk_lean_kmax)
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
-                       int epi = 0, GatherTab gt = {}, bool lean = false);
+                       int epi = 0, GatherTab gt = {}, bool lean = false, bool pf = false);
 hipError_t launch_stamp(uint64_t* slot, hipStream_t st);
 
 hipError_t launch_hwid(uint32_t* out, int nwg, int threads, int spin, hipStream_t st);

@@ -300,8 +300,12 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
                                      L.epi);
         case L_PANEL:
         case L_CB:
+        {
+            GatherTab gt = N.gtab;
+            gt.info = N.d_info;
             return launch_syrk(N.d_gemm + L.off, N.d_tiles + L.toff, L.count, L.bt, L.kind == L_CB ? 1 : 0, st, L.epi,
-                               N.gtab, L.lean != 0);
+                               gt, L.lean != 0, L.pf != 0);
+        }
         case L_COMM:
             return comm_launch(N, L);
     }

@@ -164,6 +164,7 @@ struct Launch {
     int32_t bt;       // SYRK tile edge (64 or 128)
     int32_t epi;      // SYRK epilogue with its C loads batched (short-K and critical-path launches)
     int32_t lean;     // SYRK on 64 x 64 tiles with half the LDS (deepest K <= syrk_lean_kmax)
+    int32_t pf;       // panel update carrying pre-factor workgroups (GemmTask.pf; 64 x 64 tiles)
     int32_t strm;     // 0 = main stream, 1 = lookahead stream, 2 = comm stream
     int32_t vr;       // hosted rank whose DevPlan the kernel uses
     double flops;     // algorithmic SYRK flops (CB launches: mb*(mb+1)*w)

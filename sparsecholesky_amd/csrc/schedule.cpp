@@ -180,15 +180,27 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // more to the lean instance's smaller gather batches than they gain in occupancy)
         L.lean = L.bt == SYRK_BT_SMALL && S.opt.syrk_lean_kmax > 0 && maxK <= S.opt.syrk_lean_kmax &&
                  (kind == L_PANEL || maxK > 64);
+        // panel-chain lookahead: a task whose pre-factor workgroup forms and factors the next
+        // step's diagonal block (tile (0, 0), marker y = -1) -- 64 x 64 tiles, batched epilogue
+        for (auto& t : tasks) L.pf |= t.pf >= 0 ? 1 : 0;
+        if (L.pf) {
+            L.bt = SYRK_BT_SMALL;
+            L.lean = 0;
+            L.epi = 1;
+        }
         L.toff = (int64_t)tiles.size();
         L.bytes = 0.0;
         for (size_t q = 0; q < tasks.size(); ++q) {
+            const size_t first = tiles.size();
             append_tiles(tiles, (int)q, tasks[q].M, tasks[q].N, L.bt);
+            if (tasks[q].pf >= 0) tiles[first].y = -1;  // append_tiles emits tile (0, 0) first
             gemm.push_back(tasks[q]);
             L.bytes += task_bytes(tasks[q]);
         }
         L.count = (int32_t)((int64_t)tiles.size() - L.toff);
         xcd_order_tasks(tiles.data() + L.toff, L.count, tasks.data(), (int)tasks.size());
+        if (L.pf)  // the pre-factor workgroups (the longest, on the chain) are dispatched first
+            std::stable_partition(tiles.begin() + L.toff, tiles.end(), [](const int2& t) { return t.y < 0; });
         L.ntasks = (int32_t)tasks.size();
         L.big = big;
         L.flops = flops;
@@ -415,6 +427,13 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         return multi && D.early[s] && D.owner[s] == N.R[v].rank;
     };
     auto is_dasm = [&](int32_t s) { return multi && D.dasm[s]; };
+    // panel_prefactor: the recursive inner update after a chain step also factors the next
+    // step's diagonal block when that block is a full 64-column block of the same slab and
+    // the update runs on 64 x 64 tiles (span <= 128; K = 64 or 128)
+    auto prefactor_ok = [&](int span, int k1, int slab1) {
+        return S.opt.panel_prefactor && S.opt.inner_order == 1 && S.opt.syrk_tile != 128 && span <= 2 * PNB &&
+               k1 + PNB <= slab1;
+    };
     // distributed assembly: one write-once tile-assembly launch of the front columns of
     // s that hosted rank v owns (its panel slabs and CB column blocks, D.col_owner), in
     // 16-column blocks; a block straddling another rank's columns computes those too,
@@ -577,6 +596,9 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             vec.push_back(t);
             fl += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
         };
+        // fronts whose block at the current step was pre-factored by the previous step's
+        // inner update (panel_prefactor): their TRSM loads L11 (trsm_panel_g_kernel<2>)
+        std::vector<char> pre((size_t)S.ns, 0);
         for (int k0 = 0; k0 < maxw; k0 += PNB) {
             Launch Lp {};
             Lp.kind = L_POTRF;
@@ -611,6 +633,8 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 if (nb < PNB) {
                     potrf.push_back(make_int2(s, k0));
                     for (int r0 = k1; r0 < m; r0 += TRSM_ROWS) trsm_part.push_back(TrsmTask {s, k0, r0, m, 0});
+                } else if (pre[s]) {  // L11 in place: the rows below only
+                    for (int r0 = k1; r0 < m; r0 += TRSM_ROWS) trsm_split.push_back(TrsmTask {s, k0, r0, m, 0});
                 } else if (split_step) {
                     potrf.push_back(make_int2(s, k0));
                     for (int r0 = k1; r0 < m; r0 += TRSM_ROWS) trsm_split.push_back(TrsmTask {s, k0, r0, m, 0});
@@ -619,6 +643,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     for (int r0 = k1; r0 < std::max(m, k1 + 1); r0 += TRSM_ROWS) trsm.push_back(TrsmTask {s, k0, r0, m, ctr});
                 }
                 double* pan = panel_pool + poff[s];
+                pre[s] = 0;
                 if (k1 < slab1 && S.opt.inner_order == 1) {
                     // recursive order: block b of the slab closes a run of 2^t blocks
                     // (t = trailing zeros of b + 1); that run updates the next 2^t
@@ -627,6 +652,10 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     const int b = (k0 - slab0) / PNB;
                     const int span = PNB << __builtin_ctz((unsigned)(b + 1));
                     add_update(upd, uflops, pan, m, m, k1, std::min(slab1, k1 + span), k1 - span, k1);
+                    if (prefactor_ok(span, k1, slab1)) {
+                        upd.back().pf = S.sn_start[s] + k1;
+                        pre[s] = 1;
+                    }
                 } else if (k1 < slab1) {
                     add_update(upd, uflops, pan, m, m, k1, slab1, k0, k1);
                 }
@@ -803,6 +832,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 const int e = last_ev1(vk, k - 2);
                 if (e >= 0) push_wait(0, e);
                 double* pan = pan_of(vk);
+                bool pre_blk = false;  // this block was pre-factored by the previous inner update
                 for (int k0 = k0s; k0 < k1s; k0 += PNB) {
                     const int nb = std::min(PNB, k1s - k0), k1 = k0 + nb;
                     Launch Lp {};
@@ -821,9 +851,11 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     Lt.vr = vk;
                     Lt.off = (int64_t)trsm.size();
                     Lt.big = nb < PNB ? 1 : 0;
-                    const int ctr = nb < PNB ? 0 : (int)trsm.size() + 1;  // fused POTRF: arrival counter
-                    for (int r0 = k1; r0 < (nb < PNB ? m : std::max(m, k1 + 1)); r0 += TRSM_ROWS)
+                    Lt.epi = pre_blk ? 2 : 0;  // L11 already in place: load it
+                    const int ctr = (nb < PNB || pre_blk) ? 0 : (int)trsm.size() + 1;  // fused POTRF: arrival counter
+                    for (int r0 = k1; r0 < ((nb < PNB || pre_blk) ? m : std::max(m, k1 + 1)); r0 += TRSM_ROWS)
                         trsm.push_back(TrsmTask {s, k0, r0, m, ctr});
+                    pre_blk = false;
                     Lt.count = (int32_t)((int64_t)trsm.size() - Lt.off);
                     if (Lt.count > 0) N.sched.push_back(Lt);
                     // a finished piece of the slab leaves now (dist_pieces)
@@ -837,6 +869,10 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                             const int c1 = std::min(k1s, k1 + span);
                             upd_task(upd, fl, pan + (int64_t)k1 * m + k1, m, pan + (int64_t)(k1 - span) * m + k1, m,
                                      m - k1, c1 - k1, span);
+                            if (!upd.empty() && prefactor_ok(span, k1, k1s)) {
+                                upd.back().pf = S.sn_start[s] + k1;
+                                pre_blk = true;
+                            }
                         } else {
                             upd_task(upd, fl, pan + (int64_t)k1 * m + k1, m, pan + (int64_t)k0 * m + k1, m, m - k1,
                                      k1s - k1, nb);

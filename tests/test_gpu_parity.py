@@ -907,11 +907,13 @@ PANEL_CASES = [("lap16_allfronts", dict(small_front_max=0)),
 def test_panel_variants_oracle_and_bitwise(gpu, case, opts):
     # the large-front panel chain (POTRF / TRSM / inner and outer updates) on dense and
     # Laplacian inputs, slab widths that do and do not divide the front: eager and hipGraph
-    # replay, twice each through the same handle, are bitwise identical and match the oracle
+    # replay, twice each through the same handle, with and without the chain lookahead
+    # (panel_prefactor: the next diagonal block factored inside the inner update launch),
+    # are bitwise identical and match the oracle
     A = _dense_spd(1350, 5) if case.startswith("dense") else sc.laplacian3d(int(case[3:5]))
     facs = []
-    for graph in (0, 1):
-        num = sc.Numeric(sc.Symbolic(A, use_graph=graph, **opts))
+    for graph, pf in ((0, 1), (1, 1), (0, 0), (1, 0)):
+        num = sc.Numeric(sc.Symbolic(A, use_graph=graph, panel_prefactor=pf, **opts))
         for _ in range(2):
             assert num.factor(A.x) == 0
             facs.append(num.export()[1].x.copy())
@@ -932,8 +934,25 @@ def test_panel_not_positive_definite(gpu):
     x[diag] = -1.0
     st, *_ = oracle.chol(sc.csc_matrix(A.n_rows, A.n_cols, A.p, A.i, x))
     assert st > 0
-    num = sc.Numeric(sc.Symbolic(A))
-    assert num.factor(x) == st
-    assert num.factor(A.x) == 0
-    _, L = num.export()
-    assert rel_fro(L.x, oracle.chol(A)[3]) < TOL
+    for pf in (1, 0):
+        num = sc.Numeric(sc.Symbolic(A, panel_prefactor=pf))
+        assert num.factor(x) == st
+        assert num.factor(A.x) == 0
+        _, L = num.export()
+        assert rel_fro(L.x, oracle.chol(A)[3]) < TOL
+
+
+@pytest.mark.parametrize("k", [333, 334, 397, 640])
+def test_panel_not_pd_each_block_position(gpu, k):
+    # a failing pivot at the first / second / a middle / a late column of a 64-column block
+    # (blocks factored by the fused TRSM launch, by the pre-factor workgroup of an inner
+    # update, or in a partial last block): the oracle's column either way
+    A = _dense_spd(700, 9)
+    x = A.x.copy()
+    x[A.p[k + 1] - 1] = -1.0
+    st, *_ = oracle.chol(sc.csc_matrix(A.n_rows, A.n_cols, A.p, A.i, x))
+    assert st == k + 1
+    for pf in (1, 0):
+        for nbo in (1024, 128):
+            num = sc.Numeric(sc.Symbolic(A, panel_prefactor=pf, panel_nb_outer=nbo))
+            assert num.factor(x) == st, (pf, nbo)
