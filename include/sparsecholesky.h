@@ -78,9 +78,10 @@ typedef struct sc_options {
                                 has its contribution block computed by the other ranks of its group, slab-streamed
                                 (1, default); 0: every front on one rank */
     int32_t dist_cbb;        /* multi-GPU: column-block width of contribution-block ownership and transfers (1024) */
-    int32_t ordering;        /* SC_ORDER_NATURAL (default: the given order, as the reference) or SC_ORDER_ND:
-                                factor P A P^T with a nested-dissection P (sc_symbolic_perm); L, the pattern
-                                and the statistics are then those of P A P^T, solves take and return A's order */
+    int32_t ordering;        /* SC_ORDER_NATURAL (default: the given order, as the reference), SC_ORDER_ND or
+                                SC_ORDER_AMD: factor P A P^T with a nested-dissection / approximate-minimum-degree
+                                P (sc_symbolic_perm); L, the pattern and the statistics are then those of P A P^T,
+                                solves take and return A's order; other values: SC_ERR_ARG */
     int32_t dist_early;      /* multi-GPU: a large child whose parent runs on another rank computes its CB in
                                 4-block column groups and sends each group as soon as it is done (1, default) */
     int32_t dist_panel;      /* multi-GPU: a shared front wider than one slab (panel_nb_outer) has its panel
@@ -116,10 +117,11 @@ typedef struct sc_options {
                                 (K = 64 or 128) also forms and factors the NEXT step's 64 x 64 diagonal block in one
                                 extra workgroup, so that step's TRSM loads L11 instead of every TRSM workgroup
                                 factoring it (the POTRF runs beside the update's tiles, off the chain's critical
-                                path; bitwise-identical factor); 0: every full step fuses its POTRF */
+                                path; bitwise-identical factor); 2: also after the K = 256 / 512 inner updates
+                                (their launches then run on 64 x 64 tiles); 0: every full step fuses its POTRF */
 } sc_options;
 
-enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1 };
+enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1, SC_ORDER_AMD = 2 };
 
 /* Symbolic statistics (host analysis). */
 typedef struct sc_symbolic_stats {

@@ -128,7 +128,10 @@ int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_opt
     std::string err;
     int64_t rc;
     try {
-        if (o.ordering == SC_ORDER_ND && n > 0 && Ap && (Ai || Ap[n] == 0)) {
+        if (o.ordering != SC_ORDER_NATURAL && o.ordering != SC_ORDER_ND && o.ordering != SC_ORDER_AMD) {
+            rc = SC_ERR_ARG;
+            err = "sc_options.ordering must be SC_ORDER_NATURAL, SC_ORDER_ND or SC_ORDER_AMD";
+        } else if (o.ordering != SC_ORDER_NATURAL && n > 0 && Ap && (Ai || Ap[n] == 0)) {
             // factor B = P A P^T; numeric values still come from A's arrays (a_src remapped)
             std::vector<int32_t> perm((size_t)n);
             std::vector<int64_t> Bp, src;
@@ -141,7 +144,11 @@ int64_t sc_analyze(int64_t n, const int64_t* Ap, const int32_t* Ai, const sc_opt
                 if (Ai[p] < 0 || Ai[p] >= n) rc = SC_ERR_ARG;
             if (rc != SC_OK) err = "malformed CSC";
             if (rc == SC_OK) {
-                sc::nd_order(n, Ap, Ai, perm.data());
+                rc = o.ordering == SC_ORDER_AMD ? sc::amd_order(n, Ap, Ai, perm.data())
+                                                : sc::nd_order(n, Ap, Ai, perm.data());
+                if (rc != SC_OK) err = "ordering failed";
+            }
+            if (rc == SC_OK) {
                 sc::permute_upper(n, Ap, Ai, perm.data(), Bp, Bi, src);
                 rc = sc::analyze(n, Bp.data(), Bi.data(), o, h->S, err);
             }

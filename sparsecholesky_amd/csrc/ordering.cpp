@@ -9,6 +9,7 @@
 // numbered first, separators last (so separators become the top supernodes and
 // the two parts independent subtrees), recursively down to small leaves.
 #include <algorithm>
+#include <cmath>
 #include <vector>
 
 #include "symbolic.hpp"
@@ -187,6 +188,309 @@ i64 nd_order(i64 n, const i64* Ap, const i32* Ai, i32* perm) {
         stack.push_back({std::move(A), hb - nbv});
         stack.push_back({std::move(B), hb});
     }
+    return SC_OK;
+}
+
+// Approximate minimum degree (Amestoy, Davis & Duff, SIAM J. Matrix Anal. Appl. 17(4),
+// 1996): greedy minimum-degree elimination on the quotient graph, where eliminated
+// pivots become ELEMENTS (cliques stored by their variable lists) and a variable's
+// exact external degree is replaced by the AMD bound
+//   d_i <= min(n - k, d_i_old + |L_p \ i|, |A_i \ i| + |L_p \ i| + sum_{e in E_i, e != p} |L_e \ L_p|),
+// with element absorption, indistinguishable-variable (supervariable) detection by
+// hashing, mass elimination and the usual dense-row postponement.  The elimination
+// order is then postordered over the element tree.  perm[new] = old.
+//
+// Storage: one integer array iw holds every list -- a variable's elements first
+// (elen[i] of them) then its variables; an element's variables.  pe[i] is i's list
+// start, len[i] its length.  An absorbed variable / element j gets pe[j] = flip(parent)
+// (its representative supervariable or absorbing element), so the final tree is read
+// back from pe.  nv[i]: supervariable size (0 = absorbed; negated while i is in the
+// new element).  Degree lists: head[d] / next / prev.  w[]: marks for |L_e \ L_p|.
+i64 amd_order(i64 n, const i64* Ap, const i32* Ai, i32* perm) {
+    if (n <= 0) return SC_OK;
+    const Graph G = build_graph(n, Ap, Ai);
+    const i64 nnz = (i64)G.adj.size();
+    auto flip = [](i64 x) { return -x - 2; };
+    // dense rows: postponed to the end (absorbed into the dummy root n)
+    i64 dense = std::max<i64>(16, (i64)(10.0 * std::sqrt((double)n)));
+    dense = std::min<i64>(n - 2, dense);
+    i64 cap = nnz + nnz / 5 + 2 * n + 1;  // elbow room for the new elements
+    std::vector<i64> iw((size_t)cap);
+    std::vector<i64> pe((size_t)n + 1), len((size_t)n + 1), nv((size_t)n + 1, 1), nxt((size_t)n + 1, -1),
+        prv((size_t)n + 1, -1), head((size_t)n + 1, -1), elen((size_t)n + 1, 0), deg((size_t)n + 1),
+        w((size_t)n + 1, 1), hhead((size_t)n + 1, -1);
+    for (i64 i = 0; i < n; ++i) {
+        pe[i] = G.xadj[i];
+        len[i] = G.xadj[i + 1] - G.xadj[i];
+    }
+    std::copy(G.adj.begin(), G.adj.end(), iw.begin());
+    i64 used = nnz;  // iw[0, used) in use
+    len[n] = 0;
+    nv[n] = 0;
+    elen[n] = -2;
+    pe[n] = -1;
+    w[n] = 0;
+    // w-marks: reset when the stamp would overflow
+    i64 lemax = 0, mark = 2;
+    auto wclear = [&](i64 m2) {
+        if (m2 < 2 || m2 + lemax < 0) {
+            for (i64 k = 0; k < n; ++k)
+                if (w[k] != 0) w[k] = 1;
+            m2 = 2;
+        }
+        return m2;
+    };
+    auto list_remove = [&](i64 i) {
+        if (nxt[i] != -1) prv[nxt[i]] = prv[i];
+        if (prv[i] != -1)
+            nxt[prv[i]] = nxt[i];
+        else
+            head[deg[i]] = nxt[i];
+    };
+    auto list_insert = [&](i64 i, i64 d) {
+        if (head[d] != -1) prv[head[d]] = i;
+        nxt[i] = head[d];
+        prv[i] = -1;
+        head[d] = i;
+    };
+    i64 nel = 0, mindeg = 0;
+    for (i64 i = 0; i < n; ++i) {
+        deg[i] = len[i];
+        if (deg[i] == 0) {  // isolated: an element at once
+            elen[i] = -2;
+            ++nel;
+            pe[i] = -1;
+            w[i] = 0;
+        } else if (deg[i] > dense) {  // dense: absorbed into the root, ordered last
+            nv[i] = 0;
+            elen[i] = -1;
+            ++nel;
+            pe[i] = flip(n);
+            nv[n]++;
+        } else {
+            list_insert(i, deg[i]);
+        }
+    }
+    while (nel < n) {
+        // pivot k of minimum approximate degree
+        i64 k = -1;
+        for (; mindeg < n && (k = head[mindeg]) == -1; ++mindeg) {
+        }
+        if (nxt[k] != -1) prv[nxt[k]] = -1;
+        head[mindeg] = nxt[k];
+        const i64 elenk = elen[k];
+        i64 nvk = nv[k];
+        nel += nvk;
+        // compact iw when the new element might not fit after `used`
+        if (elenk > 0 && used + mindeg >= cap) {
+            for (i64 j = 0; j < n; ++j) {
+                const i64 p = pe[j];
+                if (p >= 0) {  // live list: mark its start with its owner
+                    pe[j] = iw[p];
+                    iw[p] = flip(j);
+                }
+            }
+            i64 q = 0;
+            for (i64 p = 0; p < used;) {
+                const i64 j = flip(iw[p++]);
+                if (j >= 0) {
+                    iw[q] = pe[j];
+                    pe[j] = q++;
+                    for (i64 t = 0; t < len[j] - 1; ++t) iw[q++] = iw[p++];
+                }
+            }
+            used = q;
+        }
+        // new element L_k: every variable reachable from k through its elements and
+        // its own variable list, each once (nv negated to mark membership)
+        i64 dk = 0;
+        nv[k] = -nvk;
+        i64 p = pe[k];
+        const i64 pk1 = elenk == 0 ? p : used;  // no elements: build in place
+        i64 pk2 = pk1;
+        for (i64 k1 = 1; k1 <= elenk + 1; ++k1) {
+            i64 e, pj, ln;
+            if (k1 > elenk) {
+                e = k;
+                pj = p;
+                ln = len[k] - elenk;
+            } else {
+                e = iw[p++];
+                pj = pe[e];
+                ln = len[e];
+            }
+            for (i64 k2 = 1; k2 <= ln; ++k2) {
+                const i64 i = iw[pj++];
+                const i64 nvi = nv[i];
+                if (nvi <= 0) continue;  // absorbed, or already in L_k
+                dk += nvi;
+                nv[i] = -nvi;
+                iw[pk2++] = i;
+                list_remove(i);
+            }
+            if (e != k) {  // element e is absorbed into k
+                pe[e] = flip(k);
+                w[e] = 0;
+            }
+        }
+        if (elenk != 0) used = pk2;
+        deg[k] = dk;
+        pe[k] = pk1;
+        len[k] = pk2 - pk1;
+        elen[k] = -2;  // k is an element now
+        // |L_e \ L_k| for every element e adjacent to a variable of L_k: w[e] - mark
+        mark = wclear(mark);
+        for (i64 pk = pk1; pk < pk2; ++pk) {
+            const i64 i = iw[pk];
+            const i64 eln = elen[i];
+            if (eln <= 0) continue;
+            const i64 nvi = -nv[i];
+            const i64 wnvi = mark - nvi;
+            for (i64 q = pe[i]; q <= pe[i] + eln - 1; ++q) {
+                const i64 e = iw[q];
+                if (w[e] >= mark)
+                    w[e] -= nvi;
+                else if (w[e] != 0)
+                    w[e] = deg[e] + wnvi;
+            }
+        }
+        // approximate degrees of the variables of L_k; prune absorbed elements
+        for (i64 pk = pk1; pk < pk2; ++pk) {
+            const i64 i = iw[pk];
+            const i64 p1 = pe[i], p2 = p1 + elen[i] - 1;
+            i64 pn = p1, h = 0, d = 0;
+            for (i64 q = p1; q <= p2; ++q) {
+                const i64 e = iw[q];
+                if (w[e] == 0) continue;
+                const i64 dext = w[e] - mark;
+                if (dext > 0) {
+                    d += dext;
+                    iw[pn++] = e;
+                    h += e;
+                } else {  // aggressive absorption: L_e is inside L_k
+                    pe[e] = flip(k);
+                    w[e] = 0;
+                }
+            }
+            elen[i] = pn - p1 + 1;  // + the new element k
+            const i64 p3 = pn, p4 = p1 + len[i];
+            for (i64 q = p2 + 1; q < p4; ++q) {  // variables still in i's list
+                const i64 j = iw[q];
+                const i64 nvj = nv[j];
+                if (nvj <= 0) continue;  // absorbed, or in L_k (covered by the element)
+                d += nvj;
+                iw[pn++] = j;
+                h += j;
+            }
+            if (d == 0) {  // mass elimination: i is adjacent to L_k only
+                pe[i] = flip(k);
+                const i64 nvi = -nv[i];
+                dk -= nvi;
+                nvk += nvi;
+                nel += nvi;
+                nv[i] = 0;
+                elen[i] = -1;
+            } else {
+                deg[i] = std::min(deg[i], d);
+                iw[pn] = iw[p3];  // element k goes first in i's list
+                iw[p3] = iw[p1];
+                iw[p1] = k;
+                len[i] = pn - p1 + 1;
+                h %= n;
+                nxt[i] = hhead[h];  // hash bucket (nxt / prv reused: i is off the degree lists)
+                hhead[h] = i;
+                prv[i] = h;
+            }
+        }
+        deg[k] = dk;
+        lemax = std::max(lemax, dk);
+        mark = wclear(mark + lemax);
+        // supervariables: variables of L_k with identical lists merge
+        for (i64 pk = pk1; pk < pk2; ++pk) {
+            i64 i = iw[pk];
+            if (nv[i] >= 0) continue;
+            const i64 h = prv[i];
+            i = hhead[h];
+            hhead[h] = -1;
+            for (; i != -1 && nxt[i] != -1; i = nxt[i], ++mark) {
+                const i64 ln = len[i], eln = elen[i];
+                for (i64 q = pe[i] + 1; q <= pe[i] + ln - 1; ++q) w[iw[q]] = mark;
+                i64 jlast = i;
+                for (i64 j = nxt[i]; j != -1;) {
+                    bool same = len[j] == ln && elen[j] == eln;
+                    for (i64 q = pe[j] + 1; same && q <= pe[j] + ln - 1; ++q)
+                        if (w[iw[q]] != mark) same = false;
+                    if (same) {  // j joins supervariable i
+                        pe[j] = flip(i);
+                        nv[i] += nv[j];
+                        nv[j] = 0;
+                        elen[j] = -1;
+                        j = nxt[j];
+                        nxt[jlast] = j;
+                    } else {
+                        jlast = j;
+                        j = nxt[j];
+                    }
+                }
+            }
+        }
+        // finish L_k: its live variables back on the degree lists
+        i64 pw = pk1;
+        for (i64 pk = pk1; pk < pk2; ++pk) {
+            const i64 i = iw[pk];
+            const i64 nvi = -nv[i];
+            if (nvi <= 0) continue;
+            nv[i] = nvi;
+            i64 d = deg[i] + dk - nvi;
+            d = std::min(d, n - nel - nvi);
+            list_insert(i, d);
+            mindeg = std::min(mindeg, d);
+            deg[i] = d;
+            iw[pw++] = i;
+        }
+        nv[k] = nvk;
+        if ((len[k] = pw - pk1) == 0) {  // an element with no variables: a tree root
+            pe[k] = -1;
+            w[k] = 0;
+        }
+        if (elenk != 0) used = pw;
+    }
+    // postorder the assembly tree read back from pe (parent = flip(pe)); absorbed
+    // variables follow their representative
+    for (i64 i = 0; i < n; ++i) pe[i] = flip(pe[i]);
+    std::fill(head.begin(), head.end(), -1);
+    for (i64 j = n - 1; j >= 0; --j) {  // absorbed variables: children of their representative (n: a root)
+        if (nv[j] > 0) continue;
+        nxt[j] = head[pe[j]];
+        head[pe[j]] = j;
+    }
+    for (i64 e = n; e >= 0; --e) {  // elements: children of their absorbing element
+        if (nv[e] <= 0) continue;
+        if (pe[e] != -1) {
+            nxt[e] = head[pe[e]];
+            head[pe[e]] = e;
+        }
+    }
+    std::vector<i64> stack;
+    std::vector<i32> order;
+    order.reserve((size_t)n + 1);
+    for (i64 r = 0; r <= n; ++r) {
+        if (pe[r] != -1) continue;  // not a root
+        stack.push_back(r);
+        while (!stack.empty()) {
+            const i64 v = stack.back();
+            const i64 c = head[v];
+            if (c == -1) {
+                stack.pop_back();
+                if (v != n) order.push_back((i32)v);
+            } else {
+                head[v] = nxt[c];
+                stack.push_back(c);
+            }
+        }
+    }
+    if ((i64)order.size() != n) return SC_ERR_ARG;  // cannot happen: every vertex is in the tree
+    std::copy(order.begin(), order.end(), perm);
     return SC_OK;
 }
 

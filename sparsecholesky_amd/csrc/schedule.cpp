@@ -431,8 +431,8 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
     // step's diagonal block when that block is a full 64-column block of the same slab and
     // the update runs on 64 x 64 tiles (span <= 128; K = 64 or 128)
     auto prefactor_ok = [&](int span, int k1, int slab1) {
-        return S.opt.panel_prefactor && S.opt.inner_order == 1 && S.opt.syrk_tile != 128 && span <= 2 * PNB &&
-               k1 + PNB <= slab1;
+        return S.opt.panel_prefactor && S.opt.inner_order == 1 && S.opt.syrk_tile != 128 &&
+               (span <= 2 * PNB || S.opt.panel_prefactor == 2) && k1 + PNB <= slab1;
     };
     // distributed assembly: one write-once tile-assembly launch of the front columns of
     // s that hosted rank v owns (its panel slabs and CB column blocks, D.col_owner), in

@@ -107,6 +107,8 @@ i64 analyze(i64 n, const i64* Ap, const i32* Ai, const sc_options& opt, Symbolic
 // Fill-reducing ordering (ordering.cpp): nested dissection by level structures,
 // perm[new] = old; and B = P A P^T as upper CSC with src[q] = A-index of entry q.
 i64 nd_order(i64 n, const i64* Ap, const i32* Ai, i32* perm);
+// Approximate minimum degree ordering (ordering.cpp), perm[new] = old.
+i64 amd_order(i64 n, const i64* Ap, const i32* Ai, i32* perm);
 void permute_upper(i64 n, const i64* Ap, const i32* Ai, const i32* perm, std::vector<i64>& Bp,
                    std::vector<i32>& Bi, std::vector<i64>& src);
 

@@ -315,17 +315,18 @@ def test_solve_vs_oracle(gpu, mtx, case):
     assert _backward_error(A, x, b) < 1e-14
 
 
+@pytest.mark.parametrize("ordering", [1, 2], ids=["nd", "amd"])
 @pytest.mark.parametrize("case", ["1138_bus", "lap16nat", "random"])
-def test_nd_ordering_factor_and_solve(gpu, mtx, case):
-    # with ordering=ND the GPU factors P A P^T; parity is defined on the
-    # permuted input (oracle chol of P A P^T), and solves take / return A's order
+def test_nd_ordering_factor_and_solve(gpu, mtx, case, ordering):
+    # with ordering=ND (or AMD) the GPU factors P A P^T; parity is defined on
+    # the permuted input (oracle chol of P A P^T), and solves take / return A's order
     if case == "1138_bus":
         A = mtx(case)
     elif case == "lap16nat":
         A = sc.laplacian3d(16, nd=False)
     else:
         A = random_spd(600, 0.01, 9)
-    s = sc.Symbolic(A, ordering=1)
+    s = sc.Symbolic(A, ordering=ordering)
     num = sc.Numeric(s)
     assert num.factor(A.x) == 0
     _, L = num.export()
@@ -334,7 +335,7 @@ def test_nd_ordering_factor_and_solve(gpu, mtx, case):
     assert st == 0
     assert np.array_equal(L.p, Lp) and np.array_equal(L.i, Li)
     assert rel_fro(L.x, Lx) < TOL
-    r = sc.chol(A, ordering=1)
+    r = sc.chol(A, ordering=ordering)
     assert r.has_value() and rel_fro(r.value().x, Lx) < TOL
     b = np.random.default_rng(4).standard_normal(A.size())
     x = num.solve(b)

@@ -147,10 +147,7 @@ def test_empty_and_single():
     assert s["nnz_L"] == 1 and s["n_supernodes"] == 1
 
 
-@pytest.mark.parametrize("name", ["1138_bus", "lap20nat", "random"])
-def test_nd_ordering_pattern_and_fill(mtx, name):
-    # the factor of P A P^T (nested dissection) has the oracle's pattern of
-    # P A P^T and less fill than the given order
+def _ordering_case(mtx, name):
     if name == "1138_bus":
         A = mtx(name)
     elif name == "lap20nat":
@@ -163,7 +160,16 @@ def test_nd_ordering_pattern_and_fill(mtx, name):
         A = sc.triplet_to_csc_matrix(np.concatenate([np.minimum(i, j), np.arange(n)]).astype(np.int32),
                                      np.concatenate([np.maximum(i, j), np.arange(n)]).astype(np.int32),
                                      np.concatenate([-np.ones(2000), np.full(n, 50.0)]), n)
-    s = sc.Symbolic(A, ordering=1)
+    return A
+
+
+@pytest.mark.parametrize("ordering", [1, 2], ids=["nd", "amd"])
+@pytest.mark.parametrize("name", ["1138_bus", "lap20nat", "random"])
+def test_nd_ordering_pattern_and_fill(mtx, name, ordering):
+    # the factor of P A P^T (nested dissection, or approximate minimum degree)
+    # has the oracle's pattern of P A P^T and less fill than the given order
+    A = _ordering_case(mtx, name)
+    s = sc.Symbolic(A, ordering=ordering)
     p = s.perm()
     assert np.array_equal(np.sort(p), np.arange(A.size()))
     B = sc.permute_symmetric(A, p)
@@ -173,3 +179,80 @@ def test_nd_ordering_pattern_and_fill(mtx, name):
     s0 = sc.Symbolic(A)
     assert s.nnz_L < s0.nnz_L and s.flops < s0.flops
     assert np.array_equal(s0.perm(), np.arange(A.size()))  # default: the given order
+
+
+def _arrow_plus_grid(n_grid=12, n_dense=3):
+    """2D 5-point grid plus n_dense rows coupled to every vertex (AMD's dense-row path)."""
+    k = n_grid
+    n = k * k + n_dense
+    ti, tj = list(range(n)), list(range(n))
+    tx = [float(n)] * n
+    for x in range(k):
+        for y in range(k):
+            v = x * k + y
+            for u in ((x + 1) * k + y if x + 1 < k else -1, v + 1 if y + 1 < k else -1):
+                if u >= 0:
+                    ti.append(v), tj.append(u), tx.append(-1.0)
+    for d in range(n_dense):
+        for v in range(k * k):
+            ti.append(v), tj.append(k * k + d), tx.append(-0.01)
+    return sc.triplet_to_csc_matrix(np.array(ti, np.int32), np.array(tj, np.int32), np.array(tx), n)
+
+
+@pytest.mark.parametrize("case", ["1138_bus", "lap16nat", "arrow", "disconnected", "duplicates", "diag"])
+def test_amd_ordering_properties(mtx, case):
+    # the approximate-minimum-degree ordering (ordering = SC_ORDER_AMD): a permutation,
+    # oracle pattern of P A P^T, fill no worse than the given order; dense rows ordered
+    # last; isolated vertices and duplicate entries handled
+    if case == "1138_bus":
+        A = mtx(case)
+    elif case == "lap16nat":
+        A = sc.laplacian3d(16, nd=False)
+    elif case == "arrow":
+        A = _arrow_plus_grid()
+    elif case == "disconnected":  # two grids and isolated vertices
+        B = sc.laplacian3d(6, nd=False)
+        n1 = B.size()
+        col = np.repeat(np.arange(n1), np.diff(B.p))
+        ti = np.concatenate([B.i, B.i + n1, np.arange(2 * n1, 2 * n1 + 5)]).astype(np.int32)
+        tj = np.concatenate([col, col + n1, np.arange(2 * n1, 2 * n1 + 5)]).astype(np.int32)
+        tx = np.concatenate([B.x, B.x, np.ones(5)])
+        A = sc.triplet_to_csc_matrix(ti, tj, tx, 2 * n1 + 5)
+    elif case == "duplicates":
+        g = _arrow_plus_grid(8, 0)
+        col = np.repeat(np.arange(g.size()), np.diff(g.p))
+        A = sc.csc_matrix(g.size(), g.size(), *_dup_cols(g.p, g.i, g.x))
+    else:
+        A = sc.triplet_to_csc_matrix(np.arange(7, dtype=np.int32), np.arange(7, dtype=np.int32), np.ones(7), 7)
+    s = sc.Symbolic(A, ordering=2)
+    p = s.perm()
+    n = A.size()
+    assert np.array_equal(np.sort(p), np.arange(n))
+    B = sc.permute_symmetric(A, p)
+    Lp, Li = s.pattern()
+    Op, Oi, _ = oracle.schol(B)
+    assert np.array_equal(Lp, Op) and np.array_equal(Li, Oi)
+    s0 = sc.Symbolic(A)
+    assert s.nnz_L <= s0.nnz_L
+    if case == "arrow":  # the dense rows come last
+        assert set(p[-3:].tolist()) == {n - 3, n - 2, n - 1}
+    if case == "1138_bus":  # a power network: minimum degree leaves almost no fill
+        assert s.nnz_L < 4000 < sc.Symbolic(A, ordering=1).nnz_L
+
+
+def _dup_cols(Ap, Ai, Ax):
+    """Every stored entry twice (the second copy is the one the reference keeps)."""
+    p = [0]
+    i, x = [], []
+    for j in range(len(Ap) - 1):
+        for q in range(Ap[j], Ap[j + 1]):
+            i += [Ai[q], Ai[q]]
+            x += [Ax[q] * 0.5, Ax[q]]
+        p.append(len(i))
+    return np.array(p, np.int64), np.array(i, np.int32), np.array(x)
+
+
+def test_ordering_value_checked():
+    A = sc.laplacian3d(4)
+    with pytest.raises(Exception):
+        sc.Symbolic(A, ordering=7)
