@@ -22,8 +22,8 @@
 //   owner of s, parent here CB(s)                        [L, Lp]
 //   owner of s, parent away CB(s), sent after level L    [L, L+1]
 //   parent's owner          CB(c) of a remote child c     [Lc, Lp] (received)
-//   CB rank of split s      its column blocks (compact)  [L, L+1]; in place in a
-//                           full-square CB(s) when it also owns the parent
+//   CB rank of split s      the column range of its blocks [L, L+1] (round 6: the range a
+//                           rank touches, not the whole square; ld stays mb)
 //                           R_LAND(s) (the L21 slabs)     [L, L+1]
 //   holder of distributed s a full panel copy in the panel arena (permanent: its
 //                           slabs are part of the factor; gathered for export)
@@ -132,6 +132,44 @@ int64_t place(std::vector<Req>& reqs, int64_t* live_max) {
     return peak;
 }
 
+// Greedy by size (largest region first, each at the lowest offset free over its whole
+// lifetime) for the regions of at least `big` doubles, then the sweep above for the rest
+// placed on top of them.  Returns the arena size.
+int64_t place_by_size(std::vector<Req>& reqs, int64_t big) {
+    std::vector<size_t> large, small;
+    for (size_t i = 0; i < reqs.size(); ++i) (reqs[i].size >= big ? large : small).push_back(i);
+    std::stable_sort(large.begin(), large.end(), [&](size_t a, size_t b) { return reqs[a].size > reqs[b].size; });
+    int32_t tmax = 0;
+    for (const Req& r : reqs) tmax = std::max(tmax, r.t1);
+    // per level: placed (offset, end) intervals, sorted by offset
+    std::vector<std::vector<std::pair<int64_t, int64_t>>> at((size_t)tmax + 1);
+    int64_t top = 0;
+    std::vector<std::pair<int64_t, int64_t>> busy;
+    for (size_t i : large) {
+        Req& r = reqs[i];
+        busy.clear();
+        for (int32_t t = r.t0; t <= r.t1; ++t) busy.insert(busy.end(), at[t].begin(), at[t].end());
+        std::sort(busy.begin(), busy.end());
+        int64_t off = 0;
+        for (const auto& b : busy) {
+            if (b.first >= off + r.size) break;  // the gap before b fits
+            off = std::max(off, b.second);
+        }
+        *r.out = off;
+        top = std::max(top, off + r.size);
+        for (int32_t t = r.t0; t <= r.t1; ++t) {
+            auto& v = at[t];
+            v.insert(std::upper_bound(v.begin(), v.end(), std::make_pair(off, off + r.size)), {off, off + r.size});
+        }
+    }
+    std::vector<Req> rest;
+    for (size_t i : small) rest.push_back(reqs[i]);
+    const int64_t base = align_up(top);
+    const int64_t peak = place(rest, nullptr);
+    for (size_t i : small) *reqs[i].out += base;
+    return base + peak;
+}
+
 }  // namespace
 
 int64_t plan_rank_panels(const Symbolic& S, const DistPlan* D, int rank, std::vector<int64_t>& panel_off) {
@@ -151,6 +189,7 @@ int64_t plan_rank_memory(const Symbolic& S, const DistPlan* D, int rank, RankMem
     R.rank = rank;
     R.panel_off.assign((size_t)ns, -1);
     R.cb_off.assign((size_t)ns, -1);
+    R.cb_col0.assign((size_t)ns, 0);
     R.land_off.assign((size_t)ns, -1);
     auto owner = [&](i32 s) { return D ? D->owner[s] : 0; };
     R.panel_total = plan_rank_panels(S, D, rank, R.panel_off);
@@ -165,20 +204,64 @@ int64_t plan_rank_memory(const Symbolic& S, const DistPlan* D, int rank, RankMem
             req(sq, L, Lp, &R.cb_off[s]);
             continue;
         }
-        // a full-square CB(s) wherever part of it is computed (until it is sent after
-        // level L) or received for the parent's assembly (until level Lp)
+        // CB(s) wherever part of it is computed (until it is sent after level L) or
+        // received for the parent's assembly (until level Lp): only the column range the
+        // rank touches -- a CB rank's column blocks, a receiver's columns that map into the
+        // parent columns it assembles (ld stays mb, so every kernel addresses it as the square)
         const bool prod = D->produces_cb(S, s, rank), recv = D->receives(S, s, rank);
-        if (recv)
-            req(sq, L, Lp, &R.cb_off[s]);
-        else if (prod)
-            req(sq, L, L + 1, &R.cb_off[s]);
+        if (!prod && !recv) continue;
+        int64_t lo = mb, hi = 0;
+        auto all = [&]() {
+            lo = 0;
+            hi = mb;
+        };
+        if (prod) {
+            if (D->split[s] < 0 || (owner(s) == rank && !D->dasm[s])) {
+                all();
+            } else {
+                const std::vector<i32>& cbr = D->cb_rank[D->split[s]];
+                for (int jb = 0; jb < (int)cbr.size(); ++jb)
+                    if (cbr[jb] == rank) {
+                        lo = std::min<int64_t>(lo, (int64_t)jb * D->cbb);
+                        hi = std::max<int64_t>(hi, std::min<int64_t>(mb, (int64_t)(jb + 1) * D->cbb));
+                    }
+            }
+        }
+        if (recv) {
+            if (!D->dasm[p]) {
+                all();
+            } else {
+                const i32* rel = S.relind.data() + S.rel_ptr[s];
+                for (int64_t j = 0; j < mb; ++j)
+                    if (D->col_owner(S, p, rel[j]) == rank) {
+                        lo = std::min(lo, j);
+                        hi = std::max(hi, j + 1);
+                    }
+            }
+        }
+        if (hi <= lo) all();  // cannot happen: a producer or receiver touches some column
+        R.cb_col0[s] = (i32)lo;
+        req((hi - lo) * mb, L, recv ? Lp : L + 1, &R.cb_off[s]);
         bool cbrank = false;
         if (D->split[s] >= 0)
             for (i32 r : D->cb_rank[D->split[s]]) cbrank |= r == rank;
         if (cbrank && D->pd[s] < 0 && owner(s) != rank)  // L21 slabs (a distributed panel: its copy)
             req(mb * S.w(s), L, L + 1, &R.land_off[s]);
     }
-    R.work_total = place(reqs, &R.work_live_max);
+    // two placements, the smaller arena kept: the level sweep (best fit, regions born at a
+    // level placed largest first), and greedy by size for the regions >= 1 MB (the sweep
+    // for the small rest on top); offsets are static either way
+    std::vector<int64_t> sweep_off(reqs.size());
+    {
+        std::vector<Req> r2 = reqs;
+        for (size_t i = 0; i < r2.size(); ++i) r2[i].out = &sweep_off[i];
+        R.work_total = place(r2, &R.work_live_max);
+    }
+    const int64_t gsz = place_by_size(reqs, 1 << 17);
+    if (gsz < R.work_total)
+        R.work_total = gsz;
+    else
+        for (size_t i = 0; i < reqs.size(); ++i) *reqs[i].out = sweep_off[i];
     if (placed)
         for (const Req& q : reqs) placed->push_back({*q.out, q.size, q.t0, q.t1});
     return SC_OK;
@@ -241,10 +324,10 @@ bool region_addr(const Symbolic& S, const DistPlan* D, const RankMem& R, int kin
             off = R.land_off[s] + (int64_t)col * ld + row;
             return true;
         case R_CB:
-            if (R.cb_off[s] < 0) return false;
+            if (R.cb_off[s] < 0 || col < R.cb_col0[s]) return false;
             arena = 1;
             ld = S.mb(s);
-            off = R.cb_off[s] + (int64_t)col * ld + row;
+            off = R.cb_base(S, s) + (int64_t)col * ld + row;
             return true;
     }
     (void)D;

@@ -188,7 +188,11 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
         int64_t* dp = nullptr;
         if ((rc = upload(N, R.panel_off, dp))) return fail(rc);
         R.P.panel_off = dp;
-        if ((rc = upload(N, R.cb_off, dp))) return fail(rc);
+        // the kernels address a CB as the full square from its (virtual) origin
+        std::vector<int64_t> base((size_t)S.ns, 0);
+        for (int32_t s = 0; s < S.ns; ++s)
+            if (R.cb_off[s] >= 0) base[s] = R.cb_base(S, s);
+        if ((rc = upload(N, base, dp))) return fail(rc);
         R.P.cb_off = dp;
     }
     if (!multi || N.emulated) N.gpanel = pbase;  // gathered layout == the arenas

@@ -111,7 +111,12 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D);
 struct RankMem {
     int32_t rank = 0;
     std::vector<int64_t> panel_off;  // per supernode: doubles into the panel arena, -1 = not here
-    std::vector<int64_t> cb_off;     // per supernode: full-square CB in the work arena, -1
+    std::vector<int64_t> cb_off;     // per supernode: the CB region in the work arena, -1 = not here
+    // per supernode: first CB column the region holds (columns [cb_col0, ...) of the mb x mb
+    // square, ld = mb): a rank computing or receiving only some column blocks of a shared
+    // front's CB keeps just their column range; cb_base() is the square's (virtual) origin
+    std::vector<int32_t> cb_col0;
+    int64_t cb_base(const Symbolic& S, int32_t s) const { return cb_off[s] - (int64_t)cb_col0[s] * S.mb(s); }
     std::vector<int64_t> land_off;   // per supernode: R_LAND slab (ld = mb) in the work arena, -1
     int64_t panel_total = 0;     // doubles (incl. the PNB tail the TRSM reads past)
     int64_t work_total = 0;      // doubles: high-water mark of the interval plan

@@ -414,7 +414,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                         N.err = "schedule: gathered child CB not resident on its parent's rank";
                         continue;
                     }
-                    g.cb = R.P.cb_pool + R.cb_off[c];
+                    g.cb = R.P.cb_pool + R.cb_base(S, c);
                     g.rel = R.P.relind + S.rel_ptr[c];
                     g.mbc = mbc;
                     B.gseg.push_back(g);
@@ -719,7 +719,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             const int w = S.w(s), m = S.sn_m[s], mb = m - w;
             for (int j0 = 0; j0 < mb; j0 += D.early_gw) {
                 GemmTask t {};
-                t.C = cb_pool + coff[s] + (int64_t)j0 * mb + j0;
+                t.C = cb_pool + N.R[v].cb_base(S, s) + (int64_t)j0 * mb + j0;
                 t.A = panel_pool + poff[s] + w + j0;
                 t.ldc = mb;
                 t.lda = m;
@@ -739,7 +739,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 const int w = S.w(s), m = S.sn_m[s], mb = m - w;
                 if (mb <= 0 || (w >= 256) != (big == 1) || is_split(s) || is_early_sender(s, v)) continue;
                 GemmTask t {};
-                t.C = cb_pool + coff[s];
+                t.C = cb_pool + N.R[v].cb_base(S, s);
                 t.A = panel_pool + poff[s] + w;
                 t.ldc = mb;
                 t.lda = m;
