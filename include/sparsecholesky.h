@@ -113,6 +113,10 @@ typedef struct sc_options {
     int32_t dist_pieces;     /* multi-GPU distributed panels: each final slab is handed over in this many column
                                 pieces (default 4: 256 of a 1024-column slab), each sent as soon as the chain has
                                 finished it, so the next slab's owner starts updating before the slab is done */
+    int32_t outer_pieces;    /* single device, lookahead = 1: at a slab end the next slab's update goes in this
+                                many column pieces: the first on the main stream, the rest on the lookahead stream
+                                ahead of the trailing update, each waited for just before the next slab's chain
+                                reaches its columns (default 1: the whole next slab on the main stream) */
     int32_t panel_prefactor; /* 1 (default): in the 64-column panel chain, the recursive inner update after a step
                                 (K = 64 or 128) also forms and factors the NEXT step's 64 x 64 diagonal block in one
                                 extra workgroup, so that step's TRSM loads L11 instead of every TRSM workgroup

@@ -505,7 +505,6 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         double* panel_pool = N.R[v].P.panel_pool;
         double* cb_pool = N.R[v].P.cb_pool;
         const std::vector<int64_t>& poff = N.R[v].panel_off;
-        const std::vector<int64_t>& coff = N.R[v].cb_off;
         // small fronts: one launch sized for the level's largest front when the level
         // fits one workgroup per CU (fewer dependent launches on thin levels), else one
         // launch per LDS bucket (small fronts keep their occupancy on wide levels)
@@ -599,6 +598,18 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // fronts whose block at the current step was pre-factored by the previous step's
         // inner update (panel_prefactor): their TRSM loads L11 (trsm_panel_g_kernel<2>)
         std::vector<char> pre((size_t)S.ns, 0);
+        // outer_pieces: the next slab's update at a slab end in column pieces; piece 0 on
+        // the main stream, the others on the lookahead stream ahead of the trailing update,
+        // each waited for by the main stream just before a launch touches its columns
+        const int npieces = S.opt.lookahead ? std::max(1, std::min(S.opt.outer_pieces, NBO / PNB)) : 1;
+        const int PW = (NBO / npieces + PNB - 1) / PNB * PNB;
+        std::vector<std::pair<int, int>> pend;  // (first column, event) of lookahead-stream pieces
+        auto wait_pieces = [&](int hi) {
+            while (!pend.empty() && pend.front().first < hi) {
+                push_wait(0, pend.front().second);
+                pend.erase(pend.begin());
+            }
+        };
         for (int k0 = 0; k0 < maxw; k0 += PNB) {
             Launch Lp {};
             Lp.kind = L_POTRF;
@@ -611,6 +622,9 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             Lt.vr = v;
             Lt.off = (int64_t)trsm.size();
             std::vector<GemmTask> upd, outer_a, outer_b;
+            std::vector<std::vector<GemmTask>> outer_p((size_t)npieces);  // outer_a pieces 1.. (lookahead stream)
+            std::vector<double> pfl((size_t)npieces, 0.0);
+            int uhi = 0;  // columns the step's inner update writes: [.., uhi)
             std::vector<TrsmTask> trsm_part;   // partial last blocks: own launch (big = 1)
             std::vector<TrsmTask> trsm_split;  // full blocks factored by the POTRF launch (own launch)
             // a step whose fused launch would exceed trsm_split_wg workgroups (more than the GPU
@@ -652,21 +666,27 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     const int b = (k0 - slab0) / PNB;
                     const int span = PNB << __builtin_ctz((unsigned)(b + 1));
                     add_update(upd, uflops, pan, m, m, k1, std::min(slab1, k1 + span), k1 - span, k1);
+                    uhi = std::max(uhi, std::min(slab1, k1 + span));
                     if (prefactor_ok(span, k1, slab1)) {
                         upd.back().pf = S.sn_start[s] + k1;
                         pre[s] = 1;
                     }
                 } else if (k1 < slab1) {
                     add_update(upd, uflops, pan, m, m, k1, slab1, k0, k1);
+                    uhi = std::max(uhi, slab1);
                 }
                 if (k1 == slab1 && slab1 < w) {
                     // outer_a is the last update of block slab1: a pending stream-1 outer
                     // update of those columns is waited for before outer_a runs
                     const int nxt = S.opt.lookahead ? std::min(w, slab1 + NBO) : w;
-                    add_update(outer_a, afl, pan, m, m, slab1, nxt, slab0, slab1);
+                    add_update(outer_a, afl, pan, m, m, slab1, std::min(nxt, slab1 + PW), slab0, slab1);
+                    for (int q = 1; q < npieces; ++q)
+                        add_update(outer_p[q], pfl[q], pan, m, m, slab1 + q * PW, std::min(nxt, slab1 + (q + 1) * PW),
+                                   slab0, slab1);
                     add_update(outer_b, bfl, pan, m, m, nxt, w, slab0, slab1);
                 }
             }
+            wait_pieces(k0 + PNB);  // the step's block columns
             Lp.count = (int32_t)((int64_t)potrf.size() - Lp.off);
             Lt.count = (int32_t)((int64_t)trsm.size() - Lt.off);
             if (Lp.count > 0) N.sched.push_back(Lp);
@@ -687,6 +707,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 trsm.insert(trsm.end(), trsm_part.begin(), trsm_part.end());
                 N.sched.push_back(Lq);
             }
+            wait_pieces(uhi);  // the inner update's columns
             push_gemm_launch(L_PANEL, lev, upd, 0, uflops);
             // split fronts: a slab is final after the TRSM of its last block; at a slab end
             // no inner update is pending
@@ -697,7 +718,9 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 if (k1 == w || k1 % D.nbo == 0) emit_slab(s, k0 / D.nbo);
             }
             int e_trsm = -1;
-            if (!outer_b.empty()) e_trsm = push_record(0);
+            bool any_p = false;
+            for (int q = 1; q < npieces; ++q) any_p |= !outer_p[q].empty();
+            if (!outer_b.empty() || any_p) e_trsm = push_record(0);
             if (!outer_a.empty()) {
                 if (b_pending >= 0) {
                     push_wait(0, b_pending);
@@ -705,12 +728,22 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 }
                 push_gemm_launch(L_PANEL, lev, outer_a, 0, afl);
             }
+            if (any_p) {  // the next slab's other pieces, ahead of the trailing update
+                push_wait(1, e_trsm);
+                const int c_next = (k0 / NBO + 1) * NBO;
+                for (int q = 1; q < npieces; ++q) {
+                    if (outer_p[q].empty()) continue;
+                    push_gemm_launch(L_PANEL, lev, outer_p[q], 0, pfl[q], 1);
+                    pend.push_back({c_next + q * PW, push_record(1)});
+                }
+            }
             if (!outer_b.empty()) {
                 push_wait(1, e_trsm);
                 push_gemm_launch(L_PANEL, lev, outer_b, 0, bfl, 1);
                 b_pending = push_record(1);
             }
         }
+        wait_pieces(INT32_MAX);
         if (b_pending >= 0) push_wait(0, b_pending);
         // early-delivery children: the CB SYRK in column groups, an event after each
         // (the group's comm sub-step waits for exactly that event)
