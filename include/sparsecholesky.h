@@ -113,6 +113,10 @@ typedef struct sc_options {
     int32_t dist_pieces;     /* multi-GPU distributed panels: each final slab is handed over in this many column
                                 pieces (default 4: 256 of a 1024-column slab), each sent as soon as the chain has
                                 finished it, so the next slab's owner starts updating before the slab is done */
+    int32_t dist_deliver_split; /* multi-GPU, distributed assembly: each level's delivery of child CB columns goes
+                                in two sub-steps, the columns mapping into parent PANEL columns first (the next
+                                level's chains wait only for those), then those mapping into parent CB columns
+                                (assembled and updated on the lookahead stream) (default 1) */
     int32_t outer_pieces;    /* single device, lookahead = 1: at a slab end the next slab's update goes in this
                                 many column pieces: the first on the main stream, the rest on the lookahead stream
                                 ahead of the trailing update, each waited for just before the next slab's chain

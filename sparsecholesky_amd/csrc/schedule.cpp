@@ -100,7 +100,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
     auto is_dpanel = [&](int32_t s) { return multi && D.pd[s] >= 0; };
     std::vector<int32_t> hosted_of((size_t)std::max(N.nranks, 1), -1);  // rank -> index into N.R
     for (size_t v = 0; v < N.R.size(); ++v) hosted_of[N.R[v].rank] = (int32_t)v;
-    std::vector<int32_t> init_step, deliver_step((size_t)S.nlevels, -1);
+    std::vector<int32_t> init_step, deliver_step((size_t)S.nlevels, -1), deliver_cb_step((size_t)S.nlevels, -1);
     // early children: early_step[c][g] = the DELIVER step of column group g (-1: none; a
     // group whose columns all stay on the producer has no messages and no step)
     std::vector<std::vector<int32_t>> early_step;
@@ -122,7 +122,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 if ((int)ks[t.k].size() <= t.p) ks[t.k].resize((size_t)t.p + 1, -1);
                 ks[t.k][t.p] = id;
             }
-            if (t.kind == STEP_DELIVER && t.s < 0) deliver_step[t.level] = id;
+            if (t.kind == STEP_DELIVER && t.s < 0) (t.k == 0 ? deliver_step : deliver_cb_step)[t.level] = id;
             if (t.kind == STEP_DELIVER && t.s >= 0) {
                 auto& es = early_step[t.s];
                 if ((int)es.size() <= t.k) es.resize((size_t)t.k + 1, -1);
@@ -438,7 +438,12 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
     // s that hosted rank v owns (its panel slabs and CB column blocks, D.col_owner), in
     // 16-column blocks; a block straddling another rank's columns computes those too,
     // into this rank's private copy, where nothing reads them
-    auto emit_region_asm = [&](int32_t lev, int32_t s, int v) {
+    // dist_deliver_split: the parent columns [lo, hi) of one launch -- the panel columns on
+    // the main stream (the chains wait for them only), the CB columns on the lookahead
+    // stream after the level's CB-column delivery (sub-step k = 1)
+    std::vector<std::vector<int>> cbasm_ev;  // per hosted rank, per supernode: event after its CB-column assembly
+    std::vector<int> level_cbasm;           // this level's such events (joined before its deliveries)
+    auto region_asm_launch = [&](int32_t lev, int32_t s, int v, int lo, int hi, int strm) {
         const int who = N.R[v].rank, m = S.sn_m[s];
         Launch L {};
         L.kind = L_ASM;
@@ -446,10 +451,11 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         L.vr = v;
         L.big = 1;
         L.epi = 1;  // the tasks carry column limits (B.asml)
+        L.strm = strm;
         L.off = (int64_t)asmv.size();
-        for (int cb = 0; cb * ASM_COLS < m; ++cb) {
-            const int c1 = std::min(m, (cb + 1) * ASM_COLS);
-            for (int a = cb * ASM_COLS; a < c1;) {  // each run of owned columns of the block
+        for (int cb = lo / ASM_COLS; cb * ASM_COLS < hi; ++cb) {
+            const int c1 = std::min(hi, (cb + 1) * ASM_COLS);
+            for (int a = std::max(lo, cb * ASM_COLS); a < c1;) {  // each run of owned columns of the block
                 if (D.col_owner(S, s, a) != who) {
                     ++a;
                     continue;
@@ -466,6 +472,25 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         }
         L.count = (int32_t)((int64_t)asmv.size() - L.off);
         if (L.count > 0) N.sched.push_back(L);
+        return L.count > 0;
+    };
+    auto emit_region_asm = [&](int32_t lev, int32_t s, int v) {
+        const int m = S.sn_m[s], w = S.w(s);
+        if (!S.opt.dist_deliver_split || m == w) {
+            region_asm_launch(lev, s, v, 0, m, 0);
+            return;
+        }
+        region_asm_launch(lev, s, v, 0, w, 0);
+        const int e0 = push_record(0);  // the rank's own children's CBs (main stream) are done
+        const size_t mark = N.sched.size();
+        push_wait(1, e0);
+        if (region_asm_launch(lev, s, v, w, m, 1)) {
+            if (cbasm_ev.empty()) cbasm_ev.assign(N.R.size(), std::vector<int>((size_t)S.ns, -1));
+            cbasm_ev[v][s] = push_record(1);
+            level_cbasm.push_back(cbasm_ev[v][s]);
+        } else {
+            N.sched.resize(mark);  // no CB columns here: drop the wait
+        }
     };
     // CB rank (hosted index v) of split front s: per final panel slab, CB -= L21_k
     // L21_k^T on the column blocks it owns (K = slab width), from its R_LAND copy
@@ -473,10 +498,12 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         const int who = N.R[v].rank;
         const std::vector<int32_t>& cbr = D.cb_rank[D.split[s]];
         const int w = S.w(s), m = S.sn_m[s], mb = m - w;
-        if (is_dasm(s))
+        if (is_dasm(s)) {
             emit_region_asm(lev, s, v);  // its own CB blocks, from the children's columns it received
-        else
+            if (!cbasm_ev.empty() && cbasm_ev[v][s] >= 0) push_wait(0, cbasm_ev[v][s]);  // (the updates below: main stream)
+        } else {
             emit_step(init_step[s]);
+        }
         for (int k0 = 0, k = 0; k0 < w; k0 += D.nbo, ++k) {
             const int k1 = std::min(w, k0 + D.nbo);
             emit_slab(s, k);
@@ -1147,7 +1174,10 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 if (g < (int)early_step[c].size())
                     emit_step(early_step[c][g], vs >= 0 && !early_ev[c].empty() ? early_ev[c][g] : -1);
         }
+        for (int e : level_cbasm) push_wait(0, e);  // CB columns assembled on the lookahead stream
+        level_cbasm.clear();
         emit_step(deliver_step[lev]);
+        emit_step(deliver_cb_step[lev], -1, 1);  // CB-column delivery: the lookahead stream waits for it
         comm_done[lev] = push_record(2);
     }
     if (multi) push_wait(0, push_record(2));  // join the comm stream (its last sends)
