@@ -117,6 +117,10 @@ typedef struct sc_options {
                                 in two sub-steps, the columns mapping into parent PANEL columns first (the next
                                 level's chains wait only for those), then those mapping into parent CB columns
                                 (assembled and updated on the lookahead stream) (default 1) */
+    int32_t la_next;         /* single device, lookahead = 1: 1 splits each slab end's lookahead-stream update into
+                                the slab after next (which the next slab end's main-stream update waits for) and
+                                the rest (which trails behind on the lookahead stream); 0 (default): one launch,
+                                waited for whole */
     int32_t outer_pieces;    /* single device, lookahead = 1: at a slab end the next slab's update goes in this
                                 many column pieces: the first on the main stream, the rest on the lookahead stream
                                 ahead of the trailing update, each waited for just before the next slab's chain

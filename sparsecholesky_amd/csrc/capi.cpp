@@ -96,6 +96,7 @@ void sc_default_options(sc_options* opt) {
     opt->dist_asm = 1;
     opt->dist_pieces = 4;
     opt->dist_deliver_split = 1;
+    opt->la_next = 0;
     opt->outer_pieces = 1;
     opt->panel_prefactor = 1;
 }

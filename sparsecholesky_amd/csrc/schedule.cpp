@@ -607,6 +607,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // (stream 1), which overlaps the next slab's factorization.  A later outer
         // update of overlapping columns waits for the stream-1 work first.
         int b_pending = -1;
+        int b_rest = -1;  // la_next: the trailing part of the last split outer_b
         // rows [c_lo, r_hi) of columns [c_lo, c_hi) -= their product over columns [ka, kb)
         auto add_update = [&](std::vector<GemmTask>& vec, double& fl, double* pan, int m, int r_hi, int c_lo, int c_hi,
                               int ka, int kb) {
@@ -650,6 +651,8 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             Lt.off = (int64_t)trsm.size();
             std::vector<GemmTask> upd, outer_a, outer_b;
             std::vector<std::vector<GemmTask>> outer_p((size_t)npieces);  // outer_a pieces 1.. (lookahead stream)
+            std::vector<GemmTask> outer_b1;  // la_next: the slab after next, split off outer_b
+            double b1fl = 0.0;
             std::vector<double> pfl((size_t)npieces, 0.0);
             int uhi = 0;  // columns the step's inner update writes: [.., uhi)
             std::vector<TrsmTask> trsm_part;   // partial last blocks: own launch (big = 1)
@@ -710,7 +713,13 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     for (int q = 1; q < npieces; ++q)
                         add_update(outer_p[q], pfl[q], pan, m, m, slab1 + q * PW, std::min(nxt, slab1 + (q + 1) * PW),
                                    slab0, slab1);
-                    add_update(outer_b, bfl, pan, m, m, nxt, w, slab0, slab1);
+                    if (S.opt.la_next && S.opt.lookahead) {
+                        const int nxt2 = std::min(w, nxt + NBO);
+                        add_update(outer_b1, b1fl, pan, m, m, nxt, nxt2, slab0, slab1);
+                        add_update(outer_b, bfl, pan, m, m, nxt2, w, slab0, slab1);
+                    } else {
+                        add_update(outer_b, bfl, pan, m, m, nxt, w, slab0, slab1);
+                    }
                 }
             }
             wait_pieces(k0 + PNB);  // the step's block columns
@@ -747,7 +756,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             int e_trsm = -1;
             bool any_p = false;
             for (int q = 1; q < npieces; ++q) any_p |= !outer_p[q].empty();
-            if (!outer_b.empty() || any_p) e_trsm = push_record(0);
+            if (!outer_b.empty() || !outer_b1.empty() || any_p) e_trsm = push_record(0);
             if (!outer_a.empty()) {
                 if (b_pending >= 0) {
                     push_wait(0, b_pending);
@@ -764,13 +773,21 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     pend.push_back({c_next + q * PW, push_record(1)});
                 }
             }
+            if (!outer_b1.empty()) {  // la_next: the next outer_a waits for this part only
+                push_wait(1, e_trsm);
+                push_gemm_launch(L_PANEL, lev, outer_b1, 0, b1fl, 1);
+                b_pending = push_record(1);
+            }
             if (!outer_b.empty()) {
                 push_wait(1, e_trsm);
                 push_gemm_launch(L_PANEL, lev, outer_b, 0, bfl, 1);
-                b_pending = push_record(1);
+                const int eb = push_record(1);
+                if (outer_b1.empty()) b_pending = eb;
+                else b_rest = eb;
             }
         }
         wait_pieces(INT32_MAX);
+        if (b_rest >= 0) push_wait(0, b_rest);
         if (b_pending >= 0) push_wait(0, b_pending);
         // early-delivery children: the CB SYRK in column groups, an event after each
         // (the group's comm sub-step waits for exactly that event)
