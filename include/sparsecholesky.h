@@ -113,24 +113,11 @@ typedef struct sc_options {
     int32_t dist_pieces;     /* multi-GPU distributed panels: each final slab is handed over in this many column
                                 pieces (default 4: 256 of a 1024-column slab), each sent as soon as the chain has
                                 finished it, so the next slab's owner starts updating before the slab is done */
-    int32_t dist_deliver_split; /* multi-GPU, distributed assembly: each level's delivery of child CB columns goes
-                                in two sub-steps, the columns mapping into parent PANEL columns first (the next
-                                level's chains wait only for those), then those mapping into parent CB columns
-                                (assembled and updated on the lookahead stream) (default 1) */
-    int32_t la_next;         /* single device, lookahead = 1: 1 splits each slab end's lookahead-stream update into
-                                the slab after next (which the next slab end's main-stream update waits for) and
-                                the rest (which trails behind on the lookahead stream); 0 (default): one launch,
-                                waited for whole */
-    int32_t outer_pieces;    /* single device, lookahead = 1: at a slab end the next slab's update goes in this
-                                many column pieces: the first on the main stream, the rest on the lookahead stream
-                                ahead of the trailing update, each waited for just before the next slab's chain
-                                reaches its columns (default 1: the whole next slab on the main stream) */
     int32_t panel_prefactor; /* 1 (default): in the 64-column panel chain, the recursive inner update after a step
                                 (K = 64 or 128) also forms and factors the NEXT step's 64 x 64 diagonal block in one
                                 extra workgroup, so that step's TRSM loads L11 instead of every TRSM workgroup
                                 factoring it (the POTRF runs beside the update's tiles, off the chain's critical
-                                path; bitwise-identical factor); 2: also after the K = 256 / 512 inner updates
-                                (their launches then run on 64 x 64 tiles); 0: every full step fuses its POTRF */
+                                path; bitwise-identical factor); 0: every full step fuses its POTRF */
 } sc_options;
 
 enum { SC_ORDER_NATURAL = 0, SC_ORDER_ND = 1, SC_ORDER_AMD = 2 };

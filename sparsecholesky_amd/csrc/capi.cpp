@@ -95,9 +95,6 @@ void sc_default_options(sc_options* opt) {
     opt->tiny_dense = 1;
     opt->dist_asm = 1;
     opt->dist_pieces = 4;
-    opt->dist_deliver_split = 1;
-    opt->la_next = 0;
-    opt->outer_pieces = 1;
     opt->panel_prefactor = 1;
 }
 

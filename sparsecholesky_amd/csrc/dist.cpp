@@ -377,23 +377,18 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
         // parent columns they map into: the parent's owner, or, distributed assembly,
         // each run of consecutive columns to the owner of its parent slab / CB block
         // (rows from the run's first column down; a run on src itself stays put)
-        // split (dist_deliver_split, distributed assembly): a run whose parent columns
-        // cross the parent's panel / CB boundary goes in two messages, the panel part to
-        // `out`, the CB part to `out_cb` (a later sub-step)
-        auto deliver_cols = [&](std::vector<DistMsg>& out, std::vector<DistMsg>* out_cb, i32 c, int src, int j0,
-                                int j1) {
+        auto deliver_cols = [&](int32_t id, i32 c, int src, int j0, int j1) {
             const i32 p = S.sn_parent[c];
-            const int mbc = S.mb(c), wp = S.w(p);
+            const int mbc = S.mb(c);
             const int32_t* rel = S.relind.data() + S.rel_ptr[c];
-            const bool split_pc = out_cb && D.dasm[p];
             auto dst_of = [&](int j) { return D.dasm[p] ? D.col_owner(S, p, rel[j]) : D.owner[p]; };
             for (int a = j0; a < j1;) {
                 const int r = dst_of(a);
-                const bool cbpart = split_pc && rel[a] >= wp;
                 int b = a + 1;
-                while (b < j1 && dst_of(b) == r && (!split_pc || (rel[b] >= wp) == cbpart)) ++b;
+                while (b < j1 && dst_of(b) == r) ++b;
                 if (r != src) {
                     DistMsg g {};
+                    g.step = id;
                     g.src = src;
                     g.dst = r;
                     g.skind = g.dkind = R_CB;
@@ -401,47 +396,32 @@ int64_t dist_plan(const Symbolic& S, int nranks, DistPlan& D) {
                     g.rows = mbc - a;
                     g.cols = b - a;
                     g.s = c;
-                    (cbpart ? *out_cb : out).push_back(g);
+                    D.msgs.push_back(g);
                 }
                 a = b;
             }
         };
-        auto add_step_msgs = [&](int kind, int lev2, int s2, int k2, std::vector<DistMsg>& v) {
-            const int32_t id = open_step(kind, lev2, s2, k2);
-            for (DistMsg& g : v) {
-                g.step = id;
-                D.msgs.push_back(g);
-            }
-            close_step(id);
-            v.clear();
-        };
         for (i32 c : by_level[lev]) {  // early children: one sub-step per column group
             if (!D.early[c]) continue;
             const int mbc = S.mb(c), per = D.early_gw / D.cbb;
-            std::vector<DistMsg> v;
             for (int g = 0; g * D.early_gw < mbc; ++g) {
+                const int32_t id = open_step(STEP_DELIVER, lev, c, g);
                 for (int jb = g * per; jb < (g + 1) * per && jb * D.cbb < mbc; ++jb)
-                    deliver_cols(v, nullptr, c, D.owner[c], jb * D.cbb, std::min(mbc, (jb + 1) * D.cbb));
-                add_step_msgs(STEP_DELIVER, lev, c, g, v);
+                    deliver_cols(id, c, D.owner[c], jb * D.cbb, std::min(mbc, (jb + 1) * D.cbb));
+                close_step(id);
             }
         }
-        // the level's delivery: with dist_deliver_split, the children's columns that map
-        // into parent PANEL columns first (k = 0: the next level's chains wait only for
-        // these), the ones that map into parent CB columns after them (k = 1: waited for
-        // by the lookahead stream, which assembles and updates the CB blocks)
-        std::vector<DistMsg> vp, vc;
-        const bool dsplit = S.opt.dist_deliver_split != 0;
+        int32_t id = open_step(STEP_DELIVER, lev, -1, 0);
         for (i32 c : by_level[lev]) {
             const i32 p = S.sn_parent[c];
             const int mbc = S.mb(c);
             if (p < 0 || mbc <= 0 || D.early[c]) continue;
             for (int jb = 0; jb * D.cbb < mbc; ++jb) {
                 const int src = D.split[c] >= 0 ? D.cb_rank[D.split[c]][jb] : D.owner[c];
-                deliver_cols(vp, dsplit ? &vc : nullptr, c, src, jb * D.cbb, std::min(mbc, (jb + 1) * D.cbb));
+                deliver_cols(id, c, src, jb * D.cbb, std::min(mbc, (jb + 1) * D.cbb));
             }
         }
-        add_step_msgs(STEP_DELIVER, lev, -1, 0, vp);
-        add_step_msgs(STEP_DELIVER, lev, -1, 1, vc);
+        close_step(id);
     }
     return SC_OK;
 }

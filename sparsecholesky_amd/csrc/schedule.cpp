@@ -100,7 +100,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
     auto is_dpanel = [&](int32_t s) { return multi && D.pd[s] >= 0; };
     std::vector<int32_t> hosted_of((size_t)std::max(N.nranks, 1), -1);  // rank -> index into N.R
     for (size_t v = 0; v < N.R.size(); ++v) hosted_of[N.R[v].rank] = (int32_t)v;
-    std::vector<int32_t> init_step, deliver_step((size_t)S.nlevels, -1), deliver_cb_step((size_t)S.nlevels, -1);
+    std::vector<int32_t> init_step, deliver_step((size_t)S.nlevels, -1);
     // early children: early_step[c][g] = the DELIVER step of column group g (-1: none; a
     // group whose columns all stay on the producer has no messages and no step)
     std::vector<std::vector<int32_t>> early_step;
@@ -122,7 +122,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 if ((int)ks[t.k].size() <= t.p) ks[t.k].resize((size_t)t.p + 1, -1);
                 ks[t.k][t.p] = id;
             }
-            if (t.kind == STEP_DELIVER && t.s < 0) (t.k == 0 ? deliver_step : deliver_cb_step)[t.level] = id;
+            if (t.kind == STEP_DELIVER && t.s < 0) deliver_step[t.level] = id;
             if (t.kind == STEP_DELIVER && t.s >= 0) {
                 auto& es = early_step[t.s];
                 if ((int)es.size() <= t.k) es.resize((size_t)t.k + 1, -1);
@@ -431,19 +431,14 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
     // step's diagonal block when that block is a full 64-column block of the same slab and
     // the update runs on 64 x 64 tiles (span <= 128; K = 64 or 128)
     auto prefactor_ok = [&](int span, int k1, int slab1) {
-        return S.opt.panel_prefactor && S.opt.inner_order == 1 && S.opt.syrk_tile != 128 &&
-               (span <= 2 * PNB || S.opt.panel_prefactor == 2) && k1 + PNB <= slab1;
+        return S.opt.panel_prefactor && S.opt.inner_order == 1 && S.opt.syrk_tile != 128 && span <= 2 * PNB &&
+               k1 + PNB <= slab1;
     };
     // distributed assembly: one write-once tile-assembly launch of the front columns of
     // s that hosted rank v owns (its panel slabs and CB column blocks, D.col_owner), in
     // 16-column blocks; a block straddling another rank's columns computes those too,
     // into this rank's private copy, where nothing reads them
-    // dist_deliver_split: the parent columns [lo, hi) of one launch -- the panel columns on
-    // the main stream (the chains wait for them only), the CB columns on the lookahead
-    // stream after the level's CB-column delivery (sub-step k = 1)
-    std::vector<std::vector<int>> cbasm_ev;  // per hosted rank, per supernode: event after its CB-column assembly
-    std::vector<int> level_cbasm;           // this level's such events (joined before its deliveries)
-    auto region_asm_launch = [&](int32_t lev, int32_t s, int v, int lo, int hi, int strm) {
+    auto emit_region_asm = [&](int32_t lev, int32_t s, int v) {
         const int who = N.R[v].rank, m = S.sn_m[s];
         Launch L {};
         L.kind = L_ASM;
@@ -451,11 +446,10 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         L.vr = v;
         L.big = 1;
         L.epi = 1;  // the tasks carry column limits (B.asml)
-        L.strm = strm;
         L.off = (int64_t)asmv.size();
-        for (int cb = lo / ASM_COLS; cb * ASM_COLS < hi; ++cb) {
-            const int c1 = std::min(hi, (cb + 1) * ASM_COLS);
-            for (int a = std::max(lo, cb * ASM_COLS); a < c1;) {  // each run of owned columns of the block
+        for (int cb = 0; cb * ASM_COLS < m; ++cb) {
+            const int c1 = std::min(m, (cb + 1) * ASM_COLS);
+            for (int a = cb * ASM_COLS; a < c1;) {  // each run of owned columns of the block
                 if (D.col_owner(S, s, a) != who) {
                     ++a;
                     continue;
@@ -472,25 +466,6 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         }
         L.count = (int32_t)((int64_t)asmv.size() - L.off);
         if (L.count > 0) N.sched.push_back(L);
-        return L.count > 0;
-    };
-    auto emit_region_asm = [&](int32_t lev, int32_t s, int v) {
-        const int m = S.sn_m[s], w = S.w(s);
-        if (!S.opt.dist_deliver_split || m == w) {
-            region_asm_launch(lev, s, v, 0, m, 0);
-            return;
-        }
-        region_asm_launch(lev, s, v, 0, w, 0);
-        const int e0 = push_record(0);  // the rank's own children's CBs (main stream) are done
-        const size_t mark = N.sched.size();
-        push_wait(1, e0);
-        if (region_asm_launch(lev, s, v, w, m, 1)) {
-            if (cbasm_ev.empty()) cbasm_ev.assign(N.R.size(), std::vector<int>((size_t)S.ns, -1));
-            cbasm_ev[v][s] = push_record(1);
-            level_cbasm.push_back(cbasm_ev[v][s]);
-        } else {
-            N.sched.resize(mark);  // no CB columns here: drop the wait
-        }
     };
     // CB rank (hosted index v) of split front s: per final panel slab, CB -= L21_k
     // L21_k^T on the column blocks it owns (K = slab width), from its R_LAND copy
@@ -498,12 +473,10 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         const int who = N.R[v].rank;
         const std::vector<int32_t>& cbr = D.cb_rank[D.split[s]];
         const int w = S.w(s), m = S.sn_m[s], mb = m - w;
-        if (is_dasm(s)) {
+        if (is_dasm(s))
             emit_region_asm(lev, s, v);  // its own CB blocks, from the children's columns it received
-            if (!cbasm_ev.empty() && cbasm_ev[v][s] >= 0) push_wait(0, cbasm_ev[v][s]);  // (the updates below: main stream)
-        } else {
+        else
             emit_step(init_step[s]);
-        }
         for (int k0 = 0, k = 0; k0 < w; k0 += D.nbo, ++k) {
             const int k1 = std::min(w, k0 + D.nbo);
             emit_slab(s, k);
@@ -532,6 +505,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         double* panel_pool = N.R[v].P.panel_pool;
         double* cb_pool = N.R[v].P.cb_pool;
         const std::vector<int64_t>& poff = N.R[v].panel_off;
+        const std::vector<int64_t>& coff = N.R[v].cb_off;
         // small fronts: one launch sized for the level's largest front when the level
         // fits one workgroup per CU (fewer dependent launches on thin levels), else one
         // launch per LDS bucket (small fronts keep their occupancy on wide levels)
@@ -607,7 +581,6 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // (stream 1), which overlaps the next slab's factorization.  A later outer
         // update of overlapping columns waits for the stream-1 work first.
         int b_pending = -1;
-        int b_rest = -1;  // la_next: the trailing part of the last split outer_b
         // rows [c_lo, r_hi) of columns [c_lo, c_hi) -= their product over columns [ka, kb)
         auto add_update = [&](std::vector<GemmTask>& vec, double& fl, double* pan, int m, int r_hi, int c_lo, int c_hi,
                               int ka, int kb) {
@@ -626,18 +599,6 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // fronts whose block at the current step was pre-factored by the previous step's
         // inner update (panel_prefactor): their TRSM loads L11 (trsm_panel_g_kernel<2>)
         std::vector<char> pre((size_t)S.ns, 0);
-        // outer_pieces: the next slab's update at a slab end in column pieces; piece 0 on
-        // the main stream, the others on the lookahead stream ahead of the trailing update,
-        // each waited for by the main stream just before a launch touches its columns
-        const int npieces = S.opt.lookahead ? std::max(1, std::min(S.opt.outer_pieces, NBO / PNB)) : 1;
-        const int PW = (NBO / npieces + PNB - 1) / PNB * PNB;
-        std::vector<std::pair<int, int>> pend;  // (first column, event) of lookahead-stream pieces
-        auto wait_pieces = [&](int hi) {
-            while (!pend.empty() && pend.front().first < hi) {
-                push_wait(0, pend.front().second);
-                pend.erase(pend.begin());
-            }
-        };
         for (int k0 = 0; k0 < maxw; k0 += PNB) {
             Launch Lp {};
             Lp.kind = L_POTRF;
@@ -650,11 +611,6 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             Lt.vr = v;
             Lt.off = (int64_t)trsm.size();
             std::vector<GemmTask> upd, outer_a, outer_b;
-            std::vector<std::vector<GemmTask>> outer_p((size_t)npieces);  // outer_a pieces 1.. (lookahead stream)
-            std::vector<GemmTask> outer_b1;  // la_next: the slab after next, split off outer_b
-            double b1fl = 0.0;
-            std::vector<double> pfl((size_t)npieces, 0.0);
-            int uhi = 0;  // columns the step's inner update writes: [.., uhi)
             std::vector<TrsmTask> trsm_part;   // partial last blocks: own launch (big = 1)
             std::vector<TrsmTask> trsm_split;  // full blocks factored by the POTRF launch (own launch)
             // a step whose fused launch would exceed trsm_split_wg workgroups (more than the GPU
@@ -696,33 +652,21 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     const int b = (k0 - slab0) / PNB;
                     const int span = PNB << __builtin_ctz((unsigned)(b + 1));
                     add_update(upd, uflops, pan, m, m, k1, std::min(slab1, k1 + span), k1 - span, k1);
-                    uhi = std::max(uhi, std::min(slab1, k1 + span));
                     if (prefactor_ok(span, k1, slab1)) {
                         upd.back().pf = S.sn_start[s] + k1;
                         pre[s] = 1;
                     }
                 } else if (k1 < slab1) {
                     add_update(upd, uflops, pan, m, m, k1, slab1, k0, k1);
-                    uhi = std::max(uhi, slab1);
                 }
                 if (k1 == slab1 && slab1 < w) {
                     // outer_a is the last update of block slab1: a pending stream-1 outer
                     // update of those columns is waited for before outer_a runs
                     const int nxt = S.opt.lookahead ? std::min(w, slab1 + NBO) : w;
-                    add_update(outer_a, afl, pan, m, m, slab1, std::min(nxt, slab1 + PW), slab0, slab1);
-                    for (int q = 1; q < npieces; ++q)
-                        add_update(outer_p[q], pfl[q], pan, m, m, slab1 + q * PW, std::min(nxt, slab1 + (q + 1) * PW),
-                                   slab0, slab1);
-                    if (S.opt.la_next && S.opt.lookahead) {
-                        const int nxt2 = std::min(w, nxt + NBO);
-                        add_update(outer_b1, b1fl, pan, m, m, nxt, nxt2, slab0, slab1);
-                        add_update(outer_b, bfl, pan, m, m, nxt2, w, slab0, slab1);
-                    } else {
-                        add_update(outer_b, bfl, pan, m, m, nxt, w, slab0, slab1);
-                    }
+                    add_update(outer_a, afl, pan, m, m, slab1, nxt, slab0, slab1);
+                    add_update(outer_b, bfl, pan, m, m, nxt, w, slab0, slab1);
                 }
             }
-            wait_pieces(k0 + PNB);  // the step's block columns
             Lp.count = (int32_t)((int64_t)potrf.size() - Lp.off);
             Lt.count = (int32_t)((int64_t)trsm.size() - Lt.off);
             if (Lp.count > 0) N.sched.push_back(Lp);
@@ -743,7 +687,6 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 trsm.insert(trsm.end(), trsm_part.begin(), trsm_part.end());
                 N.sched.push_back(Lq);
             }
-            wait_pieces(uhi);  // the inner update's columns
             push_gemm_launch(L_PANEL, lev, upd, 0, uflops);
             // split fronts: a slab is final after the TRSM of its last block; at a slab end
             // no inner update is pending
@@ -754,9 +697,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 if (k1 == w || k1 % D.nbo == 0) emit_slab(s, k0 / D.nbo);
             }
             int e_trsm = -1;
-            bool any_p = false;
-            for (int q = 1; q < npieces; ++q) any_p |= !outer_p[q].empty();
-            if (!outer_b.empty() || !outer_b1.empty() || any_p) e_trsm = push_record(0);
+            if (!outer_b.empty()) e_trsm = push_record(0);
             if (!outer_a.empty()) {
                 if (b_pending >= 0) {
                     push_wait(0, b_pending);
@@ -764,30 +705,12 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 }
                 push_gemm_launch(L_PANEL, lev, outer_a, 0, afl);
             }
-            if (any_p) {  // the next slab's other pieces, ahead of the trailing update
-                push_wait(1, e_trsm);
-                const int c_next = (k0 / NBO + 1) * NBO;
-                for (int q = 1; q < npieces; ++q) {
-                    if (outer_p[q].empty()) continue;
-                    push_gemm_launch(L_PANEL, lev, outer_p[q], 0, pfl[q], 1);
-                    pend.push_back({c_next + q * PW, push_record(1)});
-                }
-            }
-            if (!outer_b1.empty()) {  // la_next: the next outer_a waits for this part only
-                push_wait(1, e_trsm);
-                push_gemm_launch(L_PANEL, lev, outer_b1, 0, b1fl, 1);
-                b_pending = push_record(1);
-            }
             if (!outer_b.empty()) {
                 push_wait(1, e_trsm);
                 push_gemm_launch(L_PANEL, lev, outer_b, 0, bfl, 1);
-                const int eb = push_record(1);
-                if (outer_b1.empty()) b_pending = eb;
-                else b_rest = eb;
+                b_pending = push_record(1);
             }
         }
-        wait_pieces(INT32_MAX);
-        if (b_rest >= 0) push_wait(0, b_rest);
         if (b_pending >= 0) push_wait(0, b_pending);
         // early-delivery children: the CB SYRK in column groups, an event after each
         // (the group's comm sub-step waits for exactly that event)
@@ -1191,10 +1114,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 if (g < (int)early_step[c].size())
                     emit_step(early_step[c][g], vs >= 0 && !early_ev[c].empty() ? early_ev[c][g] : -1);
         }
-        for (int e : level_cbasm) push_wait(0, e);  // CB columns assembled on the lookahead stream
-        level_cbasm.clear();
         emit_step(deliver_step[lev]);
-        emit_step(deliver_cb_step[lev], -1, 1);  // CB-column delivery: the lookahead stream waits for it
         comm_done[lev] = push_record(2);
     }
     if (multi) push_wait(0, push_record(2));  // join the comm stream (its last sends)

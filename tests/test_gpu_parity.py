@@ -521,10 +521,9 @@ def lap48_oracle():
 
 
 @pytest.mark.parametrize("opts", [{}, dict(asm_tile_min_m=1024), dict(cb_gather=0), dict(trsm_split_wg=1),
-                                  dict(lookahead=0), dict(cb_gather=0, panel_nb_outer=256),
-                                  dict(outer_pieces=4, panel_prefactor=2, la_next=1)],
+                                  dict(lookahead=0), dict(cb_gather=0, panel_nb_outer=256)],
                          ids=["default", "tiled_asm", "assembled_cb", "split_potrf", "no_lookahead",
-                              "assembled_cb_nbo256", "pieces4_pf2"])
+                              "assembled_cb_nbo256"])
 def test_lap48_full_parity(gpu, lap48_oracle, opts):
     # the whole 48^3 factor (n = 110592, F = 7.07e10: a 2304-wide root, CB SYRK with K
     # up to 1152 on 128 x 128 tiles) against the oracle, exact pattern and rel-Fro;
@@ -910,15 +909,12 @@ def test_panel_variants_oracle_and_bitwise(gpu, case, opts):
     # the large-front panel chain (POTRF / TRSM / inner and outer updates) on dense and
     # Laplacian inputs, slab widths that do and do not divide the front: eager and hipGraph
     # replay, twice each through the same handle, with and without the chain lookahead
-    # (panel_prefactor: the next diagonal block factored inside the inner update launch;
-    # 2: after every inner update) and with the next-slab update in column pieces on the
-    # lookahead stream (outer_pieces), with the lookahead update split at the slab after
-    # next (la_next), are bitwise identical and match the oracle
+    # (panel_prefactor: the next diagonal block factored inside the inner update launch),
+    # are bitwise identical and match the oracle
     A = _dense_spd(1350, 5) if case.startswith("dense") else sc.laplacian3d(int(case[3:5]))
     facs = []
-    for graph, pf, op, ln in ((0, 1, 1, 0), (1, 1, 1, 0), (0, 0, 1, 0), (1, 0, 1, 0), (0, 1, 4, 0), (1, 2, 4, 1),
-                              (0, 2, 2, 1), (1, 1, 1, 1)):
-        num = sc.Numeric(sc.Symbolic(A, use_graph=graph, panel_prefactor=pf, outer_pieces=op, la_next=ln, **opts))
+    for graph, pf in ((0, 1), (1, 1), (0, 0), (1, 0)):
+        num = sc.Numeric(sc.Symbolic(A, use_graph=graph, panel_prefactor=pf, **opts))
         for _ in range(2):
             assert num.factor(A.x) == 0
             facs.append(num.export()[1].x.copy())
