@@ -505,7 +505,6 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         double* panel_pool = N.R[v].P.panel_pool;
         double* cb_pool = N.R[v].P.cb_pool;
         const std::vector<int64_t>& poff = N.R[v].panel_off;
-        const std::vector<int64_t>& coff = N.R[v].cb_off;
         // small fronts: one launch sized for the level's largest front when the level
         // fits one workgroup per CU (fewer dependent launches on thin levels), else one
         // launch per LDS bucket (small fronts keep their occupancy on wide levels)
