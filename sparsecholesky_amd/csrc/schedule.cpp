@@ -867,9 +867,11 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             vec.push_back(t);
             fl += 2.0 * t.K * ((double)t.N * t.M - (double)t.N * (t.N - 1) / 2.0);
         };
+        int local_ev = -1;  // dist_local_pieces: event after the last local piece update
         for (int k = 0; k < nsl; ++k) {
             const int k0s = slab_c0(k), k1s = slab_c1(k);
             const int vk = hosted_of[sr[k]];
+            local_ev = -1;
             if (vk >= 0) {
                 // factor slab k: per 64 columns POTRF, TRSM of the rows below, and the
                 // update of the slab's next columns (recursive order, as emit_level)
@@ -877,6 +879,10 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 if (e >= 0) push_wait(0, e);
                 double* pan = pan_of(vk);
                 bool pre_blk = false;  // this block was pre-factored by the previous inner update
+                // dist_local_pieces: when this rank also owns the next slab, its update by each
+                // finished piece of this slab goes on the lookahead stream while the chain goes on
+                const bool local_next = S.opt.dist_local_pieces && k + 1 < nsl && sr[k + 1] == sr[k];
+                local_ev = -1;
                 for (int k0 = k0s; k0 < k1s; k0 += PNB) {
                     const int nb = std::min(PNB, k1s - k0), k1 = k0 + nb;
                     Launch Lp {};
@@ -903,7 +909,20 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                     Lt.count = (int32_t)((int64_t)trsm.size() - Lt.off);
                     if (Lt.count > 0) N.sched.push_back(Lt);
                     // a finished piece of the slab leaves now (dist_pieces)
-                    if (k1 == k1s || (k1 - k0s) % D.pw == 0) emit_step(slab_piece(s, k, (k1 - 1 - k0s) / D.pw));
+                    if (k1 == k1s || (k1 - k0s) % D.pw == 0) {
+                        const int pc = (k1 - 1 - k0s) / D.pw;
+                        emit_step(slab_piece(s, k, pc));
+                        if (local_next) {  // dist_local_pieces: this rank's next slab, by this piece, now
+                            const int j0 = slab_c0(k + 1), j1 = slab_c1(k + 1), c0 = k0s + pc * D.pw;
+                            std::vector<GemmTask> t0;
+                            double fl = 0.0;
+                            upd_task(t0, fl, pan + (int64_t)j0 * m + j0, m, pan + (int64_t)c0 * m + j0, m, m - j0,
+                                     j1 - j0, std::min(k1s, c0 + D.pw) - c0);
+                            push_wait(1, push_record(0));
+                            push_gemm_launch(L_PANEL, lev, t0, 0, fl, 1);
+                            local_ev = push_record(1);
+                        }
+                    }
                     if (k1 < k1s) {
                         std::vector<GemmTask> upd;
                         double fl = 0.0;
@@ -932,7 +951,9 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
                 double* pan = pan_of(v);
                 const double* Lk = pan + (int64_t)k0s * m;  // column k0s of the slab, row 0
                 const int K = k1s - k0s;
-                if (k + 1 < nsl && sr[k + 1] == r) {  // the next slab: critical path, piece by piece
+                if (k + 1 < nsl && sr[k + 1] == r && v == vk && local_ev >= 0) {  // done during the chain
+                    push_wait(0, local_ev);
+                } else if (k + 1 < nsl && sr[k + 1] == r) {  // the next slab: critical path, piece by piece
                     const int e = last_ev1(v, k - 1);
                     if (e >= 0) push_wait(0, e);
                     const int j0 = slab_c0(k + 1), j1 = slab_c1(k + 1);

@@ -544,6 +544,7 @@ def test_lap48_full_parity(gpu, lap48_oracle, opts):
                                                (4, True, {}), (8, True, {}),
                                                (8, False, dict(dist_asm=0)), (4, True, dict(dist_asm=0)),
                                                (4, False, dict(dist_pieces=1)), (8, True, dict(dist_pieces=16)),
+                                               (2, False, dict(dist_local_pieces=1)), (4, True, dict(dist_local_pieces=1)),
                                                (4, True, dict(dist_pieces=3))])
 def test_partitioned_defaults_lap48(gpu, lap48_oracle, nranks, rccl, opts):
     # the distributed plan at the DEFAULT options the N-GPU bench runs (panel_nb_outer
