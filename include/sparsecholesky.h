@@ -115,9 +115,8 @@ typedef struct sc_options {
                                 finished it, so the next slab's owner starts updating before the slab is done */
     int32_t dist_local_pieces; /* multi-GPU distributed panels: when a rank owns two consecutive slabs, its update of
                                 the second by each finished piece of the first runs on the lookahead stream while
-                                the first slab's chain goes on (1), instead of after the chain on the main stream (0) */
-    int32_t xcd_front_min;   /* SYRK launches of at least this many fronts place each front's tiles on one XCD
-                                (its own L2) instead of spreading every front over the eight XCDs (0: never) */
+                                the first slab's chain goes on (1, default), instead of after the chain on the
+                                main stream (0) */
     int32_t panel_prefactor; /* 1 (default): in the 64-column panel chain, the recursive inner update after a step
                                 (K = 64 or 128) also forms and factors the NEXT step's 64 x 64 diagonal block in one
                                 extra workgroup, so that step's TRSM loads L11 instead of every TRSM workgroup

@@ -74,7 +74,7 @@ class Options(C.Structure):
         ("dist_slab_block", C.c_int32), ("trsm_split_wg", C.c_int32),
         ("syrk_lean_kmax", C.c_int32), ("cb_tail_split", C.c_int32), ("tiny_dense", C.c_int32),
         ("dist_asm", C.c_int32),
-        ("dist_pieces", C.c_int32), ("dist_local_pieces", C.c_int32), ("xcd_front_min", C.c_int32), ("panel_prefactor", C.c_int32),
+        ("dist_pieces", C.c_int32), ("dist_local_pieces", C.c_int32), ("panel_prefactor", C.c_int32),
     ]
 
 

@@ -95,8 +95,7 @@ void sc_default_options(sc_options* opt) {
     opt->tiny_dense = 1;
     opt->dist_asm = 1;
     opt->dist_pieces = 4;
-    opt->dist_local_pieces = 0;
-    opt->xcd_front_min = 0;
+    opt->dist_local_pieces = 1;
     opt->panel_prefactor = 1;
 }
 

@@ -80,48 +80,6 @@ void xcd_order_tasks(int2* tiles, int64_t n, const GemmTask* tasks, int ntasks) 
     for (int64_t b = 0; b < n; ++b) tiles[b] = per[b % 8][b / 8];
 }
 
-// Front-major XCD order for launches of many tasks (xcd_front_min): whole tasks go to
-// one XCD each (longest K first, to the XCD with the fewest tiles so far), so an XCD's
-// resident workgroups work on one front at a time and its operand rows stay in that
-// XCD's L2 (the chunked order above spreads every front over all eight L2s).  Tail
-// tiles move from over-full XCDs to under-full ones so that each XCD still receives
-// exactly its ceil((n - x) / 8) tiles.
-void xcd_order_fronts(int2* tiles, int64_t n, const GemmTask* tasks, int ntasks) {
-    if (n <= 8) return;
-    std::vector<int64_t> beg((size_t)ntasks + 1, 0);
-    for (int64_t i = 0; i < n; ++i) beg[(size_t)tiles[i].x + 1]++;
-    for (int t = 0; t < ntasks; ++t) beg[t + 1] += beg[t];
-    std::vector<int> ord((size_t)ntasks);
-    for (int t = 0; t < ntasks; ++t) ord[t] = t;
-    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
-        const int64_t na = beg[a + 1] - beg[a], nb = beg[b + 1] - beg[b];
-        return tasks[a].K != tasks[b].K ? tasks[a].K > tasks[b].K : na > nb;
-    });
-    std::vector<std::vector<int2>> per(8);
-    for (int t : ord) {
-        int x = 0;
-        for (int y = 1; y < 8; ++y)
-            if ((int64_t)per[y].size() * 8 < (int64_t)per[x].size() * 8) x = y;
-        per[x].insert(per[x].end(), tiles + beg[t], tiles + beg[t + 1]);
-    }
-    std::vector<int2> spill;
-    for (int x = 0; x < 8; ++x) {
-        const int64_t need = (n - x + 7) / 8;
-        while ((int64_t)per[x].size() > need) {
-            spill.push_back(per[x].back());
-            per[x].pop_back();
-        }
-    }
-    for (int x = 0; x < 8; ++x) {
-        const int64_t need = (n - x + 7) / 8;
-        while ((int64_t)per[x].size() < need) {
-            per[x].push_back(spill.back());
-            spill.pop_back();
-        }
-    }
-    for (int64_t b = 0; b < n; ++b) tiles[b] = per[b % 8][b / 8];
-}
-
 int64_t build_schedule(Numeric& N, SchedBuild& B) {
     const Symbolic& S = *N.S;
     std::vector<int32_t>& small = B.small;
@@ -240,10 +198,7 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
             L.bytes += task_bytes(tasks[q]);
         }
         L.count = (int32_t)((int64_t)tiles.size() - L.toff);
-        if (S.opt.xcd_front_min > 0 && (int)tasks.size() >= S.opt.xcd_front_min)
-            xcd_order_fronts(tiles.data() + L.toff, L.count, tasks.data(), (int)tasks.size());
-        else
-            xcd_order_tasks(tiles.data() + L.toff, L.count, tasks.data(), (int)tasks.size());
+        xcd_order_tasks(tiles.data() + L.toff, L.count, tasks.data(), (int)tasks.size());
         if (L.pf)  // the pre-factor workgroups (the longest, on the chain) are dispatched first
             std::stable_partition(tiles.begin() + L.toff, tiles.end(), [](const int2& t) { return t.y < 0; });
         L.ntasks = (int32_t)tasks.size();

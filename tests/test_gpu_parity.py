@@ -521,9 +521,9 @@ def lap48_oracle():
 
 
 @pytest.mark.parametrize("opts", [{}, dict(asm_tile_min_m=1024), dict(cb_gather=0), dict(trsm_split_wg=1),
-                                  dict(lookahead=0), dict(cb_gather=0, panel_nb_outer=256), dict(xcd_front_min=4)],
+                                  dict(lookahead=0), dict(cb_gather=0, panel_nb_outer=256)],
                          ids=["default", "tiled_asm", "assembled_cb", "split_potrf", "no_lookahead",
-                              "assembled_cb_nbo256", "xcd_front_major"])
+                              "assembled_cb_nbo256"])
 def test_lap48_full_parity(gpu, lap48_oracle, opts):
     # the whole 48^3 factor (n = 110592, F = 7.07e10: a 2304-wide root, CB SYRK with K
     # up to 1152 on 128 x 128 tiles) against the oracle, exact pattern and rel-Fro;
@@ -544,7 +544,7 @@ def test_lap48_full_parity(gpu, lap48_oracle, opts):
                                                (4, True, {}), (8, True, {}),
                                                (8, False, dict(dist_asm=0)), (4, True, dict(dist_asm=0)),
                                                (4, False, dict(dist_pieces=1)), (8, True, dict(dist_pieces=16)),
-                                               (2, False, dict(dist_local_pieces=1)), (4, True, dict(dist_local_pieces=1)),
+                                               (2, False, dict(dist_local_pieces=0)), (4, True, dict(dist_local_pieces=0)),
                                                (4, True, dict(dist_pieces=3))])
 def test_partitioned_defaults_lap48(gpu, lap48_oracle, nranks, rccl, opts):
     # the distributed plan at the DEFAULT options the N-GPU bench runs (panel_nb_outer
