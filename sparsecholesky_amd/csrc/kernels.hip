@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "kernels.hpp"
 
@@ -1446,7 +1447,21 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const in
 // over k < K (A column-major, ld lda; rows past M (i) / N (j) read as 0).  BK = 16,
 // register-staged double-buffered LDS (As / Bs: 2 stages of BK x (BT + 16) doubles
 // each, +128 B row pad: the two k-rows read by a half-wave hit disjoint banks).
-template <int BT, int WM, int WN, int BK = 16>
+#ifndef SC_KSKIP
+#define SC_KSKIP 1
+#endif
+#ifndef SC_DSKIP
+#define SC_DSKIP 1
+#endif
+// DIAG (a tile on the diagonal of C, row0 == col0): every epilogue discards the entries
+// above the diagonal, so the MFMAs of this wave's 16 x 16 tiles lying wholly above it are
+// skipped (28 of the 64 of a 128-tile; the live tiles' sums are unchanged, bit for bit).
+// The last K stage is peeled (no prefetch) and skips its 4-deep sub-steps past K (K =
+// 16q + 1 is common: 225, 961, 3969, 8001).  Interleaved at 128^3 (profiles/r06/ab_kloop.txt):
+// 503.8 / 504.5 ms before, 502.7 / 502.5 peeled, 502.4 / 501.6 + the K skip, 501.1 / 501.9
+// + the diagonal skip; the same skips as in-loop branches (513.2), or a whole-wave skip of
+// the dead waves (551), lose: the branches break the K loop's schedule.
+template <int BT, int WM, int WN, int BK = 16, bool DIAG = false>
 __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t lda, int K, int M, int N, int row0,
                                            int col0, double4_t (&acc)[BT / WM / 16][BT / WN / 16], double* smem) {
     static_assert(BK == 16 || BK == 8, "four-deep k sub-steps of the MFMA");
@@ -1459,6 +1474,8 @@ __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t
     const int lane = tid & 63;
     const int wid = tid >> 6;
     const int wr = wid / WN, wc = wid % WN;
+    // 16-row tile a of this wave vs its 16-column tile b: live iff dq + a - b >= 0
+    const int dq = DIAG ? __builtin_amdgcn_readfirstlane(wr * RTM - wc * RTN) : 0;
     // staging: BK x BT doubles per operand over NT threads
     constexpr int PER = BT * BK / NT;
     // Operands through a per-stage buffer resource (columns k0 .. k0 + BK of A):
@@ -1488,12 +1505,12 @@ __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t
     };
 
     const int nk = (K + BK - 1) / BK;
-    gload(0);
-    sstore(0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
+    const int krem = K - (nk - 1) * BK;  // live k of the last stage
+    // one K stage; LAST: no prefetch, and its sub-steps past K skipped (SC_KSKIP)
+    auto stage = [&](int kt, auto last) {
+        constexpr bool LAST = decltype(last)::value;
         const int cur = kt & 1;
-        if (kt + 1 < nk) gload((kt + 1) * BK);
+        if (!LAST) gload((kt + 1) * BK);
         // LDS operand fragments double-buffered across the 4-deep k sub-steps: the
         // reads of sub-step kk + 1 are in flight while sub-step kk's MFMAs issue
         double av[2][RTM], bv[2][RTN];
@@ -1510,20 +1527,27 @@ __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t
 #pragma unroll
         for (int kk = 0; kk < BK; kk += 4) {
             const int slot = (kk / 4) & 1;
+            if (LAST && SC_KSKIP && kk >= krem) break;
             if (kk + 4 < BK) lread(kk + 4, slot ^ 1);
 #pragma unroll
             for (int a = 0; a < RTM; ++a)
 #pragma unroll
                 for (int b = 0; b < RTN; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[slot][a], bv[slot][b], acc[a][b], 0, 0, 0);
+                    if (!DIAG || !SC_DSKIP || dq + a - b >= 0)
+                        acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[slot][a], bv[slot][b], acc[a][b], 0, 0, 0);
             // the next stage's LDS stores go out under the last sub-step's MFMAs, not
             // between them and the barrier: 547 -> 532 ms at 128^3 (stores after sub-step
             // 1: 535.8; A after 1 and B after 2: 533.0; the loads issued after sub-step 0
             // instead: 533.3, both: 536.8)
-            if (kk == BK - 8 && kt + 1 < nk) sstore(cur ^ 1);
+            if (!LAST && kk == BK - 8) sstore(cur ^ 1);
         }
         __syncthreads();
-    }
+    };
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    for (int kt = 0; kt + 1 < nk; ++kt) stage(kt, std::false_type {});
+    if (nk > 0) stage(nk - 1, std::true_type {});
 }
 
 // Panel chain lookahead (the pre-factor workgroup of an inner panel update, tile marker
@@ -1623,7 +1647,10 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
         for (int b = 0; b < RTN; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
     // (operand stages by LDS-DMA, buffer_load_dwordx4 ... lds per 1-KB k-row, measured
     // slower: 510.5 ms with two 16-deep stages, 521.5 with four 8-deep, vs 505.7-507.3)
-    mfma_kloop<BT, WM, WN, BK>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
+    if (row0 == col0)
+        mfma_kloop<BT, WM, WN, BK, true>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
+    else
+        mfma_kloop<BT, WM, WN, BK>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
 
     if constexpr (TAG == 1) {
         if (T.gs >= 0) {  // the front's CB is not assembled: gather the children's entries
