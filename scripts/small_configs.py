@@ -17,6 +17,9 @@ import torch  # noqa: E402
 import oracle  # noqa: E402
 import sparsecholesky_amd as sc  # noqa: E402
 
+if os.environ.get("SC_LIB"):  # A/B: another build of the library
+    sc.LIB_PATH = os.environ["SC_LIB"]
+
 
 def timeit(fn, reps):
     fn()

@@ -255,7 +255,13 @@ i64 analyze(i64 n, const i64* Ap, const i32* Ai, const sc_options& opt, Symbolic
             const double newzeros = (double)nscol0 * (double)(nscol0 + lnz1 - lnz0);
             const double totz = newzeros + zeros[j] + zeros[j + 1];
             bool merge = false;
-            if (opt.relax_wmax > 0 && nscol0 > opt.relax_wmax && nscol1 > opt.relax_wmax && gkids[j + 1] > 1) {
+            // a merged front that still runs in the one-workgroup register kernel (m <=
+            // small_front_max) has no CB SYRK to keep the coupling in, and every merge
+            // takes one dependent front off a chain (1138_bus: 93 -> 54 levels, 0.614 ->
+            // 0.469 ms; the 128^3 tree is unchanged)
+            const bool small_merged = nscol0 + lnz1 <= opt.small_front_max;
+            if (opt.relax_wmax > 0 && nscol0 > opt.relax_wmax && nscol1 > opt.relax_wmax && gkids[j + 1] > 1 &&
+                !small_merged) {
                 // a wide child of a wide parent with siblings stays apart: its coupling goes
                 // through the CB SYRK and the siblings stay parallel.  Chains still merge.
                 merge = false;
