@@ -1028,13 +1028,16 @@ __global__ __launch_bounds__(256) void chain_init_kernel(DevPlan P, ChainPlan C,
     for (int idx = threadIdx.x; idx < tot; idx += 256) out[idx] = F[idx];
 }
 
+#ifndef SC_CHAIN_DB
+#define SC_CHAIN_DB 1
+#endif
 // Chain, part 2 (one workgroup of CHAIN_NT threads, one tile each): iteration i loads
 // front i's tiles from the LDS front buffer, writes front i + 1's image (held in
 // registers since iteration i - 1) into the buffer, issues the loads of front i + 2's
 // image and CB relind, factors front i, stores its panel, and adds its CB into the
 // buffer at the parent's positions (the last front's CB goes to HBM).
 constexpr int CHAIN_IMG = (128 * 129 / 2 + CHAIN_NT - 1) / CHAIN_NT;  // image doubles per thread
-__global__ __launch_bounds__(CHAIN_NT) void front_chain_kernel(DevPlan P, ChainPlan C, int first, int count) {
+__global__ __launch_bounds__(CHAIN_NT) void front_chain_kernel(DevPlan P, ChainPlan C, int first, int count, int fsz) {
     extern __shared__ double F[];
     __shared__ __attribute__((aligned(16))) double colbuf[2 * 4 * COLB];
     __shared__ ChainDesc ds[CHAIN_MAXF];
@@ -1063,12 +1066,16 @@ __global__ __launch_bounds__(CHAIN_NT) void front_chain_kernel(DevPlan P, ChainP
         nrr = nbi >= 0 ? C.relp[d.relp_off + nbi] : 0u;
         nrc = nbi >= 0 ? C.relp[d.relp_off + nbj] : 0u;
     };
+    // two front buffers (SC_CHAIN_DB): front i + 1's image goes into the other buffer
+    // while front i loads its tiles, with no barrier between
+    auto Fb = [&](int f) { return SC_CHAIN_DB ? F + (f & 1) * fsz : F; };
     auto put = [&](int f) {  // image slice -> the LDS buffer
         const int tot = (ds[f].m * (ds[f].m + 1)) >> 1;
+        double* Fd = Fb(f);
 #pragma unroll
         for (int q = 0; q < CHAIN_IMG; ++q) {
             const int idx = tid + CHAIN_NT * q;
-            if (idx < tot) F[idx] = img[q];
+            if (idx < tot) Fd[idx] = img[q];
         }
     };
     int cbi, cbj;
@@ -1093,8 +1100,8 @@ __global__ __launch_bounds__(CHAIN_NT) void front_chain_kernel(DevPlan P, ChainP
         R.bi[0] = cbi;
         R.bj[0] = cbj;
         const uint32_t rr = crr, rc = crc;
-        small_load<1>(R, F, m);
-        lds_barrier();  // every thread has its tile: the buffer is free
+        small_load<1>(R, Fb(i), m);
+        if (!SC_CHAIN_DB) lds_barrier();  // every thread has its tile: the buffer is free
         if (stamp && tid == 0) stamp[1] = __builtin_amdgcn_s_memtime();
         const bool has_parent = i + 1 < count;
         if (has_parent) {
@@ -1112,13 +1119,14 @@ __global__ __launch_bounds__(CHAIN_NT) void front_chain_kernel(DevPlan P, ChainP
                 small_store_cb<1>(R, P.cb_pool + d.cb_off, m, w);
             } else {  // CB entries into the parent's front (relind injective: no collisions)
                 const int mp = ds[i + 1].m;
+                double* Fp = Fb(i + 1);
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
                         const int ii = 4 * R.bi[0] + r, jj = 4 * R.bj[0] + c;
                         const int pr = (rr >> (8 * r)) & 255, pc = (rc >> (8 * c)) & 255;
-                        if (jj >= w && ii >= jj && ii < m) F[pk_col(mp, pc) + pr - pc] += R.v[0][r * 4 + c];
+                        if (jj >= w && ii >= jj && ii < m) Fp[pk_col(mp, pc) + pr - pc] += R.v[0][r * 4 + c];
                     }
             }
         }
@@ -1740,9 +1748,11 @@ hipError_t launch_front_chain(const DevPlan& P, const ChainPlan& C, int first, i
                               const double* Ax, hipStream_t st) {
     if (count <= 0) return hipSuccess;
     if (count > CHAIN_MAXF || maxm > 128) return hipErrorInvalidValue;  // the host splits longer chains
-    const size_t lds = (size_t)maxm * (maxm + 1) / 2 * sizeof(double);
+    const int fsz = maxm * (maxm + 1) / 2;
+    const size_t lds = (size_t)fsz * sizeof(double);
     hipLaunchKernelGGL(chain_init_kernel, dim3(count), dim3(256), lds, st, P, C, first, Ax);
-    hipLaunchKernelGGL(front_chain_kernel, dim3(1), dim3(CHAIN_NT), lds, st, P, C, first, count);
+    hipLaunchKernelGGL(front_chain_kernel, dim3(1), dim3(CHAIN_NT), (SC_CHAIN_DB ? 2 : 1) * lds, st, P, C, first, count,
+                       fsz);
     return hipGetLastError();
 }
 
