@@ -1839,6 +1839,20 @@ hipError_t launch_fill_random(double* p, int64_t n, hipStream_t st) {
 // Timestamp probe for graph-captured timing (s_memrealtime: constant 100 MHz).
 __global__ void stamp_kernel(uint64_t* slot) { *slot = __builtin_amdgcn_s_memrealtime(); }
 
+// Last launch of a single-rank factorization (main stream, which every other stream has
+// joined): the status word to pinned host memory by a system-scope release store, and
+// d_info re-armed for the next factorization.
+__global__ void status_publish_kernel(int32_t* info, int32_t* host) {
+    const int32_t v = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(info, 0x7f7f7f7f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(host, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_status_publish(int32_t* info, int32_t* host, hipStream_t st) {
+    hipLaunchKernelGGL(status_publish_kernel, dim3(1), dim3(1), 0, st, info, host);
+    return hipGetLastError();
+}
+
 // Hardware placement probe: per workgroup its HW_ID (wave/SIMD/CU/SH/SE fields) and XCC_ID.
 __global__ void hwid_kernel(uint32_t* out, int spin) {
     if (threadIdx.x == 0) {

@@ -247,6 +247,8 @@ hipError_t launch_trsm_panel(const DevPlan& P, const TrsmTask* tasks, int count,
 hipError_t launch_syrk(const GemmTask* tasks, const int2* tiles, int total_tiles, int bt, int tag, hipStream_t st,
                        int epi = 0, GatherTab gt = {}, bool lean = false, bool pf = false);
 hipError_t launch_stamp(uint64_t* slot, hipStream_t st);
+// the factorization's status word (d_info) to the pinned host word, d_info re-armed
+hipError_t launch_status_publish(int32_t* info, int32_t* host, hipStream_t st);
 
 hipError_t launch_hwid(uint32_t* out, int nwg, int threads, int spin, hipStream_t st);
 hipError_t launch_fill_random(double* p, int64_t n, hipStream_t st);

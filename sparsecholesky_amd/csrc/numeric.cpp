@@ -259,6 +259,18 @@ int64_t numeric_init(Numeric& N, const Symbolic& S, int device) {
             N.TP.host_info = (int32_t*)dp;
         }
     }
+    // single-rank handles other than the tiny path: the status word published by a
+    // one-thread kernel at the end of the schedule, d_info armed once here and re-armed by
+    // that kernel (multi-rank handles keep the copy: the status is reduced over ranks)
+    if (!N.TP.host_info && N.owner.empty()) {
+        void* dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, N.h_info, 0) != hipSuccess || hipMemset(N.d_info, 0x7f, sizeof(int32_t)) != hipSuccess ||
+            hipDeviceSynchronize() != hipSuccess) {
+            N.err = "status word setup failed";
+            return fail(SC_ERR_HIP);
+        }
+        N.status_dp = (int32_t*)dp;
+    }
     B.asml.resize(B.asmv.size(), make_int2(0, INT32_MAX));
     {  // the CB gather's segment tables
         int64_t* dgb = nullptr;
@@ -317,7 +329,8 @@ static hipError_t launch_one(Numeric& N, const Launch& L, const double* d_Ax) {
 }
 
 static int64_t enqueue_all(Numeric& N, const double* d_Ax, int prof) {
-    const bool own_status = N.TP.host_info != nullptr;  // tiny tree: the kernel writes the status
+    // tiny path: the kernel writes the status; single-rank: the publish kernel at the end
+    const bool own_status = N.TP.host_info != nullptr || N.status_dp != nullptr;
     if (!own_status) HIP_TRY(hipMemsetAsync(N.d_info, 0x7f, sizeof(int32_t), N.stream));
     for (size_t i = 0; i < N.sched.size(); ++i) {
         const Launch& L = N.sched[i];
@@ -333,6 +346,7 @@ static int64_t enqueue_all(Numeric& N, const double* d_Ax, int prof) {
     // the status word to pinned host memory on the main stream, which every other
     // stream has joined by now: the status read needs one stream sync, no extra copy
     if (!own_status) HIP_TRY(hipMemcpyAsync(N.h_info, N.d_info, sizeof(int32_t), hipMemcpyDeviceToHost, N.stream));
+    if (N.status_dp) HIP_TRY(launch_status_publish(N.d_info, N.status_dp, N.stream));
     return SC_OK;
 }
 
@@ -367,7 +381,8 @@ int64_t numeric_factor(Numeric& N, const double* d_Ax, bool sync) {
     // tiny path: an earlier factorization still in flight (async, status never read) may
     // store its status word after the host re-arms it below, and that word would then be
     // read as this factorization's status -- drain it first
-    if (N.TP.host_info && N.factored && !N.status_valid) HIP_TRY(hipStreamSynchronize(N.stream));
+    const bool pinned = N.TP.host_info || N.status_dp;
+    if (pinned && N.factored && !N.status_valid) HIP_TRY(hipStreamSynchronize(N.stream));
     N.status_valid = false;
     N.last_Ax = d_Ax;
     if (N.profile == 1 && N.ev.size() != 2 * N.sched.size()) {
@@ -377,7 +392,7 @@ int64_t numeric_factor(Numeric& N, const double* d_Ax, bool sync) {
     }
     // tiny path (the kernel stores the status word to pinned host memory itself): mark
     // it pending, so that numeric_status can wait on the word instead of the stream
-    if (N.TP.host_info) *(volatile int32_t*)N.h_info = Numeric::STATUS_PENDING;
+    if (pinned) *(volatile int32_t*)N.h_info = Numeric::STATUS_PENDING;
     if (N.use_graph && N.profile != 1) {
         // the whole level schedule (both streams, and the timing events when
         // profiling) as one hipGraph, re-captured only when its inputs change
@@ -420,7 +435,7 @@ int64_t numeric_status(Numeric& N) {
     // host polls the pinned word -- a few microseconds sooner than the stream's
     // completion signal; after ~2 ms of polling it falls back to the stream sync
     bool seen = false;
-    if (N.TP.host_info && N.profile == 0) {
+    if ((N.TP.host_info || N.status_dp) && N.profile == 0) {
         const auto t0 = std::chrono::steady_clock::now();
         for (uint32_t it = 1;; ++it) {
             if (*(volatile int32_t*)N.h_info != Numeric::STATUS_PENDING) {

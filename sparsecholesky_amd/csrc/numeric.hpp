@@ -208,7 +208,10 @@ struct Numeric {
     GatherTab gtab;              // the CB SYRK extend-add gather's segment tables (schedule.cpp)
     int32_t* d_info = nullptr;       // shared by the hosted ranks' DevPlans
     int32_t* h_info = nullptr;       // pinned host copy, written at the end of each factorization
-    static constexpr int32_t STATUS_PENDING = -2;  // h_info before the tiny kernel's status store
+    static constexpr int32_t STATUS_PENDING = -2;  // h_info before the status kernel's store
+    // single-rank handles: device view of h_info; the last launch of a factorization stores
+    // the status word there (and re-arms d_info), the host polls it (no memset / copy)
+    int32_t* status_dp = nullptr;
     double* d_Ax_owned = nullptr;
     const double* last_Ax = nullptr;
     bool factored = false;

@@ -248,6 +248,20 @@ i64 analyze(i64 n, const i64* Ap, const i32* Ai, const sc_options& opt, Symbolic
         std::vector<i32> gkids((size_t)nf, 0);  // children of each (merged) group
         for (i32 f = 0; f < nf; ++f)
             if (fparent[f] >= 0) gkids[fparent[f]]++;
+        // heights in the fundamental tree (leaves 0) and, per node, how many children reach
+        // its height minus one: a child is its parent's unique deepest child when it alone
+        // sets the parent's height (children precede their parent in postorder)
+        std::vector<i32> fh((size_t)nf, 0), nmax((size_t)nf, 0);
+        for (i32 f = 0; f < nf; ++f) {
+            const i32 p = fparent[f];
+            if (p < 0) continue;
+            if (fh[f] + 1 > fh[p]) {
+                fh[p] = fh[f] + 1;
+                nmax[p] = 1;
+            } else if (fh[f] + 1 == fh[p]) {
+                nmax[p]++;
+            }
+        }
         for (i32 j = nf - 2; j >= 0; --j) {
             if (fparent[j] != j + 1) continue;
             const i64 nscol0 = nscol[j], nscol1 = nscol[j + 1], ns = nscol0 + nscol1;
@@ -256,10 +270,17 @@ i64 analyze(i64 n, const i64* Ap, const i32* Ai, const sc_options& opt, Symbolic
             const double totz = newzeros + zeros[j] + zeros[j + 1];
             bool merge = false;
             // a merged front that still runs in the one-workgroup register kernel (m <=
-            // small_front_max) has no CB SYRK to keep the coupling in, and every merge
-            // takes one dependent front off a chain (1138_bus: 93 -> 54 levels, 0.614 ->
-            // 0.469 ms; the 128^3 tree is unchanged)
+            // small_front_max) has no CB SYRK to keep the coupling in: such a merge is not
+            // blocked by the wide-sibling rule, and when the child is its parent's unique
+            // deepest child (the merge takes one dependent front off the tree's longest
+            // path) it is held to the loosest zero threshold at any width.  1138_bus: 93 ->
+            // 47 levels, 0.614 -> 0.436 ms with the pinned status word (numeric.cpp); 128^3:
+            // 164,027 -> 163,933 supernodes, 19 levels, bench neutral; an unrestricted loose
+            // threshold also merged 128^3's balanced small fronts (147,549 supernodes) and
+            // grew the 8-rank work arena 7.73 -> 8.03 GB
             const bool small_merged = nscol0 + lnz1 <= opt.small_front_max;
+            // ... and on the parent's one longest path (a merge there shortens the tree)
+            const bool deepest = fh[j] + 1 == fh[j + 1] && nmax[j + 1] == 1;
             if (opt.relax_wmax > 0 && nscol0 > opt.relax_wmax && nscol1 > opt.relax_wmax && gkids[j + 1] > 1 &&
                 !small_merged) {
                 // a wide child of a wide parent with siblings stays apart: its coupling goes
@@ -272,7 +293,8 @@ i64 analyze(i64 n, const i64* Ap, const i32* Ai, const sc_options& opt, Symbolic
                     (double)ns * (double)(ns + 1) / 2.0 + (double)ns * (double)(lnz1 - nscol1);
                 const double z = totz / denom;
                 merge = (ns <= opt.nrelax[1] && z < opt.zrelax[0]) ||
-                        (ns <= opt.nrelax[2] && z < opt.zrelax[1]) || (z < opt.zrelax[2]);
+                        (ns <= opt.nrelax[2] && z < opt.zrelax[1]) || (z < opt.zrelax[2]) ||
+                        (small_merged && deepest && z < opt.zrelax[0]);
             }
             if (merge) {
                 zeros[j] = totz;
