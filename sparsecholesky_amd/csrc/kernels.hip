@@ -1341,6 +1341,12 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
 // columns in a 64-column block: the host's segment table (GSeg) lists, per 64 x 64
 // block of the CB, each child's runs and base pointers -- one uniform (scalar) load
 // per child instead of the child-list / plan / bounds lookup chain.
+#ifndef SC_LEAN_OCC0
+#define SC_LEAN_OCC0 5  // workgroups per CU of the lean panel-update instance (6 spilled)
+#endif
+#ifndef SC_EPI_COAL
+#define SC_EPI_COAL 1
+#endif
 template <int BT, int WM, int WN, int BK = 16, int GR = 64>
 __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const int64_t* __restrict__ gblk,
                                                      const GSeg* __restrict__ gseg, int row0, int col0,
@@ -1431,9 +1437,33 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const in
         }
         __syncthreads();
         // the waves whose MFMA rows lie in this chunk (a wave's BT / WM <= 64 rows sit in
-        // one chunk) store C = G - acc (no C read)
+        // one chunk) form C = G - acc (no C read)
         static_assert(GR % (BT / WM) == 0, "a wave's rows lie in one chunk");
-        if ((wr * (BT / WM)) / GR == h) {
+        if (SC_EPI_COAL) {
+            // ... in G (each entry by its one owner lane), then the chunk leaves column by
+            // column: GR consecutive rows of a column per wave-wide store, where the MFMA
+            // layout stores 16 runs of 32 bytes (the counters saw 1.7x the written bytes)
+            if ((wr * (BT / WM)) / GR == h) {
+#pragma unroll
+                for (int a = 0; a < RTM; ++a)
+#pragma unroll
+                    for (int b = 0; b < RTN; ++b)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int lr = wr * (BT / WM) + a * 16 + MFMA_F64_ROW(lane, r);
+                            const int lc = wc * (BT / WN) + b * 16 + (lane & 15);
+                            G[lc * GLD + (lr - h * GR)] -= acc[a][b][r];
+                        }
+            }
+            __syncthreads();
+#pragma unroll 4
+            for (int e = tid; e < BT * GR; e += NT) {
+                const int lr = e % GR, lc = e / GR;
+                const int gi = r0 + lr, gj = col0 + lc;
+                const bool live = gi < T.M && gi >= gj && gj < T.N;
+                buf_st(G[lc * GLD + lr], rc, live ? (int)((gi + (int64_t)(gj - col0) * ldc) * 8) : BUF_DEAD, 0);
+            }
+        } else if ((wr * (BT / WM)) / GR == h) {
 #pragma unroll
             for (int a = 0; a < RTM; ++a)
 #pragma unroll
@@ -1447,6 +1477,62 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const in
                         const double x = G[lc * GLD + (lr - h * GR)] - acc[a][b][r];
                         buf_st(x, rc, live ? (int)((gi + (int64_t)(gj - col0) * ldc) * 8) : BUF_DEAD, 0);
                     }
+        }
+    }
+}
+
+#ifndef SC_RMW_COAL
+#define SC_RMW_COAL 2  // 1: batched-epilogue (EPI = 1) launches, 2: every C read-modify-write launch
+#endif
+// C -= acc through LDS (C read-modify-write launches: panel updates, assembled CBs), in
+// GR-row chunks: the chunk's C loaded column by column (GR consecutive rows per wave-wide
+// load), the owner lanes subtract their MFMA entries in LDS, the chunk stored column by
+// column -- where the MFMA layout reads and writes 16 runs of 32 bytes per instruction.
+template <int BT, int WM, int WN, int BK = 16, int GR = 64>
+__device__ __forceinline__ void syrk_rmw_epilogue(const GemmTask& T, int row0, int col0,
+                                                  double4_t (&acc)[BT / WM / 16][BT / WN / 16], double* smem) {
+    constexpr int NW = WM * WN, NT = 64 * NW;
+    constexpr int RTM = BT / WM / 16, RTN = BT / WN / 16;
+    constexpr int GLD = GR + 1;
+    constexpr int OPS = 2 * 2 * BK * (BT + 16);
+    static_assert(BT * GLD <= OPS, "chunk fits the operand LDS");
+    static_assert(GR % (BT / WM) == 0, "a wave's rows lie in one chunk");
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wr = wid / WN, wc = wid % WN;
+    double* G = smem;
+    const int64_t ldc = T.ldc;
+    const __amdgpu_buffer_rsrc_t rc = buf_rsrc(T.C + (int64_t)col0 * ldc, (uint32_t)(min(BT, T.N - col0) * ldc * 8));
+#pragma unroll 1
+    for (int h = 0; h < BT / GR; ++h) {
+        const int r0 = row0 + h * GR;
+        if (h) __syncthreads();  // the previous chunk's stores have read G
+#pragma unroll 4
+        for (int e = tid; e < BT * GR; e += NT) {
+            const int lr = e % GR, lc = e / GR;
+            const int gi = r0 + lr, gj = col0 + lc;
+            const bool live = gi < T.M && gi >= gj && gj < T.N;
+            G[lc * GLD + lr] = buf_ld(rc, live ? (int)((gi + (int64_t)(gj - col0) * ldc) * 8) : BUF_DEAD, 0);
+        }
+        __syncthreads();
+        if ((wr * (BT / WM)) / GR == h) {
+#pragma unroll
+            for (int a = 0; a < RTM; ++a)
+#pragma unroll
+                for (int b = 0; b < RTN; ++b)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int lr = wr * (BT / WM) + a * 16 + MFMA_F64_ROW(lane, r);
+                        const int lc = wc * (BT / WN) + b * 16 + (lane & 15);
+                        G[lc * GLD + (lr - h * GR)] -= acc[a][b][r];
+                    }
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int e = tid; e < BT * GR; e += NT) {
+            const int lr = e % GR, lc = e / GR;
+            const int gi = r0 + lr, gj = col0 + lc;
+            const bool live = gi < T.M && gi >= gj && gj < T.N;
+            buf_st(G[lc * GLD + lr], rc, live ? (int)((gi + (int64_t)(gj - col0) * ldc) * 8) : BUF_DEAD, 0);
         }
     }
 }
@@ -1666,6 +1752,10 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
             return;
         }
     }
+    if constexpr (SC_RMW_COAL >= 2 || (SC_RMW_COAL == 1 && EPI == 1)) {
+        syrk_rmw_epilogue<BT, WM, WN, BK, LEAN ? 32 : 64>(T, row0, col0, acc, smem);
+        return;
+    }
     // epilogue: f64 16x16x4 C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg.
     // C read-modify-write through a buffer resource over the tile's columns (dead
     // elements -- above the diagonal, past M / N -- masked by range, no branches).
@@ -1712,7 +1802,7 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
 }
 
 template <int BT, int WM, int WN, int TAG, int EPI, int LEAN = 0, int PF = 0>
-__global__ __launch_bounds__(64 * WM * WN, LEAN ? (TAG ? 5 : 6) : 1) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
+__global__ __launch_bounds__(64 * WM * WN, LEAN ? (TAG ? 5 : SC_LEAN_OCC0) : 1) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
                                                                   const int2* __restrict__ tiles,
                                                                   const int64_t* __restrict__ gblk,
                                                                   const GSeg* __restrict__ gseg, int32_t* info) {
