@@ -1341,9 +1341,6 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
 // columns in a 64-column block: the host's segment table (GSeg) lists, per 64 x 64
 // block of the CB, each child's runs and base pointers -- one uniform (scalar) load
 // per child instead of the child-list / plan / bounds lookup chain.
-#ifndef SC_LEAN_OCC0
-#define SC_LEAN_OCC0 5  // workgroups per CU of the lean panel-update instance (6 spilled)
-#endif
 #ifndef SC_EPI_COAL
 #define SC_EPI_COAL 1
 #endif
@@ -1541,21 +1538,15 @@ __device__ __forceinline__ void syrk_rmw_epilogue(const GemmTask& T, int row0, i
 // over k < K (A column-major, ld lda; rows past M (i) / N (j) read as 0).  BK = 16,
 // register-staged double-buffered LDS (As / Bs: 2 stages of BK x (BT + 16) doubles
 // each, +128 B row pad: the two k-rows read by a half-wave hit disjoint banks).
-#ifndef SC_KSKIP
-#define SC_KSKIP 1
-#endif
-#ifndef SC_DSKIP
-#define SC_DSKIP 1
-#endif
-// DIAG (a tile on the diagonal of C, row0 == col0): every epilogue discards the entries
-// above the diagonal, so the MFMAs of this wave's 16 x 16 tiles lying wholly above it are
-// skipped (28 of the 64 of a 128-tile; the live tiles' sums are unchanged, bit for bit).
-// The last K stage is peeled (no prefetch) and skips its 4-deep sub-steps past K (K =
-// 16q + 1 is common: 225, 961, 3969, 8001).  Interleaved at 128^3 (profiles/r06/ab_kloop.txt):
-// 503.8 / 504.5 ms before, 502.7 / 502.5 peeled, 502.4 / 501.6 + the K skip, 501.1 / 501.9
-// + the diagonal skip; the same skips as in-loop branches (513.2), or a whole-wave skip of
-// the dead waves (551), lose: the branches break the K loop's schedule.
-template <int BT, int WM, int WN, int BK = 16, bool DIAG = false>
+// The last K stage is peeled out of the loop (no prefetch, no next-stage stores): 503.8 /
+// 504.5 -> 502.7 / 502.5 ms at 128^3, interleaved (profiles/r06/ab_kloop.txt).  Skipping
+// work there was measured too and dropped: the last stage's sub-steps past K (w = 16q + 1
+// is common) and, on tiles on the diagonal of C, the MFMAs of 16 x 16 tiles above it
+// (discarded by every epilogue) gained 1-2 ms with the old epilogues and nothing with the
+// staged ones (493.7 ms without, 493.4 with the K skip, 494.7 with both), while the tiles'
+// changed timing raised the CB SYRK's L2-miss fetches 34 -> 42 / 59 GB per launch
+// (profiles/r06/ab_kskip.txt); as branches inside the K loop they lost outright (513 ms).
+template <int BT, int WM, int WN, int BK = 16>
 __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t lda, int K, int M, int N, int row0,
                                            int col0, double4_t (&acc)[BT / WM / 16][BT / WN / 16], double* smem) {
     static_assert(BK == 16 || BK == 8, "four-deep k sub-steps of the MFMA");
@@ -1568,8 +1559,6 @@ __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t
     const int lane = tid & 63;
     const int wid = tid >> 6;
     const int wr = wid / WN, wc = wid % WN;
-    // 16-row tile a of this wave vs its 16-column tile b: live iff dq + a - b >= 0
-    const int dq = DIAG ? __builtin_amdgcn_readfirstlane(wr * RTM - wc * RTN) : 0;
     // staging: BK x BT doubles per operand over NT threads
     constexpr int PER = BT * BK / NT;
     // Operands through a per-stage buffer resource (columns k0 .. k0 + BK of A):
@@ -1599,8 +1588,7 @@ __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t
     };
 
     const int nk = (K + BK - 1) / BK;
-    const int krem = K - (nk - 1) * BK;  // live k of the last stage
-    // one K stage; LAST: no prefetch, and its sub-steps past K skipped (SC_KSKIP)
+    // one K stage; LAST: no prefetch of a next stage
     auto stage = [&](int kt, auto last) {
         constexpr bool LAST = decltype(last)::value;
         const int cur = kt & 1;
@@ -1621,14 +1609,12 @@ __device__ __forceinline__ void mfma_kloop(const double* __restrict__ A, int64_t
 #pragma unroll
         for (int kk = 0; kk < BK; kk += 4) {
             const int slot = (kk / 4) & 1;
-            if (LAST && SC_KSKIP && kk >= krem) break;
             if (kk + 4 < BK) lread(kk + 4, slot ^ 1);
 #pragma unroll
             for (int a = 0; a < RTM; ++a)
 #pragma unroll
                 for (int b = 0; b < RTN; ++b)
-                    if (!DIAG || !SC_DSKIP || dq + a - b >= 0)
-                        acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[slot][a], bv[slot][b], acc[a][b], 0, 0, 0);
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[slot][a], bv[slot][b], acc[a][b], 0, 0, 0);
             // the next stage's LDS stores go out under the last sub-step's MFMAs, not
             // between them and the barrier: 547 -> 532 ms at 128^3 (stores after sub-step
             // 1: 535.8; A after 1 and B after 2: 533.0; the loads issued after sub-step 0
@@ -1741,10 +1727,7 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
         for (int b = 0; b < RTN; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
     // (operand stages by LDS-DMA, buffer_load_dwordx4 ... lds per 1-KB k-row, measured
     // slower: 510.5 ms with two 16-deep stages, 521.5 with four 8-deep, vs 505.7-507.3)
-    if (row0 == col0)
-        mfma_kloop<BT, WM, WN, BK, true>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
-    else
-        mfma_kloop<BT, WM, WN, BK>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
+    mfma_kloop<BT, WM, WN, BK>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
 
     if constexpr (TAG == 1) {
         if (T.gs >= 0) {  // the front's CB is not assembled: gather the children's entries
@@ -1802,7 +1785,7 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
 }
 
 template <int BT, int WM, int WN, int TAG, int EPI, int LEAN = 0, int PF = 0>
-__global__ __launch_bounds__(64 * WM * WN, LEAN ? (TAG ? 5 : SC_LEAN_OCC0) : 1) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
+__global__ __launch_bounds__(64 * WM * WN, LEAN ? (TAG ? 5 : 6) : 1) void syrk_mfma_kernel(const GemmTask* __restrict__ tasks,
                                                                   const int2* __restrict__ tiles,
                                                                   const int64_t* __restrict__ gblk,
                                                                   const GSeg* __restrict__ gseg, int32_t* info) {
