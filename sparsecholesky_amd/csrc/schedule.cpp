@@ -172,6 +172,10 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         }
         const bool wide = minN >= 256;
         L.bt = (S.opt.syrk_tile == 128 || (S.opt.syrk_tile == 0 && wide)) ? SYRK_BT_LARGE : SYRK_BT_SMALL;
+        // CB launches of 64 < K <= syrk_lean_kmax (level 7 at 128^3) on the lean 64-tile
+        // instance even when wide: 2.44 -> 2.24 ms (64-tiles up to K = 256 / 512 made levels
+        // 8-10 slower, profiles/r06/ab_cb64.txt)
+        if (kind == L_CB && S.opt.syrk_tile == 0 && maxK > 64 && maxK <= S.opt.syrk_lean_kmax) L.bt = SYRK_BT_SMALL;
         // batched C epilogue on the critical path (main-stream panel updates) and where
         // K is short enough that the epilogue dominates a tile (CB of levels 4-7 at
         // 128^3); deep-K CB updates and the lookahead stream keep the trickle epilogue
