@@ -1341,9 +1341,6 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
 // columns in a 64-column block: the host's segment table (GSeg) lists, per 64 x 64
 // block of the CB, each child's runs and base pointers -- one uniform (scalar) load
 // per child instead of the child-list / plan / bounds lookup chain.
-#ifndef SC_EPI_COAL
-#define SC_EPI_COAL 1
-#endif
 template <int BT, int WM, int WN, int BK = 16, int GR = 64>
 __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const int64_t* __restrict__ gblk,
                                                      const GSeg* __restrict__ gseg, int row0, int col0,
@@ -1436,31 +1433,11 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const in
         // the waves whose MFMA rows lie in this chunk (a wave's BT / WM <= 64 rows sit in
         // one chunk) form C = G - acc (no C read)
         static_assert(GR % (BT / WM) == 0, "a wave's rows lie in one chunk");
-        if (SC_EPI_COAL) {
-            // ... in G (each entry by its one owner lane), then the chunk leaves column by
-            // column: GR consecutive rows of a column per wave-wide store, where the MFMA
-            // layout stores 16 runs of 32 bytes (the counters saw 1.7x the written bytes)
-            if ((wr * (BT / WM)) / GR == h) {
-#pragma unroll
-                for (int a = 0; a < RTM; ++a)
-#pragma unroll
-                    for (int b = 0; b < RTN; ++b)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int lr = wr * (BT / WM) + a * 16 + MFMA_F64_ROW(lane, r);
-                            const int lc = wc * (BT / WN) + b * 16 + (lane & 15);
-                            G[lc * GLD + (lr - h * GR)] -= acc[a][b][r];
-                        }
-            }
-            __syncthreads();
-#pragma unroll 4
-            for (int e = tid; e < BT * GR; e += NT) {
-                const int lr = e % GR, lc = e / GR;
-                const int gi = r0 + lr, gj = col0 + lc;
-                const bool live = gi < T.M && gi >= gj && gj < T.N;
-                buf_st(G[lc * GLD + lr], rc, live ? (int)((gi + (int64_t)(gj - col0) * ldc) * 8) : BUF_DEAD, 0);
-            }
-        } else if ((wr * (BT / WM)) / GR == h) {
+        // ... in G (each entry by its one owner lane), then the chunk leaves column by
+        // column: GR consecutive rows of a column per wave-wide store, where the MFMA
+        // layout stores 16 runs of 32 bytes per instruction (502.7 / 503.5 -> 499.0 /
+        // 499.2 ms at 128^3)
+        if ((wr * (BT / WM)) / GR == h) {
 #pragma unroll
             for (int a = 0; a < RTM; ++a)
 #pragma unroll
@@ -1469,18 +1446,20 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const in
                     for (int r = 0; r < 4; ++r) {
                         const int lr = wr * (BT / WM) + a * 16 + MFMA_F64_ROW(lane, r);
                         const int lc = wc * (BT / WN) + b * 16 + (lane & 15);
-                        const int gi = row0 + lr, gj = col0 + lc;
-                        const bool live = gi < T.M && gi >= gj && gj < T.N;
-                        const double x = G[lc * GLD + (lr - h * GR)] - acc[a][b][r];
-                        buf_st(x, rc, live ? (int)((gi + (int64_t)(gj - col0) * ldc) * 8) : BUF_DEAD, 0);
+                        G[lc * GLD + (lr - h * GR)] -= acc[a][b][r];
                     }
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int e = tid; e < BT * GR; e += NT) {
+            const int lr = e % GR, lc = e / GR;
+            const int gi = r0 + lr, gj = col0 + lc;
+            const bool live = gi < T.M && gi >= gj && gj < T.N;
+            buf_st(G[lc * GLD + lr], rc, live ? (int)((gi + (int64_t)(gj - col0) * ldc) * 8) : BUF_DEAD, 0);
         }
     }
 }
 
-#ifndef SC_RMW_COAL
-#define SC_RMW_COAL 2  // 1: batched-epilogue (EPI = 1) launches, 2: every C read-modify-write launch
-#endif
 // C -= acc through LDS (C read-modify-write launches: panel updates, assembled CBs), in
 // GR-row chunks: the chunk's C loaded column by column (GR consecutive rows per wave-wide
 // load), the owner lanes subtract their MFMA entries in LDS, the chunk stored column by
@@ -1712,10 +1691,7 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
     const int ti = tl.y >> 16, tj = tl.y & 0xffff;
     const int row0 = ti * BT, col0 = tj * BT;
 
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wid = tid >> 6;
-    const int wr = wid / WN, wc = wid % WN;
+    const int wid = threadIdx.x >> 6;
     // static priority for the second-dispatched half of the waves (the arbitration loser
     // on every segment of two co-resident waves per SIMD): 547.8-548.5 -> 544.6-546.0 ms
     if (wid >= WM * WN / 2) __builtin_amdgcn_s_setprio(1);
@@ -1735,53 +1711,7 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
             return;
         }
     }
-    if constexpr (SC_RMW_COAL >= 2 || (SC_RMW_COAL == 1 && EPI == 1)) {
-        syrk_rmw_epilogue<BT, WM, WN, BK, LEAN ? 32 : 64>(T, row0, col0, acc, smem);
-        return;
-    }
-    // epilogue: f64 16x16x4 C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg.
-    // C read-modify-write through a buffer resource over the tile's columns (dead
-    // elements -- above the diagonal, past M / N -- masked by range, no branches).
-    double* __restrict__ C = T.C;
-    const int64_t ldc = T.ldc;
-    const __amdgpu_buffer_rsrc_t rc =
-        buf_rsrc(C + (int64_t)col0 * ldc, (uint32_t)(min(BT, T.N - col0) * ldc * 8));
-    // EPI = 0: element by element; the compiler may not move a C load above an earlier
-    // C store (same buffer), so each element waits one memory round trip -- a trickle
-    // that leaves the co-resident workgroup's MFMAs undisturbed (deep-K CB updates:
-    // 0.2-1.2 ms per level faster this way).  EPI = 1: two MFMA tile rows per chunk,
-    // every load of a chunk in flight before its stores (short-K launches, where the
-    // epilogue is most of a tile's life: 0.4-0.6 ms per level faster).
-    constexpr int EPI_A = EPI ? (RTM < 2 ? RTM : 2) : 1;
-#pragma unroll
-    for (int a0 = 0; a0 < RTM; a0 += EPI_A) {
-        double cv[EPI_A][RTN][4];
-        int offs[EPI_A][RTN][4];
-#pragma unroll
-        for (int a = 0; a < EPI_A; ++a)
-#pragma unroll
-            for (int b = 0; b < RTN; ++b)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int gi = row0 + wr * (BT / WM) + (a0 + a) * 16 + MFMA_F64_ROW(lane, r);
-                    const int gj = col0 + wc * (BT / WN) + b * 16 + (lane & 15);
-                    const bool live = gi < T.M && gi >= gj;
-                    offs[a][b][r] = live ? (int)((gi + (int64_t)(gj - col0) * ldc) * 8) : BUF_DEAD;
-                    if constexpr (EPI) {
-                        cv[a][b][r] = buf_ld(rc, offs[a][b][r], 0);
-                    } else {
-                        buf_st(buf_ld(rc, offs[a][b][r], 0) - acc[a0 + a][b][r], rc, offs[a][b][r], 0);
-                    }
-                }
-        if constexpr (EPI) {
-#pragma unroll
-            for (int a = 0; a < EPI_A; ++a)
-#pragma unroll
-                for (int b = 0; b < RTN; ++b)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) buf_st(cv[a][b][r] - acc[a0 + a][b][r], rc, offs[a][b][r], 0);
-        }
-    }
+    syrk_rmw_epilogue<BT, WM, WN, BK, LEAN ? 32 : 64>(T, row0, col0, acc, smem);
 }
 
 template <int BT, int WM, int WN, int TAG, int EPI, int LEAN = 0, int PF = 0>
@@ -1857,9 +1787,11 @@ hipError_t launch_trsm_panel(const DevPlan& P, const TrsmTask* tasks, int count,
     return hipGetLastError();
 }
 
-// TAG only separates the launches in profiles: 0 = panel update, 1 = CB update.
+// TAG and EPI only separate the launches in profiles: TAG 0 = panel update, 1 = CB update;
+// EPI 1 = the main-stream (critical-path) panel updates and the short-K CB launches, 0 =
+// the lookahead stream and the deep-K CB (round 6: every instance stages its epilogue
+// through LDS; until then EPI chose a batched or a trickled C read-modify-write).
 // bt = 64: 64x64 tiles on 4 waves (2x2); bt = 128: 128x128 tiles on 8 waves (2x4).
-// epi: epilogue with its C loads in flight together (see the kernel).
 template <int TAG, int EPI>
 static void launch_syrk_t(const GemmTask* tasks, const int2* tiles, int n, int bt, hipStream_t st, GatherTab gt,
                           bool lean) {

@@ -167,7 +167,7 @@ struct Launch {
     int32_t maxm;     // small-front LDS edge
     int32_t big;      // CB launch covering fronts with w >= 256
     int32_t bt;       // SYRK tile edge (64 or 128)
-    int32_t epi;      // SYRK epilogue with its C loads batched (short-K and critical-path launches)
+    int32_t epi;      // SYRK instance tag: critical-path panel updates and short-K CB launches (profiles)
     int32_t lean;     // SYRK on 64 x 64 tiles with half the LDS (deepest K <= syrk_lean_kmax)
     int32_t pf;       // panel update carrying pre-factor workgroups (GemmTask.pf; 64 x 64 tiles)
     int32_t strm;     // 0 = main stream, 1 = lookahead stream, 2 = comm stream

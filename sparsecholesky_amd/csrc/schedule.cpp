@@ -176,9 +176,10 @@ int64_t build_schedule(Numeric& N, SchedBuild& B) {
         // instance even when wide: 2.44 -> 2.24 ms (64-tiles up to K = 256 / 512 made levels
         // 8-10 slower, profiles/r06/ab_cb64.txt)
         if (kind == L_CB && S.opt.syrk_tile == 0 && maxK > 64 && maxK <= S.opt.syrk_lean_kmax) L.bt = SYRK_BT_SMALL;
-        // batched C epilogue on the critical path (main-stream panel updates) and where
-        // K is short enough that the epilogue dominates a tile (CB of levels 4-7 at
-        // 128^3); deep-K CB updates and the lookahead stream keep the trickle epilogue
+        // instance tag (profiles): the critical path (main-stream panel updates) and the
+        // short-K CB launches (levels 4-7 at 128^3) apart from the deep-K CB and the
+        // lookahead stream -- the epilogue choice it used to make went with round 6's
+        // staged epilogues (kernels.hip)
         L.epi = (kind == L_PANEL && strm == 0) || (kind == L_CB && maxK < SC_EPI_KMAX);
         // (CB launches with K <= 64 -- levels 4-6 at 128^3 -- are gather-bound and lose
         // more to the lean instance's smaller gather batches than they gain in occupancy)
