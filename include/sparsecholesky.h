@@ -34,7 +34,7 @@ extern "C" {
 #pragma GCC visibility push(default)
 #endif
 
-#define SC_VERSION 120 /* 1.2.0: persistent slab chain options removed; panel_prefactor, dist_local_pieces and SC_ORDER_AMD added; out-of-range lookahead / inner_order / ordering rejected */
+#define SC_VERSION 121 /* 1.2.1: small merged fronts amalgamated past relax_wmax (different supernode partition of some inputs, same L); 1.2.0: persistent slab chain options removed; panel_prefactor, dist_local_pieces and SC_ORDER_AMD added; out-of-range lookahead / inner_order / ordering rejected */
 
 enum sc_status {
     SC_OK = 0,

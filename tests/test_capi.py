@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_version_and_status_strings():
     L = sc.lib()
-    assert L.sc_version() == 120
+    assert L.sc_version() == 121
     assert L.sc_status_string(3) == b"A is not positive definite."
     assert L.sc_status_string(0) == b"ok"
     assert L.sc_status_string(-1) == b"invalid argument"
