@@ -1341,6 +1341,14 @@ __global__ __launch_bounds__(TRSM_ROWS) void trsm_panel_g_kernel(DevPlan P, cons
 // columns in a 64-column block: the host's segment table (GSeg) lists, per 64 x 64
 // block of the CB, each child's runs and base pointers -- one uniform (scalar) load
 // per child instead of the child-list / plan / bounds lookup chain.
+// timing probes of the gathering CB launches (results wrong by construction):
+// SC_PROBE_NOGATHER = 1 leaves the children's entries out, SC_PROBE_NOK = 1 the K loop
+#ifndef SC_PROBE_NOGATHER
+#define SC_PROBE_NOGATHER 0
+#endif
+#ifndef SC_PROBE_NOK
+#define SC_PROBE_NOK 0
+#endif
 template <int BT, int WM, int WN, int BK = 16, int GR = 64>
 __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const int64_t* __restrict__ gblk,
                                                      const GSeg* __restrict__ gseg, int row0, int col0,
@@ -1379,7 +1387,7 @@ __device__ __forceinline__ void syrk_gather_epilogue(const GemmTask& T, const in
         // blocks on or below the diagonal, in the host table's (child) order: each G
         // entry gets its children's adds in child order (deterministic, no atomics)
         const int cb1 = min(min(nb, rb + 1), (col0 + BT) >> 6);
-        for (int cbk = col0 >> 6; r0 < mb && cbk < cb1; ++cbk) {
+        for (int cbk = col0 >> 6; !SC_PROBE_NOGATHER && r0 < mb && cbk < cb1; ++cbk) {
             const int64_t bi = (int64_t)rb * (rb + 1) / 2 + cbk;
             const int64_t p0 = blk[bi], p1 = blk[bi + 1];
             for (int64_t pb = p0; pb < p1; pb += SB) {
@@ -1703,7 +1711,7 @@ __device__ __forceinline__ void syrk_tile_body(const GemmTask* __restrict__ task
         for (int b = 0; b < RTN; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
     // (operand stages by LDS-DMA, buffer_load_dwordx4 ... lds per 1-KB k-row, measured
     // slower: 510.5 ms with two 16-deep stages, 521.5 with four 8-deep, vs 505.7-507.3)
-    mfma_kloop<BT, WM, WN, BK>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
+    if (!(SC_PROBE_NOK && TAG == 1 && T.gs >= 0)) mfma_kloop<BT, WM, WN, BK>(T.A, T.lda, T.K, T.M, T.N, row0, col0, acc, smem);
 
     if constexpr (TAG == 1) {
         if (T.gs >= 0) {  // the front's CB is not assembled: gather the children's entries
